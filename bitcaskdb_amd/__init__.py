@@ -1,0 +1,14 @@
+"""bitcaskdb_amd: MI355X-native WAL record codec for bitcaskDB's compaction / recovery scan.
+
+The product is libbcw.so (C-ABI in include/bcw.h, HIP kernels for gfx950 in csrc/). This package
+is the Python host mirror of the reference interface (wal.py) and its ctypes binding (_lib.py).
+"""
+from . import _lib
+from .wal import (Context, Decoded, ErrCorruptedHintRecord, ErrInvalidData, ErrShortFile, ErrWalMismatchBlockSize,
+                  ErrWalMismatchCRC, ErrWalMismatchMagic, ErrWalUnknownRecordType, HintRecord, Meta, Record,
+                  RefPanic, Wal, WalError, compute_crc32, default_context, iterate_hint, iterate_record, load_wal)
+
+__all__ = ["Context", "Decoded", "ErrCorruptedHintRecord", "ErrInvalidData", "ErrShortFile",
+           "ErrWalMismatchBlockSize", "ErrWalMismatchCRC", "ErrWalMismatchMagic", "ErrWalUnknownRecordType",
+           "HintRecord", "Meta", "Record", "RefPanic", "Wal", "WalError", "compute_crc32", "default_context",
+           "iterate_hint", "iterate_record", "load_wal", "_lib"]

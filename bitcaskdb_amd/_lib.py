@@ -1,0 +1,107 @@
+"""ctypes binding of libbcw.so (include/bcw.h). The HIP extension is mandatory: importing
+this module without the built library raises, there is no CPU fallback on the product path."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbcw.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "bcw.h")
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+
+
+class SuperBlock(C.Structure):
+    _fields_ = [("magic", C.c_uint64), ("block_size", C.c_uint64), ("start_off", C.c_uint32),
+                ("crc", C.c_uint32), ("create_time", C.c_uint64), ("base_time", C.c_uint64)]
+
+
+class DecodeParams(C.Structure):
+    _fields_ = [("seg_len", C.c_uint64), ("base_time", C.c_uint64), ("start_off", C.c_uint32),
+                ("ns_size", C.c_uint32), ("etag_size", C.c_uint32), ("mode", C.c_uint32)]
+
+
+class RecordTable(C.Structure):
+    _fields_ = [("capacity", C.c_uint64), ("foff", u64p), ("size", u64p), ("expire", u64p),
+                ("aux0", u64p), ("aux1", u64p), ("key_len", u32p), ("val_len", u32p), ("meta_len", u32p),
+                ("first_frag", u32p), ("emit_frag", u32p), ("hdr_size", u8p), ("flags", u8p),
+                ("etag_off", u8p), ("status", u8p)]
+
+
+class DecodeResult(C.Structure):
+    _fields_ = [("n_records", C.c_uint64), ("n_records_total", C.c_uint64), ("n_frags", C.c_uint64),
+                ("err_frag", C.c_uint64), ("err_file_off", C.c_uint64), ("err_class", C.c_int32),
+                ("first_bad_record", C.c_int32), ("n_blocks", C.c_uint64), ("retry_frag_capacity", C.c_uint64)]
+
+
+class FragTable(C.Structure):
+    _fields_ = [("capacity", C.c_uint64), ("data_off", u64p), ("len", u32p), ("stored_crc", u32p),
+                ("type", u8p), ("crc_ok", u8p)]
+
+
+# the table's column names, C types and numpy dtypes (one place, used by wal.py and bench.py)
+TABLE_COLUMNS = [("foff", "u8"), ("size", "u8"), ("expire", "u8"), ("aux0", "u8"), ("aux1", "u8"),
+                 ("key_len", "u4"), ("val_len", "u4"), ("meta_len", "u4"), ("first_frag", "u4"),
+                 ("emit_frag", "u4"), ("hdr_size", "u1"), ("flags", "u1"), ("etag_off", "u1"), ("status", "u1")]
+FRAG_COLUMNS = [("data_off", "u8"), ("len", "u4"), ("stored_crc", "u4"), ("type", "u1"), ("crc_ok", "u1")]
+
+# constants mirrored from bcw.h
+BLOCK_SIZE = 32768
+HEADER_SIZE = 7
+SUPER_BLOCK_SIZE = 40
+MODE_RECORD, MODE_HINT = 0, 1
+ST_OK, ST_INVALID, ST_PANIC, ST_UNSUPPORTED = 0, 1, 2, 3
+ERR_NONE, ERR_CRC, ERR_TYPE, ERR_PANIC = 0, 1, 2, 3
+SB_OK, SB_SHORT, SB_CRC, SB_MAGIC, SB_BLOCKSIZE = 0, 1, 2, 3, 4
+E_CAPACITY = -4
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libbcw.so not built ({LIB_PATH}); run __graft_entry__.build() or `make -C bitcaskdb_amd`")
+    lib = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    sig = {
+        "bcw_abi_version": (C.c_int, []),
+        "bcw_strerror": (C.c_char_p, [C.c_int]),
+        "bcw_device_count": (C.c_int, []),
+        "bcw_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "bcw_ctx_destroy": (C.c_int, [vp]),
+        "bcw_ctx_set_stream": (C.c_int, [vp, vp]),
+        "bcw_ctx_stream": (vp, [vp]),
+        "bcw_ctx_sync": (C.c_int, [vp]),
+        "bcw_ctx_device": (C.c_int, [vp]),
+        "bcw_ctx_set_profiling": (C.c_int, [vp, C.c_int]),
+        "bcw_ctx_kernel_times": (C.c_int, [vp, C.POINTER(C.c_double), u64p, C.c_int]),
+        "bcw_kernel_name": (C.c_char_p, [C.c_int]),
+        "bcw_crc32c_masked": (C.c_uint32, [vp, C.c_uint64]),
+        "bcw_load_super_block": (C.c_int, [vp, C.c_uint64, C.POINTER(SuperBlock)]),
+        "bcw_write_super_block": (None, [vp, C.c_uint64, C.c_uint64]),
+        "bcw_max_fragments": (C.c_uint64, [C.c_uint64, C.c_uint32]),
+        "bcw_decode_segment_async": (C.c_int, [vp, vp, C.POINTER(DecodeParams), C.POINTER(RecordTable), vp]),
+        "bcw_decode_segment": (C.c_int, [vp, vp, C.POINTER(DecodeParams), C.POINTER(RecordTable),
+                                         C.POINTER(DecodeResult)]),
+        "bcw_decode_fragments_async": (C.c_int, [vp, C.POINTER(FragTable)]),
+        "bcw_decode_fragments": (C.c_int, [vp, C.POINTER(FragTable), u64p]),
+        "bcw_synth_segment": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                        C.c_int, C.c_uint64, vp, C.c_uint64, u64p, u64p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Every function the C-ABI header declares (used by the symbol-export test)."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(bcw_[a-z0-9_]+)\s*\(", text)))

@@ -1,0 +1,579 @@
+// bcw_api.cpp -- host side of libbcw.so: contexts, constant tables, super block, host WAL writer
+// and the launch orchestration of the decode pipeline (kernels in bcw_decode.hip).
+#include <hip/hip_runtime.h>
+#include <nmmintrin.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "bcw.h"
+#include "bcw_internal.h"
+
+namespace bcw {
+
+// ---- CRC-32C constant tables (reflected polynomial 0x82F63B78, Go crc32.Castagnoli) ----
+static void byte_table(uint32_t* t0) {
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t c = b;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    t0[b] = c;
+  }
+}
+
+void build_slice_tables(uint32_t* t) {
+  byte_table(t);
+  for (int b = 0; b < 256; ++b) t[256 + b] = (t[b] >> 8) ^ t[t[b] & 0xffu];
+}
+
+static inline uint32_t zero_step(const uint32_t* t0, uint32_t s) { return (s >> 8) ^ t0[s & 0xffu]; }
+
+// images of the 32 basis vectors under "advance over n zero bytes"
+static void shift_basis(const uint32_t* t0, uint64_t n, uint32_t* img) {
+  for (int i = 0; i < 32; ++i) {
+    uint32_t v = 1u << i;
+    for (uint64_t k = 0; k < n; ++k) v = zero_step(t0, v);
+    img[i] = v;
+  }
+}
+static inline uint32_t apply_basis(const uint32_t* img, uint32_t x) {
+  uint32_t r = 0;
+  for (int i = 0; x; ++i, x >>= 1)
+    if (x & 1u) r ^= img[i];
+  return r;
+}
+
+// fwd[l][i][n] = F_l(n << 4i), F_l = A_{8*128*(63-l)};  carry[i][n] = A_{8*8192}(n << 4i)
+void build_lane_tables(uint32_t* fwd, uint32_t* carry) {
+  uint32_t t0[256];
+  byte_table(t0);
+  uint32_t step128[32];
+  shift_basis(t0, kWin, step128);
+  uint32_t m[32];
+  for (int i = 0; i < 32; ++i) m[i] = 1u << i;  // identity for lane 63
+  for (int l = 63; l >= 0; --l) {
+    for (int i = 0; i < 8; ++i)
+      for (uint32_t n = 0; n < 16; ++n) fwd[(l * 8 + i) * 16 + n] = apply_basis(m, n << (4 * i));
+    for (int i = 0; i < 32; ++i) m[i] = apply_basis(step128, m[i]);
+  }
+  uint32_t c8k[32];
+  shift_basis(t0, 8192, c8k);
+  for (int i = 0; i < 8; ++i)
+    for (uint32_t n = 0; n < 16; ++n) carry[i * 16 + n] = apply_basis(c8k, n << (4 * i));
+}
+
+// initc[L] = A_{8L}(0xFFFFFFFF): the contribution of the CRC init value after L data bytes
+void build_initc(uint32_t* initc) {
+  uint32_t t0[256];
+  byte_table(t0);
+  uint32_t v = 0xffffffffu;
+  for (uint32_t L = 0; L <= kBlock; ++L) {
+    initc[L] = v;
+    v = zero_step(t0, v);
+  }
+}
+
+// ---- host CRC-32C (SSE4.2) for the writer and bcw_crc32c_masked ----
+static uint32_t crc32c_hw(const uint8_t* p, size_t n) {
+  uint64_t c = 0xffffffffu;
+  while (n >= 8) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    c = _mm_crc32_u64(c, w);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = (uint32_t)c;
+  while (n--) c32 = _mm_crc32_u8(c32, *p++);
+  return ~c32;
+}
+static inline uint32_t mask_crc(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
+
+}  // namespace bcw
+
+using namespace bcw;
+
+struct bcw_ctx {
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t own = nullptr;
+  hipStream_t cur = nullptr;
+  Tables tabs{};
+  Scratch s{};
+  uint64_t frag_hint = 0;  // capacity requested by a retry
+  // sync-API staging
+  uint8_t* d_seg = nullptr;
+  uint64_t d_seg_cap = 0;
+  void* d_tab_mem = nullptr;
+  uint64_t d_tab_cap = 0;
+  bcw_record_table d_tab{};
+  bcw_decode_result* d_result = nullptr;
+  uint32_t last_start_off = 0;
+  uint64_t last_nfrag_cap = 0;
+  Prof prof;
+};
+
+#define HIPCHK(x)                          \
+  do {                                     \
+    if ((x) != hipSuccess) return BCW_E_HIP; \
+  } while (0)
+
+extern "C" {
+
+int bcw_abi_version(void) { return BCW_ABI_VERSION; }
+
+const char* bcw_strerror(int code) {
+  switch (code) {
+    case BCW_OK: return "ok";
+    case BCW_E_INVAL: return "invalid argument";
+    case BCW_E_HIP: return "HIP runtime error";
+    case BCW_E_NOMEM: return "out of memory";
+    case BCW_E_CAPACITY: return "output capacity too small";
+    case BCW_E_NODEVICE: return "no HIP device";
+    default: return "unknown error";
+  }
+}
+
+int bcw_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+uint32_t bcw_crc32c_masked(const uint8_t* p, uint64_t n) { return mask_crc(crc32c_hw(p, (size_t)n)); }
+
+void bcw_write_super_block(uint8_t out[40], uint64_t create_time, uint64_t base_time) {
+  // wal.go:332-360: magic @0, blockSize @8, startOff @16, createTime @20, baseTime @28, crc @36
+  memset(out, 0, 40);
+  const uint64_t magic = BCW_MAGIC, bs = BCW_BLOCK_SIZE;
+  const uint32_t so = BCW_SUPER_BLOCK_SIZE;
+  memcpy(out + 0, &magic, 8);
+  memcpy(out + 8, &bs, 8);
+  memcpy(out + 16, &so, 4);
+  memcpy(out + 20, &create_time, 8);
+  memcpy(out + 28, &base_time, 8);
+  const uint32_t crc = bcw_crc32c_masked(out, 36);
+  memcpy(out + 36, &crc, 4);
+}
+
+int bcw_load_super_block(const uint8_t* p, uint64_t n, bcw_super_block* out) {
+  // wal.go:362-398: CRC first, then magic, then blockSize (startOff is not validated)
+  if (!p || !out) return BCW_E_INVAL;
+  if (n < BCW_SUPER_BLOCK_SIZE) return BCW_SB_SHORT;
+  uint32_t want;
+  memcpy(&want, p + 36, 4);
+  const uint32_t crc = bcw_crc32c_masked(p, 36);
+  if (crc != want) return BCW_SB_CRC;
+  memcpy(&out->magic, p, 8);
+  if (out->magic != BCW_MAGIC) return BCW_SB_MAGIC;
+  memcpy(&out->block_size, p + 8, 8);
+  memcpy(&out->start_off, p + 16, 4);
+  if (out->block_size != BCW_BLOCK_SIZE) return BCW_SB_BLOCKSIZE;
+  memcpy(&out->create_time, p + 20, 8);
+  memcpy(&out->base_time, p + 28, 8);
+  out->crc = crc;
+  return BCW_SB_OK;
+}
+
+uint64_t bcw_max_fragments(uint64_t seg_len, uint32_t start_off) {
+  if (seg_len <= start_off) return 0;
+  return (seg_len - start_off) / BCW_HEADER_SIZE + 1;
+}
+
+int bcw_ctx_create(int device, bcw_ctx** out) {
+  if (!out) return BCW_E_INVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return BCW_E_NODEVICE;
+  if (device < 0 || device >= n) return BCW_E_INVAL;
+  bcw_ctx* c = new (std::nothrow) bcw_ctx();
+  if (!c) return BCW_E_NOMEM;
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) { delete c; return BCW_E_HIP; }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return BCW_E_HIP; }
+  c->cur = c->own;
+  std::vector<uint32_t> slice(512), fwd(64 * 128), carry(128), initc(kBlock + 1);
+  build_slice_tables(slice.data());
+  build_lane_tables(fwd.data(), carry.data());
+  build_initc(initc.data());
+  bool ok = hipMalloc(&c->tabs.slice, slice.size() * 4) == hipSuccess &&
+            hipMalloc(&c->tabs.fwd, fwd.size() * 4) == hipSuccess &&
+            hipMalloc(&c->tabs.carry, carry.size() * 4) == hipSuccess &&
+            hipMalloc(&c->tabs.initc, initc.size() * 4) == hipSuccess &&
+            hipMalloc(&c->d_result, sizeof(bcw_decode_result)) == hipSuccess;
+  ok = ok && hipMemcpy(c->tabs.slice, slice.data(), slice.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(c->tabs.fwd, fwd.data(), fwd.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(c->tabs.carry, carry.data(), carry.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(c->tabs.initc, initc.data(), initc.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+  if (!ok) { bcw_ctx_destroy(c); return BCW_E_NOMEM; }
+  *out = c;
+  return BCW_OK;
+}
+
+static void free_scratch(Scratch& s) {
+  (void)hipFree(s.nfrag);
+  (void)hipFree(s.fbase);
+  (void)hipFree(s.frags);
+  (void)hipFree(s.sums);
+  (void)hipFree(s.ins);
+  (void)hipFree(s.misc);
+  s = Scratch{};
+}
+
+int bcw_ctx_destroy(bcw_ctx* c) {
+  if (!c) return BCW_E_INVAL;
+  (void)hipSetDevice(c->device);
+  if (c->cur) (void)hipStreamSynchronize(c->cur);
+  free_scratch(c->s);
+  (void)hipFree(c->tabs.slice);
+  (void)hipFree(c->tabs.fwd);
+  (void)hipFree(c->tabs.carry);
+  (void)hipFree(c->tabs.initc);
+  (void)hipFree(c->d_seg);
+  (void)hipFree(c->d_tab_mem);
+  (void)hipFree(c->d_result);
+  for (auto& m : c->prof.marks) { (void)hipEventDestroy(m.a); (void)hipEventDestroy(m.b); }
+  for (auto e : c->prof.pool) (void)hipEventDestroy(e);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+  return BCW_OK;
+}
+
+int bcw_ctx_set_stream(bcw_ctx* c, void* stream) {
+  if (!c) return BCW_E_INVAL;
+  c->cur = stream ? (hipStream_t)stream : c->own;
+  return BCW_OK;
+}
+void* bcw_ctx_stream(bcw_ctx* c) { return c ? (void*)c->cur : nullptr; }
+int bcw_ctx_device(bcw_ctx* c) { return c ? c->device : -1; }
+int bcw_ctx_sync(bcw_ctx* c) {
+  if (!c) return BCW_E_INVAL;
+  return hipStreamSynchronize(c->cur) == hipSuccess ? BCW_OK : BCW_E_HIP;
+}
+
+static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
+  Scratch& s = c->s;
+  if (nblocks <= s.nblocks_cap && frag_cap <= s.frag_cap && s.misc) return BCW_OK;
+  (void)hipStreamSynchronize(c->cur);
+  const uint64_t nb = std::max(nblocks, s.nblocks_cap);
+  const uint64_t fc = std::max(frag_cap, s.frag_cap);
+  free_scratch(s);
+  bool ok = hipMalloc(&s.nfrag, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess &&
+            hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
+            hipMalloc(&s.sums, (nb + 1) * sizeof(BlockSum)) == hipSuccess &&
+            hipMalloc(&s.ins, (nb + 1) * sizeof(BlockIn)) == hipSuccess &&
+            hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess;
+  if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
+  s.nblocks_cap = nb;
+  s.frag_cap = fc;
+  return BCW_OK;
+}
+
+int bcw_decode_segment_async(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_params* p,
+                             const bcw_record_table* t, bcw_decode_result* d_result) {
+  if (!c || !p || !t || !d_result) return BCW_E_INVAL;
+  if (p->mode != BCW_MODE_RECORD && p->mode != BCW_MODE_HINT) return BCW_E_INVAL;
+  if (!t->foff || !t->size || !t->expire || !t->key_len || !t->val_len || !t->meta_len || !t->first_frag ||
+      !t->emit_frag || !t->hdr_size || !t->flags || !t->etag_off || !t->status)
+    return BCW_E_INVAL;
+  if (p->mode == BCW_MODE_HINT && (!t->aux0 || !t->aux1)) return BCW_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  c->last_start_off = p->start_off;
+  bcw_decode_result r{};
+  r.err_frag = ~0ull;
+  r.first_bad_record = -1;
+  if ((uint64_t)p->start_off > p->seg_len) {
+    // wal_iterator.go:49,55: bufSize < 0 -> i.buf[:bufSize] panics before any fragment
+    r.err_class = BCW_ERR_PANIC;
+    HIPCHK(hipMemcpyAsync(d_result, &r, sizeof r, hipMemcpyHostToDevice, c->cur));
+    return BCW_OK;
+  }
+  const uint64_t nblocks = (p->seg_len - p->start_off + kBlock - 1) / kBlock;
+  if (nblocks == 0 || !d_seg) {
+    if (nblocks != 0) return BCW_E_INVAL;
+    HIPCHK(hipMemcpyAsync(d_result, &r, sizeof r, hipMemcpyHostToDevice, c->cur));
+    return BCW_OK;
+  }
+  if (bcw_max_fragments(p->seg_len, p->start_off) >= 0xfffffff0ull) return BCW_E_INVAL;  // u32 fragment ids
+  uint64_t want = std::max<uint64_t>(65536, (p->seg_len - p->start_off) / 256 + nblocks * 2);
+  want = std::max(want, c->frag_hint);
+  want = std::min(want, bcw_max_fragments(p->seg_len, p->start_off) + 64);
+  int rc = ensure_scratch(c, nblocks, want);
+  if (rc != BCW_OK) return rc;
+  if (launch_decode(d_seg, *p, *t, d_result, c->tabs, c->s, nblocks, c->cur, c->num_cus, &c->prof) != hipSuccess)
+    return BCW_E_HIP;
+  return BCW_OK;
+}
+
+int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
+  if (!c || !d_frags) return BCW_E_INVAL;
+  if (!c->s.misc) return BCW_OK;
+  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  const uint64_t n = std::min(c->s.frag_cap, d_frags->capacity);
+  return launch_export_frags(c->s, *d_frags, c->last_start_off, c->cur, n) == hipSuccess ? BCW_OK : BCW_E_HIP;
+}
+
+static const char* kKernelNames[K_NUM] = {"k_chase_count", "k_scan_u32", "k_chase_write", "k_crc",
+                                          "k_blocksum", "k_blockscan", "k_records", "k_finalize"};
+
+int bcw_ctx_set_profiling(bcw_ctx* c, int on) {
+  if (!c) return BCW_E_INVAL;
+  c->prof.on = on != 0;
+  return BCW_OK;
+}
+
+int bcw_ctx_kernel_times(bcw_ctx* c, double* total_ms, uint64_t* launches, int n) {
+  if (!c || n < 0) return BCW_E_INVAL;
+  if (hipStreamSynchronize(c->cur) != hipSuccess) return BCW_E_HIP;
+  for (int k = 0; k < n; ++k) { if (total_ms) total_ms[k] = 0; if (launches) launches[k] = 0; }
+  for (const auto& m : c->prof.marks) {
+    float ms = 0;
+    if (m.kid < n && hipEventElapsedTime(&ms, m.a, m.b) == hipSuccess) {
+      if (total_ms) total_ms[m.kid] += ms;
+      if (launches) launches[m.kid] += 1;
+    }
+    c->prof.pool.push_back(m.a);
+    c->prof.pool.push_back(m.b);
+  }
+  c->prof.marks.clear();
+  return K_NUM;
+}
+
+const char* bcw_kernel_name(int kid) { return (kid >= 0 && kid < K_NUM) ? kKernelNames[kid] : nullptr; }
+
+int bcw_decode_fragments(bcw_ctx* c, const bcw_frag_table* h, uint64_t* n_total) {
+  if (!c || !h) return BCW_E_INVAL;
+  if (n_total) *n_total = 0;
+  if (!c->s.misc) return BCW_OK;
+  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  uint64_t misc[16];
+  HIPCHK(hipMemcpyAsync(misc, c->s.misc, sizeof misc, hipMemcpyDeviceToHost, c->cur));
+  HIPCHK(hipStreamSynchronize(c->cur));
+  const uint64_t total = std::min(misc[4], c->s.frag_cap);
+  if (n_total) *n_total = total;
+  const uint64_t n = std::min(total, h->capacity);
+  if (n == 0) return BCW_OK;
+  void* mem = nullptr;
+  if (hipMalloc(&mem, n * 19) != hipSuccess) return BCW_E_NOMEM;
+  uint8_t* m = (uint8_t*)mem;
+  bcw_frag_table d;
+  d.capacity = n;
+  d.data_off = (uint64_t*)m; m += n * 8;
+  d.len = (uint32_t*)m; m += n * 4;
+  d.stored_crc = (uint32_t*)m; m += n * 4;
+  d.type = m; m += n;
+  d.crc_ok = m;
+  bool ok = launch_export_frags(c->s, d, c->last_start_off, c->cur, n) == hipSuccess;
+  auto cp = [&](void* dst, const void* src, size_t esz) {
+    return !dst || hipMemcpyAsync(dst, src, n * esz, hipMemcpyDeviceToHost, c->cur) == hipSuccess;
+  };
+  ok = ok && cp(h->data_off, d.data_off, 8) && cp(h->len, d.len, 4) && cp(h->stored_crc, d.stored_crc, 4) &&
+       cp(h->type, d.type, 1) && cp(h->crc_ok, d.crc_ok, 1);
+  ok = ok && hipStreamSynchronize(c->cur) == hipSuccess;
+  (void)hipFree(mem);
+  return ok ? BCW_OK : BCW_E_HIP;
+}
+
+static int ensure_dev_table(bcw_ctx* c, uint64_t cap, bool hint) {
+  if (cap <= c->d_tab_cap && c->d_tab_mem) return BCW_OK;
+  (void)hipStreamSynchronize(c->cur);
+  (void)hipFree(c->d_tab_mem);
+  c->d_tab_mem = nullptr;
+  const uint64_t n = std::max<uint64_t>(cap, 1);
+  const size_t bytes = n * (8 * 5 + 4 * 5 + 4);
+  if (hipMalloc(&c->d_tab_mem, bytes) != hipSuccess) { c->d_tab_cap = 0; return BCW_E_NOMEM; }
+  uint8_t* m = (uint8_t*)c->d_tab_mem;
+  bcw_record_table& t = c->d_tab;
+  t.capacity = n;
+  t.foff = (uint64_t*)m; m += n * 8;
+  t.size = (uint64_t*)m; m += n * 8;
+  t.expire = (uint64_t*)m; m += n * 8;
+  t.aux0 = (uint64_t*)m; m += n * 8;
+  t.aux1 = (uint64_t*)m; m += n * 8;
+  t.key_len = (uint32_t*)m; m += n * 4;
+  t.val_len = (uint32_t*)m; m += n * 4;
+  t.meta_len = (uint32_t*)m; m += n * 4;
+  t.first_frag = (uint32_t*)m; m += n * 4;
+  t.emit_frag = (uint32_t*)m; m += n * 4;
+  t.hdr_size = m; m += n;
+  t.flags = m; m += n;
+  t.etag_off = m; m += n;
+  t.status = m;
+  c->d_tab_cap = n;
+  (void)hint;
+  return BCW_OK;
+}
+
+int bcw_decode_segment(bcw_ctx* c, const uint8_t* h_seg, const bcw_decode_params* p,
+                       const bcw_record_table* h, bcw_decode_result* h_result) {
+  if (!c || !p || !h || !h_result) return BCW_E_INVAL;
+  if (p->seg_len && !h_seg) return BCW_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  if (p->seg_len > c->d_seg_cap) {
+    (void)hipStreamSynchronize(c->cur);
+    (void)hipFree(c->d_seg);
+    c->d_seg = nullptr;
+    c->d_seg_cap = 0;
+    if (hipMalloc(&c->d_seg, p->seg_len) != hipSuccess) return BCW_E_NOMEM;
+    c->d_seg_cap = p->seg_len;
+  }
+  if (p->seg_len) HIPCHK(hipMemcpyAsync(c->d_seg, h_seg, p->seg_len, hipMemcpyHostToDevice, c->cur));
+  int rc = ensure_dev_table(c, h->capacity, p->mode == BCW_MODE_HINT);
+  if (rc != BCW_OK) return rc;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    rc = bcw_decode_segment_async(c, c->d_seg, p, &c->d_tab, c->d_result);
+    if (rc != BCW_OK) return rc;
+    HIPCHK(hipMemcpyAsync(h_result, c->d_result, sizeof *h_result, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(hipStreamSynchronize(c->cur));
+    if (!h_result->retry_frag_capacity) break;
+    c->frag_hint = h_result->retry_frag_capacity + 64;
+  }
+  if (h_result->retry_frag_capacity) return BCW_E_NOMEM;
+  const uint64_t n = std::min(h_result->n_records, h->capacity);
+  const bcw_record_table& d = c->d_tab;
+  auto cp = [&](void* dst, const void* src, size_t esz) -> bool {
+    if (!dst || n == 0) return true;
+    return hipMemcpyAsync(dst, src, n * esz, hipMemcpyDeviceToHost, c->cur) == hipSuccess;
+  };
+  bool ok = cp(h->foff, d.foff, 8) && cp(h->size, d.size, 8) && cp(h->expire, d.expire, 8) &&
+            cp(h->aux0, d.aux0, 8) && cp(h->aux1, d.aux1, 8) && cp(h->key_len, d.key_len, 4) &&
+            cp(h->val_len, d.val_len, 4) && cp(h->meta_len, d.meta_len, 4) && cp(h->first_frag, d.first_frag, 4) &&
+            cp(h->emit_frag, d.emit_frag, 4) && cp(h->hdr_size, d.hdr_size, 1) && cp(h->flags, d.flags, 1) &&
+            cp(h->etag_off, d.etag_off, 1) && cp(h->status, d.status, 1);
+  if (!ok) return BCW_E_HIP;
+  HIPCHK(hipStreamSynchronize(c->cur));
+  return h_result->n_records > h->capacity ? BCW_E_CAPACITY : BCW_OK;
+}
+
+// ---- host WAL writer: Record.Encode (record.go:57-138) at synthetic shapes + WriteRecord ----
+namespace {
+struct Writer {
+  uint8_t* out;
+  uint64_t cap;
+  uint64_t len;
+  void put(const void* p, uint64_t n) {
+    if (out && len + n <= cap) memcpy(out + len, p, n);
+    len += n;
+  }
+  // wal.go:490-553 (writeOffset(true) = len - 40); returns the record offset
+  uint64_t write_record(const uint8_t* rec, uint64_t n, bool compute_crc) {
+    static const uint8_t pad[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t offset = 0, left = n;
+    bool begin = true;
+    while (left > 0) {
+      uint64_t leftover = BCW_BLOCK_SIZE - ((len - BCW_SUPER_BLOCK_SIZE) % BCW_BLOCK_SIZE);
+      if (leftover < BCW_HEADER_SIZE) {
+        put(pad, leftover);
+        leftover = BCW_BLOCK_SIZE;
+      }
+      if (begin) offset = len;
+      const uint64_t avail = leftover - BCW_HEADER_SIZE;
+      const uint64_t frag = std::min(left, avail);
+      const bool end = left == frag;
+      const uint8_t type = (begin && end) ? BCW_RECORD_FULL : begin ? BCW_RECORD_FIRST : end ? BCW_RECORD_LAST
+                                                                                          : BCW_RECORD_MIDDLE;
+      uint8_t hdr[7];
+      const uint32_t crc = compute_crc ? mask_crc(crc32c_hw(rec, frag)) : 0;
+      const uint16_t l16 = (uint16_t)frag;
+      memcpy(hdr, &crc, 4);
+      memcpy(hdr + 4, &l16, 2);
+      hdr[6] = type;
+      put(hdr, 7);
+      put(rec, frag);
+      rec += frag;
+      left -= frag;
+      begin = false;
+    }
+    return offset;
+  }
+};
+
+inline uint64_t splitmix64(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+inline void fill_rand(uint64_t& s, uint8_t* p, size_t n) {
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    const uint64_t v = splitmix64(s);
+    memcpy(p + i, &v, 8);
+  }
+  if (i < n) {
+    const uint64_t v = splitmix64(s);
+    memcpy(p + i, &v, n - i);
+  }
+}
+inline int put_uvarint(uint8_t* o, uint64_t v) {
+  int i = 0;
+  while (v >= 0x80) { o[i++] = (uint8_t)(v | 0x80); v >>= 7; }
+  o[i++] = (uint8_t)v;
+  return i;
+}
+}  // namespace
+
+int bcw_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_t seed, uint32_t ns_size,
+                      uint32_t key_len, uint32_t value_len, int value_mode, uint64_t base_time, uint8_t* h_out,
+                      uint64_t out_cap, uint64_t* out_len, uint64_t* out_records) {
+  if (value_mode != 0 && value_mode != 1) return BCW_E_INVAL;
+  if (ns_size > 255 || key_len > (1u << 20) || value_len > (1u << 26)) return BCW_E_INVAL;
+  Writer w{h_out, out_cap, 0};
+  uint8_t sb[40];
+  bcw_write_super_block(sb, base_time, base_time);
+  w.put(sb, 40);
+  std::vector<double> cdf;
+  if (value_mode == 1) {
+    cdf.resize(512);
+    double acc = 0;
+    for (int k = 1; k <= 512; ++k) { acc += std::pow((double)k, -1.1); cdf[k - 1] = acc; }
+    for (auto& x : cdf) x /= acc;
+  }
+  const size_t vmax = value_mode == 1 ? 128 * 512 : value_len;
+  std::vector<uint8_t> key(key_len + 8), val(vmax + 8), rec(vmax + key_len + ns_size + 64);
+  std::vector<uint8_t> ns(ns_size);
+  for (uint32_t i = 0; i < ns_size; ++i) ns[i] = (uint8_t)('A' + i % 26);
+  uint64_t s = seed, n = 0;
+  const bool fill = h_out != nullptr;
+  for (uint64_t i = 0; (max_records == 0 || i < max_records) && w.len < target_bytes; ++i) {
+    size_t vl = value_len;
+    if (value_mode == 1) {
+      const double u = (double)(splitmix64(s) >> 11) * (1.0 / 9007199254740992.0);
+      vl = 128u * (size_t)(std::lower_bound(cdf.begin(), cdf.end(), u) - cdf.begin() + 1);
+    }
+    if (fill) {
+      fill_rand(s, key.data(), key_len);
+      if (key_len >= 8) memcpy(key.data(), &i, 8);
+      fill_rand(s, val.data(), vl);
+    } else {
+      s += 0x9E3779B97F4A7C15ull * (uint64_t)(((key_len + 7) / 8) + ((vl + 7) / 8));
+    }
+    // Record.Encode with no etag, no expire, no meta (record.go:57-138)
+    uint8_t tmp[30];
+    int t = 0;
+    t += put_uvarint(tmp + t, key_len);
+    t += put_uvarint(tmp + t, vl);
+    t += put_uvarint(tmp + t, 0);
+    const size_t header = (size_t)t + ns_size + 2;
+    size_t o = 0;
+    rec[o++] = (uint8_t)header;
+    memcpy(rec.data() + o, ns.data(), ns_size); o += ns_size;
+    rec[o++] = (uint8_t)((1u << 0) | (1u << 1));  // noEtag | noExpire
+    memcpy(rec.data() + o, tmp, t); o += t;
+    memcpy(rec.data() + o, key.data(), key_len); o += key_len;
+    memcpy(rec.data() + o, val.data(), vl); o += vl;
+    w.write_record(rec.data(), o, fill);
+    ++n;
+  }
+  if (out_len) *out_len = w.len;
+  if (out_records) *out_records = n;
+  if (h_out && w.len > out_cap) return BCW_E_CAPACITY;
+  return BCW_OK;
+}
+
+}  // extern "C"

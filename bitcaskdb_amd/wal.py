@@ -1,0 +1,325 @@
+"""Host-side mirror of the reference's WAL decode interface, backed by the MI355X codec.
+
+Names, argument meaning and error behaviour follow wenzhang-dev/bitcaskDB:
+  load_wal            LoadWal / loadSuperBlock            wal.go:218-259, 362-398
+  iterate_record      IterateRecord                       record.go:242-266
+  iterate_hint        IterateHint                         hint.go:163-188
+  compute_crc32       ComputeCRC32                        utils.go:24-29
+Every record comes out of the GPU decode (libbcw.so); the callback replay below reproduces the
+reference's sequential error semantics (records before the first failure are delivered, then
+the first error is returned/raised).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+
+# ---- Go sentinel errors (wal.go:15-26, hint.go:22, record.go:74,147,193) ----
+class WalError(Exception):
+    pass
+
+
+class ErrWalMismatchCRC(WalError):
+    def __init__(self, msg="CRC mismatch, corrupted data"):
+        super().__init__(msg)
+
+
+class ErrWalUnknownRecordType(WalError):
+    def __init__(self, msg="invalid record type"):
+        super().__init__(msg)
+
+
+class ErrWalMismatchMagic(WalError):
+    def __init__(self, msg="magic number mismatch"):
+        super().__init__(msg)
+
+
+class ErrWalMismatchBlockSize(WalError):
+    def __init__(self, msg="block size mismatch"):
+        super().__init__(msg)
+
+
+class ErrInvalidData(WalError):
+    def __init__(self, msg="invalid data"):
+        super().__init__(msg)
+
+
+class ErrCorruptedHintRecord(WalError):
+    def __init__(self, msg="corrupted hint record"):
+        super().__init__(msg)
+
+
+class RefPanic(WalError):
+    """The Go reference panics on these bytes (slice bounds out of range)."""
+
+
+class ErrShortFile(WalError):
+    def __init__(self, msg="EOF"):
+        super().__init__(msg)
+
+
+def compute_crc32(data: bytes) -> int:
+    """ComputeCRC32 (utils.go:24-29): masked CRC-32C."""
+    buf = (C.c_uint8 * len(data)).from_buffer_copy(data) if data else None
+    return int(L.lib.bcw_crc32c_masked(buf, len(data)))
+
+
+# ---- context ----
+class Context:
+    """One HIP stream + device tables on one GPU (bcw_ctx)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        rc = L.lib.bcw_ctx_create(device, C.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"bcw_ctx_create({device}) failed: {L.lib.bcw_strerror(rc).decode()}")
+        self._h = h
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            L.lib.bcw_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int | None):
+        L.lib.bcw_ctx_set_stream(self._h, C.c_void_p(stream_ptr or 0))
+
+    def sync(self):
+        rc = L.lib.bcw_ctx_sync(self._h)
+        if rc != 0:
+            raise RuntimeError(L.lib.bcw_strerror(rc).decode())
+
+    # synchronous host-in/host-out decode
+    def decode(self, seg, start_off: int, base_time: int, ns_size: int, etag_size: int,
+               mode: int = L.MODE_RECORD, capacity: int | None = None, with_frags: bool = False):
+        seg = np.frombuffer(seg, dtype=np.uint8) if not isinstance(seg, np.ndarray) else seg
+        seg = np.ascontiguousarray(seg, dtype=np.uint8)
+        n = int(seg.size)
+        p = L.DecodeParams(n, base_time, start_off, ns_size, etag_size, mode)
+        cap = capacity if capacity is not None else max(16, n // 64)
+        while True:
+            cols = {name: np.zeros(max(cap, 1), dtype=dt) for name, dt in L.TABLE_COLUMNS}
+            tab = L.RecordTable(cap, *[cols[name].ctypes.data_as(getattr(L, "u8p" if dt == "u1" else
+                                                                         ("u32p" if dt == "u4" else "u64p")))
+                                       for name, dt in L.TABLE_COLUMNS])
+            res = L.DecodeResult()
+            rc = L.lib.bcw_decode_segment(self._h, seg.ctypes.data_as(C.c_void_p) if n else None, C.byref(p),
+                                          C.byref(tab), C.byref(res))
+            if rc == L.E_CAPACITY:
+                cap = int(res.n_records) + 16
+                continue
+            if rc != 0:
+                raise RuntimeError(f"bcw_decode_segment: {L.lib.bcw_strerror(rc).decode()}")
+            break
+        nr = int(res.n_records)
+        out = Decoded(result=res, table={k: v[:nr].copy() for k, v in cols.items()}, seg=seg, mode=mode,
+                      ns_size=ns_size, etag_size=etag_size)
+        if with_frags:
+            out.frags = self.fragments(max(int(res.n_frags), 1))
+        return out
+
+    def fragments(self, capacity: int):
+        cols = {name: np.zeros(max(capacity, 1), dtype=dt) for name, dt in L.FRAG_COLUMNS}
+        ft = L.FragTable(capacity, cols["data_off"].ctypes.data_as(L.u64p), cols["len"].ctypes.data_as(L.u32p),
+                         cols["stored_crc"].ctypes.data_as(L.u32p), cols["type"].ctypes.data_as(L.u8p),
+                         cols["crc_ok"].ctypes.data_as(L.u8p))
+        total = C.c_uint64(0)
+        rc = L.lib.bcw_decode_fragments(self._h, C.byref(ft), C.byref(total))
+        if rc != 0:
+            raise RuntimeError(f"bcw_decode_fragments: {L.lib.bcw_strerror(rc).decode()}")
+        t = int(total.value)
+        if t > capacity:
+            return self.fragments(t)
+        return {k: v[:t].copy() for k, v in cols.items()}
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+@dataclass
+class Decoded:
+    result: L.DecodeResult
+    table: dict
+    seg: np.ndarray
+    mode: int
+    ns_size: int
+    etag_size: int
+    frags: dict | None = None
+
+    @property
+    def n_records(self) -> int:
+        return int(self.result.n_records)
+
+    def record_bytes(self, r: int) -> bytes:
+        """Payload of row r: the data of fragments [first_frag, emit_frag] (needs with_frags)."""
+        if self.frags is None:
+            raise ValueError("decode(..., with_frags=True) is needed to gather record bytes")
+        t, fr = self.table, self.frags
+        f0, f1 = int(t["first_frag"][r]), int(t["emit_frag"][r])
+        parts = [bytes(self.seg[int(fr["data_off"][g]):int(fr["data_off"][g]) + int(fr["len"][g])])
+                 for g in range(f0, f1 + 1)]
+        out = b"".join(parts)
+        if len(out) != int(t["size"][r]):
+            raise AssertionError(f"record {r}: gathered {len(out)} bytes, table says {int(t['size'][r])}")
+        return out
+
+
+# ---- Wal (read side) ----
+@dataclass
+class Wal:
+    data: np.ndarray
+    fid: int = 0
+    start_off: int = 40
+    base_time: int = 0
+    create_time: int = 0
+    path: str | None = None
+
+    def size(self) -> int:
+        return int(self.data.size)
+
+    def BaseTime(self) -> int:  # noqa: N802 (reference spelling)
+        return self.base_time
+
+
+def load_wal(src, fid: int = 0) -> Wal:
+    """LoadWal (wal.go:218-259): read the file, validate the super block (CRC, magic, blockSize)."""
+    path = None
+    if isinstance(src, (str, os.PathLike)):
+        path = os.fspath(src)
+        with open(path, "rb") as fh:
+            raw = fh.read()
+    else:
+        raw = bytes(src)
+    sb = L.SuperBlock()
+    buf = (C.c_uint8 * max(len(raw), 1)).from_buffer_copy(raw if raw else b"\0")
+    rc = L.lib.bcw_load_super_block(buf, len(raw), C.byref(sb))
+    if rc == L.SB_SHORT:
+        raise ErrShortFile()
+    if rc == L.SB_CRC:
+        raise ErrWalMismatchCRC()
+    if rc == L.SB_MAGIC:
+        raise ErrWalMismatchMagic()
+    if rc == L.SB_BLOCKSIZE:
+        raise ErrWalMismatchBlockSize()
+    return Wal(np.frombuffer(raw, dtype=np.uint8), fid, int(sb.start_off), int(sb.base_time),
+               int(sb.create_time), path)
+
+
+# ---- records ----
+@dataclass
+class Meta:
+    expire: int = 0
+    etag: bytes | None = None
+    flags: int = 0
+    app_meta: bytes = b""  # msgpack bytes, opaque (msgpack parity unpinned)
+
+    def is_tombstone(self) -> bool:
+        return bool(self.flags & 1)
+
+
+@dataclass
+class Record:
+    ns: bytes
+    key: bytes
+    value: bytes
+    meta: Meta = field(default_factory=Meta)
+
+
+@dataclass
+class HintRecord:
+    ns: bytes
+    key: bytes
+    fid: int
+    off: int
+    size: int
+
+
+def _frag_error(res):
+    if res.err_class == L.ERR_CRC:
+        return ErrWalMismatchCRC()
+    if res.err_class == L.ERR_TYPE:
+        return ErrWalUnknownRecordType()
+    if res.err_class == L.ERR_PANIC:
+        return RefPanic("slice bounds out of range (startOff beyond file size)")
+    return None
+
+
+def _record_of(dec: Decoded, r: int, payload: bytes) -> Record:
+    t = dec.table
+    flags = int(t["flags"][r])
+    o = int(t["etag_off"][r])
+    etag_len = 0 if flags & 1 else dec.etag_size
+    hdr = int(t["hdr_size"][r])
+    kl, vl, ml = int(t["key_len"][r]), int(t["val_len"][r]), int(t["meta_len"][r])
+    key = payload[hdr:hdr + kl]
+    value = payload[hdr + kl:hdr + kl + vl]
+    meta = payload[hdr + kl + vl:hdr + kl + vl + ml]
+    return Record(ns=payload[1:1 + dec.ns_size], key=key, value=value,
+                  meta=Meta(expire=int(t["expire"][r]), etag=payload[o:o + etag_len],
+                            flags=1 if flags & 4 else 0, app_meta=meta))
+
+
+def iterate_record(wal: Wal, cb, ns_size: int = 20, etag_size: int = 20, ctx: Context | None = None):
+    """IterateRecord (record.go:242-266): cb(record, foff, size) per record; raises the first error."""
+    ctx = ctx or default_context()
+    dec = ctx.decode(wal.data, wal.start_off, wal.base_time, ns_size, etag_size, L.MODE_RECORD, with_frags=True)
+    for r in range(dec.n_records):
+        st = int(dec.table["status"][r])
+        if st == L.ST_INVALID:
+            raise ErrInvalidData()
+        if st == L.ST_PANIC:
+            raise RefPanic("slice bounds out of range")
+        if st == L.ST_UNSUPPORTED:
+            raise WalError("record length >= 2^32 is not supported by the device table")
+        payload = dec.record_bytes(r)
+        ret = cb(_record_of(dec, r, payload), int(dec.table["foff"][r]), int(dec.table["size"][r]))
+        if ret is not None:
+            raise ret if isinstance(ret, BaseException) else WalError(str(ret))
+    err = _frag_error(dec.result)
+    if err is not None:
+        raise err
+
+
+def iterate_hint(hint: Wal, cb, ns_size: int = 20, ctx: Context | None = None):
+    """IterateHint (hint.go:163-188): cb(HintRecord) per record; raises the first error."""
+    ctx = ctx or default_context()
+    dec = ctx.decode(hint.data, hint.start_off, hint.base_time, ns_size, 0, L.MODE_HINT, with_frags=True)
+    for r in range(dec.n_records):
+        st = int(dec.table["status"][r])
+        if st == L.ST_INVALID:
+            raise ErrCorruptedHintRecord()
+        if st == L.ST_PANIC:
+            raise RefPanic("slice bounds out of range")
+        payload = dec.record_bytes(r)
+        ko, kl = int(dec.table["hdr_size"][r]), int(dec.table["key_len"][r])
+        rec = HintRecord(ns=payload[:ns_size], key=payload[ko:ko + kl], fid=int(dec.table["expire"][r]),
+                         off=int(dec.table["aux0"][r]), size=int(dec.table["aux1"][r]))
+        ret = cb(rec)
+        if ret is not None:
+            raise ret if isinstance(ret, BaseException) else WalError(str(ret))
+    err = _frag_error(dec.result)
+    if err is not None:
+        raise err

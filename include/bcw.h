@@ -1,0 +1,211 @@
+/*
+ * bcw.h -- C-ABI of the MI355X-native bitcaskDB WAL record codec (libbcw.so).
+ *
+ * Drop-in boundary for the per-record loops of bitcaskDB's compaction / recovery / hint rebuild
+ * (wenzhang-dev/bitcaskDB, paths relative to the reference root):
+ *   bcw_decode_segment*  replaces  IterateRecord(wal, cb)      record.go:242-266
+ *                        i.e.      WalIterator.Next            wal_iterator.go:40-100
+ *                        plus      RecordFromBytes             record.go:140-239
+ *                        callers   compaction.go:299, hint.go:133, db_impl.go:307
+ *   mode BCW_MODE_HINT   replaces  IterateHint(hint, cb)       hint.go:163-188 (+ HintRecord.Decode hint.go:50-84)
+ *                        callers   db_impl.go:296, compaction.go:248
+ *   bcw_crc32c_masked    replaces  ComputeCRC32                utils.go:24-29
+ *   bcw_load_super_block replaces  Wal.loadSuperBlock          wal.go:362-398
+ *   bcw_write_super_block          Wal.writeSuperBlock         wal.go:332-360
+ *   bcw_synth_segment    host WAL writer: Wal.WriteRecord wal.go:490-553 over Record.Encode
+ *                                  record.go:57-138 (synthetic segments of the benchmark configs)
+ *
+ * Plain C types only (no torch / HIP types in signatures). Device pointers are `void*`/`uint8_t*`
+ * values obtained from hipMalloc (or any HIP allocator). Every call is reentrant: all mutable
+ * state lives in the bcw_ctx, one per caller thread (compaction, hint rebuild and recovery may run
+ * concurrently). Errors are returned as negative BCW_E* codes; per-record and
+ * per-segment outcomes are reported in the result structs, never by aborting.
+ */
+#ifndef BCW_H
+#define BCW_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BCW_ABI_VERSION 1
+
+/* ---- return codes ---- */
+#define BCW_OK 0
+#define BCW_E_INVAL (-1)      /* bad argument */
+#define BCW_E_HIP (-2)        /* a HIP runtime call failed */
+#define BCW_E_NOMEM (-3)      /* device / host allocation failed */
+#define BCW_E_CAPACITY (-4)   /* output table too small: see bcw_decode_result.n_records_total */
+#define BCW_E_NODEVICE (-5)   /* no HIP device */
+
+/* ---- reference constants (wal.go:45-58, record.go:44-48) ---- */
+#define BCW_BLOCK_SIZE 32768u
+#define BCW_HEADER_SIZE 7u
+#define BCW_SUPER_BLOCK_SIZE 40u
+#define BCW_MAGIC 0x77616C64ull
+#define BCW_RECORD_FULL 1
+#define BCW_RECORD_FIRST 2
+#define BCW_RECORD_MIDDLE 3
+#define BCW_RECORD_LAST 4
+
+/* ---- per-record parse status (record.go:140-239 / hint.go:50-84) ---- */
+#define BCW_ST_OK 0
+#define BCW_ST_INVALID 1     /* errors.New("invalid data") / ErrCorruptedHintRecord */
+#define BCW_ST_PANIC 2       /* the Go reference panics on these bytes (slice bounds) */
+#define BCW_ST_UNSUPPORTED 3 /* a length >= 2^32 (not representable in this table) */
+
+/* ---- segment-level error class of the first failing fragment (wal_iterator.go:75-96) ---- */
+#define BCW_ERR_NONE 0  /* iteration reached EOF (ErrWalIteratorEOF, swallowed by IterateRecord) */
+#define BCW_ERR_CRC 1   /* ErrWalMismatchCRC */
+#define BCW_ERR_TYPE 2  /* ErrWalUnknownRecordType */
+#define BCW_ERR_PANIC 3 /* startOff > file size: the reference panics slicing i.buf[:negative] */
+
+/* ---- super block load result (wal.go:362-398) ---- */
+#define BCW_SB_OK 0
+#define BCW_SB_SHORT 1      /* file shorter than 40 bytes (ReadAt -> io.EOF) */
+#define BCW_SB_CRC 2        /* ErrWalMismatchCRC */
+#define BCW_SB_MAGIC 3      /* ErrWalMismatchMagic */
+#define BCW_SB_BLOCKSIZE 4  /* ErrWalMismatchBlockSize */
+
+#define BCW_MODE_RECORD 0 /* data WAL: RecordFromBytes per record */
+#define BCW_MODE_HINT 1   /* hint WAL: HintRecord.Decode per record */
+
+typedef struct bcw_super_block {
+  uint64_t magic;
+  uint64_t block_size;
+  uint32_t start_off;
+  uint32_t crc;
+  uint64_t create_time;
+  uint64_t base_time;
+} bcw_super_block;
+
+/* Decode parameters. ns_size / etag_size replace the process-global gOpts read by the
+ * reference codec (record.go:141,178; hint.go:51). start_off / base_time come from the WAL's
+ * super block (LoadWal, wal.go:218-259). */
+typedef struct bcw_decode_params {
+  uint64_t seg_len;   /* file size in bytes (Wal.Size) */
+  uint64_t base_time; /* super block baseTime (IterateRecord passes wal.BaseTime()) */
+  uint32_t start_off; /* super block startOff (Wal.offset) */
+  uint32_t ns_size;
+  uint32_t etag_size;
+  uint32_t mode;      /* BCW_MODE_RECORD or BCW_MODE_HINT */
+} bcw_decode_params;
+
+/* Struct-of-arrays record table. All arrays are DEVICE pointers with `capacity` entries.
+ * Row r describes the r-th record the reference iterator emits (in file order).
+ *   record mode: expire = decoded expire incl. baseTime; key/val/meta_len = varint lengths;
+ *                hdr_size = data[0]; flags = flag byte; etag_off = offset of the etag field.
+ *   hint mode:   key_len, hdr_size = key offset; expire = fid; aux0 = off; aux1 = size.
+ * foff is the iterator offset (data start of the record's first non-empty fragment,
+ * wal_iterator.go:70-72); callers subtract BCW_HEADER_SIZE as compaction.go:302 does.
+ * first_frag / emit_frag are global fragment indices: the record's bytes are the data of
+ * fragments [first_frag, emit_frag] (a Full emission: only emit_frag). */
+typedef struct bcw_record_table {
+  uint64_t capacity;
+  uint64_t* foff;
+  uint64_t* size;
+  uint64_t* expire;
+  uint64_t* aux0; /* hint mode only (may be NULL in record mode) */
+  uint64_t* aux1; /* hint mode only (may be NULL in record mode) */
+  uint32_t* key_len;
+  uint32_t* val_len;
+  uint32_t* meta_len;
+  uint32_t* first_frag;
+  uint32_t* emit_frag;
+  uint8_t* hdr_size;
+  uint8_t* flags;
+  uint8_t* etag_off;
+  uint8_t* status;
+} bcw_record_table;
+
+/* Segment-level outcome, written by the device (async API) or the host (sync API).
+ * The Go shim replays rows [0, n_records) in order through the existing callbacks, stops at the
+ * first row whose status != BCW_ST_OK (mapped to the reference's error), and otherwise returns
+ * the error of err_class (or nil when BCW_ERR_NONE). That reproduces IterateRecord exactly. */
+typedef struct bcw_decode_result {
+  uint64_t n_records;       /* records emitted before the first failing fragment */
+  uint64_t n_records_total; /* records emitted by the whole framing (>= n_records) */
+  uint64_t n_frags;         /* fragments parsed by the iterator up to (incl.) err_frag or EOF */
+  uint64_t err_frag;        /* global index of the first failing fragment, UINT64_MAX if none */
+  uint64_t err_file_off;    /* file offset of that fragment's header (0 if none) */
+  int32_t err_class;        /* BCW_ERR_* */
+  int32_t first_bad_record; /* first row < n_records with status != OK, or -1 (capped at INT32_MAX) */
+  uint64_t n_blocks;
+  /* != 0: the context's fragment scratch was too small for this segment; the outputs are invalid.
+   * The next call on this context sizes its scratch to this value (the sync API retries itself). */
+  uint64_t retry_frag_capacity;
+} bcw_decode_result;
+
+/* Fragment table (device arrays, `capacity` entries, global fragment order). */
+typedef struct bcw_frag_table {
+  uint64_t capacity;
+  uint64_t* data_off; /* file offset of the fragment data */
+  uint32_t* len;      /* length after the clamp of wal_iterator.go:75 */
+  uint32_t* stored_crc;
+  uint8_t* type;
+  uint8_t* crc_ok;
+} bcw_frag_table;
+
+/* ---- library ---- */
+int bcw_abi_version(void);
+const char* bcw_strerror(int code);
+int bcw_device_count(void);
+
+/* ---- context: one HIP stream + device tables + grow-only scratch, bound to one device ---- */
+typedef struct bcw_ctx bcw_ctx;
+int bcw_ctx_create(int device, bcw_ctx** out);
+int bcw_ctx_destroy(bcw_ctx* ctx);
+/* Use a caller-owned hipStream_t (passed as void*), e.g. torch.cuda.current_stream().cuda_stream.
+ * NULL restores the context's own stream. */
+int bcw_ctx_set_stream(bcw_ctx* ctx, void* hip_stream);
+void* bcw_ctx_stream(bcw_ctx* ctx);
+int bcw_ctx_sync(bcw_ctx* ctx);
+int bcw_ctx_device(bcw_ctx* ctx);
+/* Per-kernel HIP-event timing of the decode pipeline (events on the launch stream around each
+ * kernel). bcw_ctx_kernel_times synchronises, fills total_ms[k] / launches[k] for kernel ids
+ * k < n accumulated since the last call, resets, and returns the number of kernel ids. */
+int bcw_ctx_set_profiling(bcw_ctx* ctx, int on);
+int bcw_ctx_kernel_times(bcw_ctx* ctx, double* total_ms, uint64_t* launches, int n);
+const char* bcw_kernel_name(int kernel_id);
+
+/* ---- host helpers (no device work) ---- */
+uint32_t bcw_crc32c_masked(const uint8_t* p, uint64_t n);
+int bcw_load_super_block(const uint8_t* p, uint64_t n, bcw_super_block* out);
+void bcw_write_super_block(uint8_t out[40], uint64_t create_time, uint64_t base_time);
+/* Upper bound of records / fragments a segment of seg_len bytes can hold. */
+uint64_t bcw_max_fragments(uint64_t seg_len, uint32_t start_off);
+
+/* ---- decode ----
+ * Async, device-resident: d_seg is a device pointer to the whole file image (super block
+ * included), d_result a device pointer to one bcw_decode_result. Launches on the context stream,
+ * does not synchronise. If the table is too small, d_result->n_records_total still tells the size
+ * needed and rows beyond capacity are not written (check after sync). */
+int bcw_decode_segment_async(bcw_ctx* ctx, const uint8_t* d_seg, const bcw_decode_params* p,
+                             const bcw_record_table* d_table, bcw_decode_result* d_result);
+/* Synchronous, host in / host out: copies seg (host) to the device, decodes, copies the table
+ * (host arrays in h_table) and the result back. Returns BCW_E_CAPACITY when h_table is too small. */
+int bcw_decode_segment(bcw_ctx* ctx, const uint8_t* h_seg, const bcw_decode_params* p,
+                       const bcw_record_table* h_table, bcw_decode_result* h_result);
+/* Fragment table of the most recent decode on this context (device arrays), global order. */
+int bcw_decode_fragments_async(bcw_ctx* ctx, const bcw_frag_table* d_frags);
+/* Same, into host arrays (synchronous). *n_total receives the number of fragments the framing
+ * has (rows beyond h_frags->capacity are not copied). */
+int bcw_decode_fragments(bcw_ctx* ctx, const bcw_frag_table* h_frags, uint64_t* n_total);
+
+/* ---- host WAL writer (wal.go:490-553 with Record.Encode record.go:57-138) ----
+ * Synthetic segment builder for benchmarks and tests: records of ns ('A'+i%26 bytes), a
+ * key_len-byte key (record index LE + splitmix64 bytes) and a value of value_len splitmix64 bytes
+ * (value_mode 1: 128*k bytes, k ~ Zipf(1.1) on [1,512]); no etag/expire/meta; createTime =
+ * baseTime. Records are appended while the file is shorter than target_bytes (and fewer than
+ * max_records if max_records != 0). h_out (host) receives the file image when out_cap suffices;
+ * with h_out == NULL only the size is computed. Returns BCW_OK or BCW_E_CAPACITY. */
+int bcw_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_t seed, uint32_t ns_size,
+                      uint32_t key_len, uint32_t value_len, int value_mode, uint64_t base_time,
+                      uint8_t* h_out, uint64_t out_cap, uint64_t* out_len, uint64_t* out_records);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,679 @@
+/*
+ * bcw_oracle.c -- CPU restatement of bitcaskDB's WAL record codec. TEST INFRASTRUCTURE ONLY:
+ * the parity checker for bitcaskdb_amd/ (see bcw_oracle.h for the reference map and pinning).
+ * Every function cites the reference file:line it restates (paths relative to /root/reference).
+ */
+#include "bcw_oracle.h"
+
+#include <nmmintrin.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------ */
+/* CRC-32C (Castagnoli), reflected poly 0x82F63B78 == Go crc32.MakeTable(crc32.Castagnoli)      */
+/* ------------------------------------------------------------------------------------------ */
+static uint32_t g_tab[256];
+static int g_tab_init = 0;
+
+static void crc_init(void) {
+  if (g_tab_init) return;
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t c = b;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    g_tab[b] = c;
+  }
+  g_tab_init = 1;
+}
+
+uint32_t oc_crc32c_update(uint32_t crc, const uint8_t* p, size_t n) {
+  crc_init();
+  for (size_t i = 0; i < n; ++i) crc = (crc >> 8) ^ g_tab[(crc ^ p[i]) & 0xffu];
+  return crc;
+}
+
+uint32_t oc_crc32c(const uint8_t* p, size_t n) { return ~oc_crc32c_update(0xffffffffu, p, n); }
+
+/* utils.go:24-29: checksum>>15 | checksum<<17, plus 0xa282ead8 (uint32 wraparound) */
+uint32_t oc_compute_crc32(const uint8_t* p, size_t n) {
+  uint32_t c = oc_crc32c(p, n);
+  return ((c >> 15) | (c << 17)) + 0xa282ead8u;
+}
+
+/* Hardware CRC-32C with a 3-way interleave (the shape of Go's amd64 castagnoliSSE42Triple).
+ * The three partial CRCs are merged with a GF(2) shift operator built once per stripe length. */
+static uint32_t gf2_times(const uint32_t* mat, uint32_t vec) {
+  uint32_t s = 0;
+  for (int i = 0; vec; ++i, vec >>= 1)
+    if (vec & 1u) s ^= mat[i];
+  return s;
+}
+static void gf2_square(uint32_t* sq, const uint32_t* mat) {
+  for (int n = 0; n < 32; ++n) sq[n] = gf2_times(mat, mat[n]);
+}
+/* advance a raw reflected CRC state over `len` zero bytes (the zlib crc32_combine squaring) */
+static uint32_t zeros_apply(uint32_t v, size_t len) {
+  uint32_t odd[32], even[32];
+  odd[0] = 0x82F63B78u;
+  uint32_t row = 1;
+  for (int n = 1; n < 32; ++n) { odd[n] = row; row <<= 1; }
+  gf2_square(even, odd); /* 2 zero bits */
+  gf2_square(odd, even); /* 4 zero bits */
+  do {
+    gf2_square(even, odd);
+    if (len & 1) v = gf2_times(even, v);
+    len >>= 1;
+    if (!len) break;
+    gf2_square(odd, even);
+    if (len & 1) v = gf2_times(odd, v);
+    len >>= 1;
+  } while (len);
+  return v;
+}
+static void shift_op(uint32_t* op, size_t len) {
+  for (int n = 0; n < 32; ++n) op[n] = zeros_apply(1u << n, len);
+}
+
+#define HW_STRIPE 4096u
+static uint32_t g_shift_stripe[32];
+static uint32_t g_shift_2stripe[32];
+static int g_shift_init = 0;
+
+static uint32_t hw_run(uint32_t c, const uint8_t* p, size_t n) {
+  while (n >= 8) { uint64_t w; memcpy(&w, p, 8); c = (uint32_t)_mm_crc32_u64(c, w); p += 8; n -= 8; }
+  while (n) { c = _mm_crc32_u8(c, *p++); --n; }
+  return c;
+}
+
+uint32_t oc_crc32c_hw(const uint8_t* p, size_t n) {
+  if (!g_shift_init) {
+    shift_op(g_shift_stripe, HW_STRIPE);
+    shift_op(g_shift_2stripe, 2 * HW_STRIPE);
+    g_shift_init = 1;
+  }
+  uint32_t c = 0xffffffffu;
+  while (n >= 3 * HW_STRIPE) {
+    uint32_t a = c, b = 0, d = 0;
+    const uint8_t* q = p;
+    for (size_t i = 0; i < HW_STRIPE; i += 8) {
+      uint64_t w0, w1, w2;
+      memcpy(&w0, q + i, 8); memcpy(&w1, q + HW_STRIPE + i, 8); memcpy(&w2, q + 2 * HW_STRIPE + i, 8);
+      a = (uint32_t)_mm_crc32_u64(a, w0);
+      b = (uint32_t)_mm_crc32_u64(b, w1);
+      d = (uint32_t)_mm_crc32_u64(d, w2);
+    }
+    c = gf2_times(g_shift_2stripe, a) ^ gf2_times(g_shift_stripe, b) ^ d;
+    p += 3 * HW_STRIPE; n -= 3 * HW_STRIPE;
+  }
+  c = hw_run(c, p, n);
+  return ~c;
+}
+
+static inline uint32_t compute_crc32_hw(const uint8_t* p, size_t n) {
+  uint32_t c = oc_crc32c_hw(p, n);
+  return ((c >> 15) | (c << 17)) + 0xa282ead8u;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* varints: Go encoding/binary (go1.24) Uvarint / PutUvarint; utils.go:51-57 DecodeUvarint       */
+/* ------------------------------------------------------------------------------------------ */
+int oc_uvarint(const uint8_t* p, size_t n, uint64_t* v) {
+  uint64_t x = 0;
+  unsigned s = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (i == 10) { *v = 0; return -(int)(i + 1); }
+    uint8_t b = p[i];
+    if (b < 0x80) {
+      if (i == 9 && b > 1) { *v = 0; return -(int)(i + 1); }
+      *v = x | ((uint64_t)b << s);
+      return (int)(i + 1);
+    }
+    x |= (uint64_t)(b & 0x7f) << s;
+    s += 7;
+  }
+  *v = 0;
+  return 0;
+}
+
+/* DecodeUvarint: every failure maps to (0, 0) */
+static inline uint64_t decode_uvarint(const uint8_t* p, size_t n, size_t* used) {
+  uint64_t v;
+  int k = oc_uvarint(p, n, &v);
+  if (k <= 0) { *used = 0; return 0; }
+  *used = (size_t)k;
+  return v;
+}
+
+int oc_put_uvarint(uint8_t* out, uint64_t v) {
+  int i = 0;
+  while (v >= 0x80) { out[i++] = (uint8_t)(v | 0x80); v >>= 7; }
+  out[i++] = (uint8_t)v;
+  return i;
+}
+
+static inline void put_u32(uint8_t* p, uint32_t v) { memcpy(p, &v, 4); }
+static inline void put_u64(uint8_t* p, uint64_t v) { memcpy(p, &v, 8); }
+static inline uint32_t get_u32(const uint8_t* p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static inline uint64_t get_u64(const uint8_t* p) { uint64_t v; memcpy(&v, p, 8); return v; }
+
+/* ------------------------------------------------------------------------------------------ */
+/* super block: wal.go:332-360 (write), wal.go:362-398 (load: crc -> magic -> blockSize)        */
+/* ------------------------------------------------------------------------------------------ */
+void oc_super_encode(uint8_t out[40], uint64_t create_time, uint64_t base_time) {
+  memset(out, 0, 40);
+  put_u64(out + 0, OC_MAGIC);
+  put_u64(out + 8, OC_BLOCK_SIZE);
+  put_u32(out + 16, OC_SUPER_SIZE);
+  put_u64(out + 20, create_time);
+  put_u64(out + 28, base_time);
+  put_u32(out + 36, oc_compute_crc32(out, 36));
+}
+
+int oc_super_load(const uint8_t* p, size_t n, oc_super* o) {
+  if (n < OC_SUPER_SIZE) return OC_SB_SHORT; /* ReadAt returns io.EOF */
+  uint32_t crc = oc_compute_crc32(p, 36);
+  if (crc != get_u32(p + 36)) return OC_SB_CRC;
+  o->magic = get_u64(p);
+  if (o->magic != OC_MAGIC) return OC_SB_MAGIC;
+  o->block_size = get_u64(p + 8);
+  o->start_off = get_u32(p + 16);
+  if (o->block_size != OC_BLOCK_SIZE) return OC_SB_BLOCKSIZE;
+  o->create_time = get_u64(p + 20);
+  o->base_time = get_u64(p + 28);
+  o->crc = crc;
+  return OC_SB_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* writer: wal.go:482-553. The in-memory image holds the whole file (super block included), so  */
+/* writeOffset(true) = len - 40 and writeOffset(false) = len.                                   */
+/* ------------------------------------------------------------------------------------------ */
+struct oc_writer { uint8_t* buf; uint64_t len, cap; };
+
+static void w_append(oc_writer* w, const void* p, uint64_t n) {
+  if (w->len + n > w->cap) {
+    uint64_t nc = w->cap ? w->cap : 1u << 16;
+    while (nc < w->len + n) nc *= 2;
+    w->buf = (uint8_t*)realloc(w->buf, nc);
+    w->cap = nc;
+  }
+  memcpy(w->buf + w->len, p, n);
+  w->len += n;
+}
+
+oc_writer* oc_writer_new(uint64_t create_time, uint64_t base_time) {
+  oc_writer* w = (oc_writer*)calloc(1, sizeof *w);
+  uint8_t sb[40];
+  oc_super_encode(sb, create_time, base_time);
+  w_append(w, sb, 40);
+  return w;
+}
+
+uint64_t oc_writer_write(oc_writer* w, const uint8_t* rec, size_t n) {
+  static const uint8_t padding[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t offset = 0;
+  int begin = 1;
+  uint64_t left = n;
+  while (left > 0) {
+    uint64_t leftover = OC_BLOCK_SIZE - ((w->len - OC_SUPER_SIZE) % OC_BLOCK_SIZE);
+    if (leftover < OC_HEADER_SIZE) {
+      w_append(w, padding, leftover);
+      leftover = OC_BLOCK_SIZE;
+    }
+    if (begin) offset = w->len;
+    uint64_t avail = leftover - OC_HEADER_SIZE;
+    uint64_t frag = left < avail ? left : avail;
+    int end = (left == frag);
+    uint8_t type = (begin && end) ? OC_FULL : begin ? OC_FIRST : end ? OC_LAST : OC_MIDDLE;
+    uint8_t hdr[7];
+    put_u32(hdr, oc_compute_crc32(rec, frag));
+    uint16_t l16 = (uint16_t)frag;
+    memcpy(hdr + 4, &l16, 2);
+    hdr[6] = type;
+    w_append(w, hdr, 7);
+    w_append(w, rec, frag);
+    rec += frag;
+    left -= frag;
+    begin = 0;
+  }
+  return offset;
+}
+
+uint64_t oc_writer_size(const oc_writer* w) { return w->len; }
+const uint8_t* oc_writer_data(const oc_writer* w) { return w->buf; }
+void oc_writer_free(oc_writer* w) { if (w) { free(w->buf); free(w); } }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Record.Encode: record.go:57-138                                                              */
+/* ------------------------------------------------------------------------------------------ */
+int64_t oc_record_encode(uint8_t* out, const uint8_t* ns, size_t ns_len, const uint8_t* key, size_t key_len,
+                         const uint8_t* val, size_t val_len, const uint8_t* etag, size_t etag_len,
+                         uint64_t expire, int tombstone, const uint8_t* meta, size_t meta_len,
+                         uint64_t base_time) {
+  uint8_t flag = 0;
+  if (etag_len == 0) flag |= 1u << 0;
+  if (tombstone) flag |= 1u << 2;
+  uint8_t expb[10];
+  int expire_size = 0;
+  if (expire == 0) flag |= 1u << 1;
+  else if (expire < base_time) return -1; /* "invalid expire" */
+  else expire_size = oc_put_uvarint(expb, expire - base_time);
+  uint8_t tmp[30];
+  int t = 0;
+  t += oc_put_uvarint(tmp + t, key_len);
+  t += oc_put_uvarint(tmp + t, val_len);
+  t += oc_put_uvarint(tmp + t, meta_len);
+  size_t header = (size_t)t + expire_size + ns_len + etag_len + 2;
+  size_t o = 0;
+  out[o++] = (uint8_t)header; /* byte(headerSize): truncates above 255 (record.go:109) */
+  memcpy(out + o, ns, ns_len); o += ns_len;
+  out[o++] = flag;
+  memcpy(out + o, tmp, t); o += t;
+  memcpy(out + o, etag, etag_len); o += etag_len;
+  memcpy(out + o, expb, expire_size); o += expire_size;
+  memcpy(out + o, key, key_len); o += key_len;
+  memcpy(out + o, val, val_len); o += val_len;
+  memcpy(out + o, meta, meta_len); o += meta_len;
+  return (int64_t)o;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* RecordFromBytes: record.go:140-239, with Go slice-bound panics made explicit.                */
+/* `cap` is cap(data): a Full record aliases the 32 KiB iterator buffer (wal_iterator.go:76,87). */
+/* ------------------------------------------------------------------------------------------ */
+void oc_record_parse(const uint8_t* data, size_t len, size_t cap, uint64_t base_time, uint32_t ns_size,
+                     uint32_t etag_size, oc_rec* r) {
+  (void)cap;
+  r->hdr_size = 0; r->flags = 0; r->etag_off = 0;
+  r->key_len = r->val_len = r->meta_len = 0; r->expire = 0;
+  size_t min_hdr = 1 + (size_t)ns_size + 1 + 3;
+  if (len < min_hdr) { r->status = OC_ST_INVALID; return; }
+  size_t off = 0;
+  uint64_t header = data[0];
+  off++;
+  off += ns_size;
+  uint8_t flag = data[off];
+  off++;
+  size_t used;
+  uint64_t key_len = decode_uvarint(data + off, len - off, &used); off += used;
+  uint64_t val_len = decode_uvarint(data + off, len - off, &used); off += used;
+  uint64_t meta_len = decode_uvarint(data + off, len - off, &used); off += used;
+  uint64_t etag_len = (flag & 1u) ? 0 : etag_size;
+  uint64_t expire_size = 0, expire = 0;
+  r->hdr_size = (uint8_t)header; r->flags = flag; r->etag_off = (uint8_t)off;
+  r->key_len = key_len; r->val_len = val_len; r->meta_len = meta_len;
+  if ((flag & 2u) == 0) {
+    /* data[offset+etagLen:] panics when offset+etagLen > len(data) (record.go:186) */
+    if ((uint64_t)off + etag_len > (uint64_t)len) { r->status = OC_ST_PANIC; return; }
+    size_t p = off + (size_t)etag_len;
+    expire = decode_uvarint(data + p, len - p, &used);
+    expire_size = used;
+    expire += base_time; /* uint64 wraparound */
+  }
+  r->expire = expire;
+  /* currentTotalSize := currentHeaderSize + int(keyLen+valLen+metaLen): int64 arithmetic */
+  int64_t cur_hdr = (int64_t)off + (int64_t)etag_len + (int64_t)expire_size;
+  int64_t cur_total = cur_hdr + (int64_t)(key_len + val_len + meta_len);
+  if ((uint64_t)cur_hdr != header || cur_total != (int64_t)len) { r->status = OC_ST_INVALID; return; }
+  /* slicing after validation (record.go:197-212): data[o : o+int(n)] panics when int(n) < 0 or when
+   * the cumulative end passes cap(data); after a passed validation the latter happens exactly when
+   * keyLen+valLen+metaLen wrapped around 2^64 (then one length is > 2^62, far beyond any cap). */
+  {
+    uint64_t s1 = key_len + val_len;
+    int wrapped = s1 < key_len;
+    uint64_t s2 = s1 + meta_len;
+    wrapped |= s2 < s1;
+    if ((int64_t)key_len < 0 || (int64_t)val_len < 0 || (int64_t)meta_len < 0 || wrapped) {
+      r->status = OC_ST_PANIC;
+      return;
+    }
+  }
+  if (key_len > 0xffffffffull || val_len > 0xffffffffull || meta_len > 0xffffffffull || len > 0xffffffffull) {
+    r->status = OC_ST_UNSUPPORTED;
+    return;
+  }
+  /* meta > 0 would be msgpack.Unmarshal'ed (record.go:217-223): opaque here (parity unpinned) */
+  r->status = OC_ST_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* hint codec: hint.go:32-48 (Encode), hint.go:50-84 (Decode)                                   */
+/* ------------------------------------------------------------------------------------------ */
+size_t oc_hint_encode(uint8_t* out, const uint8_t* ns, size_t ns_len, const uint8_t* key, size_t key_len,
+                      uint64_t fid, uint64_t off, uint64_t size) {
+  size_t o = 0;
+  memcpy(out, ns, ns_len); o += ns_len;
+  o += oc_put_uvarint(out + o, key_len);
+  memcpy(out + o, key, key_len); o += key_len;
+  o += oc_put_uvarint(out + o, fid);
+  o += oc_put_uvarint(out + o, off);
+  o += oc_put_uvarint(out + o, size);
+  return o;
+}
+
+void oc_hint_parse(const uint8_t* data, size_t len, uint32_t ns_size, oc_rec* r) {
+  r->hdr_size = 0; r->flags = 0; r->etag_off = 0;
+  r->key_len = r->val_len = r->meta_len = 0; r->expire = 0;
+  size_t min_sz = (size_t)ns_size + 1 + 1 + 3;
+  if (len < min_sz) { r->status = OC_ST_INVALID; return; }
+  int64_t off = ns_size;
+  size_t used;
+  uint64_t key_len = decode_uvarint(data + off, len - (size_t)off, &used);
+  off += (int64_t)used;
+  int64_t key_off = off;
+  off = (int64_t)((uint64_t)off + key_len); /* offset += int(keyLen): Go int64 wraparound */
+  r->key_len = key_len;
+  r->hdr_size = (uint8_t)key_off;
+  if (off < 0 || off > (int64_t)len) { r->status = OC_ST_PANIC; return; } /* data[offset:] */
+  uint64_t fid = decode_uvarint(data + off, len - (size_t)off, &used); off += (int64_t)used;
+  uint64_t hoff = decode_uvarint(data + off, len - (size_t)off, &used); off += (int64_t)used;
+  uint64_t hsize = decode_uvarint(data + off, len - (size_t)off, &used); off += (int64_t)used;
+  r->expire = fid; r->val_len = hoff; r->meta_len = hsize;
+  if (off != (int64_t)len) { r->status = OC_ST_INVALID; return; }
+  /* r.key = data[keyOffset : keyOffset+int(keyLen)] -- panics when int(keyLen) < 0 */
+  if ((int64_t)key_len < 0) { r->status = OC_ST_PANIC; return; }
+  r->status = OC_ST_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* segment iteration: wal_iterator.go:40-100 (Next) driven as record.go:242-266 / hint.go:163  */
+/* ------------------------------------------------------------------------------------------ */
+struct oc_decode {
+  oc_frag* frags; uint64_t n_frags, cap_frags;
+  oc_rec* recs; uint64_t n_recs, cap_recs;
+  uint8_t* bytes; uint64_t n_bytes, cap_bytes;
+  uint64_t* byte_offs;
+  uint64_t err_frag;
+  int32_t err_class;
+};
+
+static void push_frag(oc_decode* d, const oc_frag* f) {
+  if (d->n_frags == d->cap_frags) {
+    d->cap_frags = d->cap_frags ? d->cap_frags * 2 : 1024;
+    d->frags = (oc_frag*)realloc(d->frags, d->cap_frags * sizeof(oc_frag));
+  }
+  d->frags[d->n_frags++] = *f;
+}
+
+static void push_rec(oc_decode* d, const oc_rec* r, const uint8_t* bytes, uint64_t n) {
+  if (d->n_recs == d->cap_recs) {
+    d->cap_recs = d->cap_recs ? d->cap_recs * 2 : 1024;
+    d->recs = (oc_rec*)realloc(d->recs, d->cap_recs * sizeof(oc_rec));
+    d->byte_offs = (uint64_t*)realloc(d->byte_offs, (d->cap_recs + 1) * sizeof(uint64_t));
+  }
+  if (d->n_bytes + n > d->cap_bytes) {
+    uint64_t nc = d->cap_bytes ? d->cap_bytes : 1u << 16;
+    while (nc < d->n_bytes + n) nc *= 2;
+    d->bytes = (uint8_t*)realloc(d->bytes, nc);
+    d->cap_bytes = nc;
+  }
+  d->byte_offs[d->n_recs] = d->n_bytes;
+  memcpy(d->bytes + d->n_bytes, bytes, n);
+  d->n_bytes += n;
+  d->recs[d->n_recs++] = *r;
+  d->byte_offs[d->n_recs] = d->n_bytes;
+}
+
+oc_decode* oc_decode_segment(const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                             uint32_t ns_size, uint32_t etag_size, int mode) {
+  oc_decode* d = (oc_decode*)calloc(1, sizeof *d);
+  d->err_frag = UINT64_MAX;
+  d->err_class = OC_ERR_NONE;
+  d->byte_offs = (uint64_t*)calloc(1, sizeof(uint64_t));
+  /* NewWalIterator: fileOff = wal.offset (super.startOff), bufOff = bufSize = 0 */
+  int64_t file_off = start_off;
+  int64_t buf_off = 0, buf_size = 0;
+  /* the Next() loop state carried across calls: record (acc) and off */
+  uint8_t* acc = NULL; uint64_t acc_len = 0, acc_cap = 0;
+  uint64_t off = 0;
+  uint32_t rec_first = 0; /* first fragment index contributing bytes to acc */
+  for (;;) {
+    if (buf_off + (int64_t)OC_HEADER_SIZE > buf_size) {
+      file_off += buf_size;
+      int64_t rem = (int64_t)len - file_off;
+      buf_size = rem < (int64_t)OC_BLOCK_SIZE ? rem : (int64_t)OC_BLOCK_SIZE;
+      if (buf_size == 0) break; /* ErrWalIteratorEOF; a pending partial record is dropped */
+      if (buf_size < 0) { d->err_class = OC_ERR_PANIC; d->err_frag = d->n_frags; break; } /* i.buf[:neg] */
+      buf_off = 0;
+      /* wal_iterator.go:62-76: after a refill the header is sliced without re-checking bufSize
+       * (cap(i.buf) is 32 KiB, so buf[0:7] is legal), then length = min(len, bufSize-7) < 0 and
+       * i.buf[7:7+length] panics: a last block of 1..6 bytes always panics. */
+      if (buf_size < (int64_t)OC_HEADER_SIZE) { d->err_class = OC_ERR_PANIC; d->err_frag = d->n_frags; break; }
+    }
+    const uint8_t* buf = seg + file_off;
+    const uint8_t* header = buf + buf_off;
+    buf_off += OC_HEADER_SIZE;
+    uint32_t crc = get_u32(header);
+    uint16_t l16; memcpy(&l16, header + 4, 2);
+    int64_t length = l16;
+    uint8_t type = header[6];
+    if (acc_len == 0) { off = (uint64_t)(file_off + buf_off); rec_first = (uint32_t)d->n_frags; }
+    if (length > buf_size - buf_off) length = buf_size - buf_off; /* wal_iterator.go:75 */
+    const uint8_t* data = buf + buf_off;
+    buf_off += length;
+    oc_frag f;
+    memset(&f, 0, sizeof f);
+    f.data_off = (uint64_t)(file_off + (buf_off - length));
+    f.len = (uint32_t)length;
+    f.stored_crc = crc;
+    f.type = type;
+    f.crc_ok = oc_compute_crc32(data, (size_t)length) == crc;
+    uint32_t fidx = (uint32_t)d->n_frags;
+    push_frag(d, &f);
+    if (!f.crc_ok) { d->err_class = OC_ERR_CRC; d->err_frag = fidx; break; }
+    const uint8_t* rec_bytes = NULL;
+    uint64_t rec_len = 0, rec_cap = 0;
+    uint32_t first = rec_first;
+    if (type == OC_FULL) {
+      rec_bytes = data; rec_len = (uint64_t)length;
+      rec_cap = (uint64_t)(buf_size - (buf_off - length)); /* cap of i.buf[bufOff:...] */
+      first = fidx;
+    } else if (type == OC_FIRST || type == OC_MIDDLE || type == OC_LAST) {
+      if (acc_len + (uint64_t)length > acc_cap) {
+        acc_cap = (acc_len + (uint64_t)length) * 2 + 64;
+        acc = (uint8_t*)realloc(acc, acc_cap);
+      }
+      memcpy(acc + acc_len, data, (size_t)length);
+      acc_len += (uint64_t)length;
+      if (type != OC_LAST) continue;
+      rec_bytes = acc; rec_len = acc_len; rec_cap = acc_len;
+    } else {
+      d->err_class = OC_ERR_TYPE; d->err_frag = fidx; break;
+    }
+    oc_rec r;
+    memset(&r, 0, sizeof r);
+    r.foff = off;
+    r.size = rec_len;
+    r.first_frag = first;
+    r.emit_frag = fidx;
+    if (mode == 0) oc_record_parse(rec_bytes, (size_t)rec_len, (size_t)rec_cap, base_time, ns_size, etag_size, &r);
+    else oc_hint_parse(rec_bytes, (size_t)rec_len, ns_size, &r);
+    push_rec(d, &r, rec_bytes, rec_len);
+    acc_len = 0; /* Next() returns: the next call starts with record == nil */
+  }
+  free(acc);
+  return d;
+}
+
+void oc_decode_counts(const oc_decode* d, uint64_t* n_frags, uint64_t* n_recs, uint64_t* err_frag,
+                      int32_t* err_class, uint64_t* rec_bytes) {
+  *n_frags = d->n_frags; *n_recs = d->n_recs; *err_frag = d->err_frag; *err_class = d->err_class;
+  *rec_bytes = d->n_bytes;
+}
+void oc_decode_frags(const oc_decode* d, oc_frag* dst) { memcpy(dst, d->frags, d->n_frags * sizeof(oc_frag)); }
+void oc_decode_recs(const oc_decode* d, oc_rec* dst) { memcpy(dst, d->recs, d->n_recs * sizeof(oc_rec)); }
+void oc_decode_bytes(const oc_decode* d, uint8_t* dst, uint64_t* offs) {
+  memcpy(dst, d->bytes, d->n_bytes);
+  memcpy(offs, d->byte_offs, (d->n_recs + 1) * sizeof(uint64_t));
+}
+void oc_decode_free(oc_decode* d) {
+  if (!d) return;
+  free(d->frags); free(d->recs); free(d->bytes); free(d->byte_offs); free(d);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* CPU baseline: the same Next() + RecordFromBytes loop with hardware CRC and no per-record      */
+/* allocation (an upper bound on the Go path's speed).                             */
+/* ------------------------------------------------------------------------------------------ */
+uint64_t oc_decode_fast(const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                        uint32_t ns_size, uint32_t etag_size, int32_t* err_class, uint64_t* checksum) {
+  int64_t file_off = start_off, buf_off = 0, buf_size = 0;
+  uint64_t acc_len = 0, off = 0, n = 0, sum = 0;
+  static __thread uint8_t* acc = NULL;
+  static __thread uint64_t acc_cap = 0;
+  uint8_t blk[OC_BLOCK_SIZE]; /* pread target: one 32 KiB block at a time (wal_iterator.go:55) */
+  *err_class = OC_ERR_NONE;
+  for (;;) {
+    if (buf_off + (int64_t)OC_HEADER_SIZE > buf_size) {
+      file_off += buf_size;
+      int64_t rem = (int64_t)len - file_off;
+      buf_size = rem < (int64_t)OC_BLOCK_SIZE ? rem : (int64_t)OC_BLOCK_SIZE;
+      if (buf_size <= 0) { if (buf_size < 0) *err_class = OC_ERR_PANIC; break; }
+      if (buf_size < (int64_t)OC_HEADER_SIZE) { *err_class = OC_ERR_PANIC; break; }
+      memcpy(blk, seg + file_off, (size_t)buf_size);
+      buf_off = 0;
+    }
+    const uint8_t* header = blk + buf_off;
+    buf_off += OC_HEADER_SIZE;
+    uint32_t crc = get_u32(header);
+    uint16_t l16; memcpy(&l16, header + 4, 2);
+    int64_t length = l16;
+    uint8_t type = header[6];
+    if (acc_len == 0) off = (uint64_t)(file_off + buf_off);
+    if (length > buf_size - buf_off) length = buf_size - buf_off;
+    const uint8_t* data = blk + buf_off;
+    buf_off += length;
+    if (compute_crc32_hw(data, (size_t)length) != crc) { *err_class = OC_ERR_CRC; break; }
+    const uint8_t* rb;
+    uint64_t rl;
+    if (type == OC_FULL) { rb = data; rl = (uint64_t)length; }
+    else if (type >= OC_FIRST && type <= OC_LAST) {
+      if (acc_len + (uint64_t)length > acc_cap) { acc_cap = (acc_len + length) * 2 + 64; acc = (uint8_t*)realloc(acc, acc_cap); }
+      memcpy(acc + acc_len, data, (size_t)length);
+      acc_len += (uint64_t)length;
+      if (type != OC_LAST) continue;
+      rb = acc; rl = acc_len;
+    } else { *err_class = OC_ERR_TYPE; break; }
+    oc_rec r;
+    oc_record_parse(rb, (size_t)rl, (size_t)rl, base_time, ns_size, etag_size, &r);
+    acc_len = 0;
+    if (r.status != OC_ST_OK) break; /* IterateRecord returns the parse error */
+    sum += off + rl + r.key_len;
+    ++n;
+  }
+  *checksum = sum;
+  return n;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* compaction (compaction.go:294-327) and hint rebuild (hint.go:123-161)                        */
+/* ------------------------------------------------------------------------------------------ */
+int64_t oc_compact_append(oc_writer* dst, oc_writer* hint, uint64_t dst_fid, const uint8_t* seg,
+                          uint64_t len, uint32_t start_off, uint64_t src_base, uint64_t dst_base,
+                          uint32_t ns_size, uint32_t etag_size, const uint8_t* keep, uint64_t n_keep,
+                          uint64_t* offs) {
+  oc_decode* d = oc_decode_segment(seg, len, start_off, src_base, ns_size, etag_size, 0);
+  uint8_t* buf = NULL;
+  size_t buf_cap = 0;
+  int64_t rc = 0;
+  for (uint64_t i = 0; i < d->n_recs; ++i) {
+    const oc_rec* r = &d->recs[i];
+    if (r->status != OC_ST_OK) { rc = -2 - (int64_t)i; break; } /* IterateRecord returns the error */
+    if (i >= n_keep || !keep[i]) { if (offs) offs[i] = UINT64_MAX; continue; } /* doFilter dropped it */
+    const uint8_t* p = d->bytes + d->byte_offs[i];
+    const uint8_t* ns = p + 1;
+    size_t etag_len = (r->flags & 1u) ? 0 : etag_size;
+    const uint8_t* etag = p + r->etag_off;
+    const uint8_t* key = p + r->hdr_size;
+    const uint8_t* val = key + r->key_len;
+    const uint8_t* meta = val + r->val_len;
+    size_t need = 64 + ns_size + etag_len + r->key_len + r->val_len + r->meta_len;
+    if (need > buf_cap) { buf_cap = need * 2; buf = (uint8_t*)realloc(buf, buf_cap); }
+    int64_t n = oc_record_encode(buf, ns, ns_size, key, r->key_len, val, r->val_len, etag, etag_len, r->expire,
+                                 (r->flags >> 2) & 1u, meta, r->meta_len, dst_base);
+    if (n < 0) { rc = -1 - (int64_t)i; break; }
+    uint64_t o = oc_writer_write(dst, buf, (size_t)n);
+    if (offs) offs[i] = o;
+    uint8_t hb[64 + 255 + 30];
+    uint8_t* hp = hb;
+    size_t hneed = ns_size + r->key_len + 40;
+    uint8_t* heap = NULL;
+    if (hneed > sizeof hb) { heap = (uint8_t*)malloc(hneed); hp = heap; }
+    size_t hn = oc_hint_encode(hp, ns, ns_size, key, r->key_len, dst_fid, o, (uint64_t)n);
+    oc_writer_write(hint, hp, hn);
+    free(heap);
+  }
+  if (d->err_class != OC_ERR_NONE && rc == 0) rc = -(int64_t)(1ull << 62); /* iterator error */
+  free(buf);
+  oc_decode_free(d);
+  return rc;
+}
+
+int64_t oc_hint_by_wal(oc_writer* hint, uint64_t fid, const uint8_t* seg, uint64_t len, uint32_t start_off,
+                       uint64_t base_time, uint32_t ns_size, uint32_t etag_size) {
+  oc_decode* d = oc_decode_segment(seg, len, start_off, base_time, ns_size, etag_size, 0);
+  int64_t rc = 0;
+  for (uint64_t i = 0; i < d->n_recs; ++i) {
+    const oc_rec* r = &d->recs[i];
+    if (r->status != OC_ST_OK) { rc = -1 - (int64_t)i; break; }
+    const uint8_t* p = d->bytes + d->byte_offs[i];
+    size_t hneed = ns_size + r->key_len + 40;
+    uint8_t* hb = (uint8_t*)malloc(hneed);
+    size_t hn = oc_hint_encode(hb, p + 1, ns_size, p + r->hdr_size, r->key_len, fid, r->foff - OC_HEADER_SIZE, r->size);
+    oc_writer_write(hint, hb, hn);
+    free(hb);
+  }
+  if (d->err_class != OC_ERR_NONE && rc == 0) rc = -(int64_t)(1ull << 62);
+  oc_decode_free(d);
+  return rc;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* synthetic segments: splitmix64 stream; ns = 'A'+i%26; key = index(8 B LE) +    */
+/* PRNG bytes; value = PRNG bytes; no etag / expire / meta; createTime = baseTime.              */
+/* ------------------------------------------------------------------------------------------ */
+static inline uint64_t splitmix64(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static void fill_rand(uint64_t* s, uint8_t* p, size_t n) {
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) { uint64_t v = splitmix64(s); memcpy(p + i, &v, 8); }
+  if (i < n) { uint64_t v = splitmix64(s); memcpy(p + i, &v, n - i); }
+}
+
+oc_writer* oc_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_t seed, uint32_t ns_size,
+                            uint32_t key_len, uint32_t value_len, int value_mode, uint64_t base_time) {
+  oc_writer* w = oc_writer_new(base_time, base_time);
+  uint64_t s = seed;
+  double cdf[512];
+  if (value_mode == 1) {
+    double acc = 0;
+    for (int k = 1; k <= 512; ++k) { acc += pow((double)k, -1.1); cdf[k - 1] = acc; }
+    for (int k = 0; k < 512; ++k) cdf[k] /= acc;
+  }
+  uint8_t* ns = (uint8_t*)malloc(ns_size + 1);
+  for (uint32_t i = 0; i < ns_size; ++i) ns[i] = (uint8_t)('A' + i % 26);
+  size_t vmax = value_mode == 1 ? 128 * 512 : value_len;
+  uint8_t* key = (uint8_t*)malloc(key_len + 8);
+  uint8_t* val = (uint8_t*)malloc(vmax + 8);
+  uint8_t* rec = (uint8_t*)malloc(vmax + key_len + ns_size + 64);
+  for (uint64_t i = 0; (max_records == 0 || i < max_records) && w->len < target_bytes; ++i) {
+    size_t vl = value_len;
+    if (value_mode == 1) {
+      double u = (double)(splitmix64(&s) >> 11) * (1.0 / 9007199254740992.0);
+      int lo = 0, hi = 511;
+      while (lo < hi) { int mid = (lo + hi) / 2; if (cdf[mid] < u) lo = mid + 1; else hi = mid; }
+      vl = 128u * (size_t)(lo + 1);
+    }
+    fill_rand(&s, key, key_len);
+    if (key_len >= 8) memcpy(key, &i, 8);
+    fill_rand(&s, val, vl);
+    int64_t n = oc_record_encode(rec, ns, ns_size, key, key_len, val, vl, NULL, 0, 0, 0, NULL, 0, base_time);
+    oc_writer_write(w, rec, (size_t)n);
+  }
+  free(ns); free(key); free(val); free(rec);
+  return w;
+}

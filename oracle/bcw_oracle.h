@@ -1,0 +1,156 @@
+/*
+ * bcw_oracle.h -- CPU restatement of bitcaskDB's WAL record codec (TEST INFRASTRUCTURE ONLY).
+ *
+ * This is the parity oracle for the MI355X codec in bitcaskdb_amd/. It restates, in plain C,
+ * the reference Go code of wenzhang-dev/bitcaskDB (snapshot mounted at /root/reference):
+ *   utils.go:24-29   ComputeCRC32 (CRC-32C, rotr15, +0xa282ead8)
+ *   utils.go:51-57   DecodeUvarint (Go encoding/binary.Uvarint, errors -> (0,0))
+ *   wal.go:29-58     super block / framing constants
+ *   wal.go:332-398   writeSuperBlock / loadSuperBlock
+ *   wal.go:482-553   writeOffset / WriteRecord
+ *   wal_iterator.go:40-100  WalIterator.Next
+ *   record.go:57-138 Record.Encode, record.go:140-239 RecordFromBytes, record.go:242-266 IterateRecord
+ *   hint.go:32-84    HintRecord.Encode/Decode, hint.go:123-161 NewHintByWal, hint.go:163-188 IterateHint
+ *   compaction.go:294-327 compactOneWal (re-encode of kept records into a dst WAL + hint WAL)
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
+ * The product path (bitcaskdb_amd/) never links or calls it.
+ *
+ * Parity pinning: the reference Go toolchain is absent from this image (no `go` binary), so the
+ * reference cannot be compiled or run here. This oracle is pinned by (i) public known answers
+ * (CRC-32C("123456789") = 0xE3069283), (ii) the reference tests' round-trip scenarios restated in
+ * tests/, and (iii) golden fixtures cross-checked against an independent pure-Python restatement
+ * (tests/golden/pyref.py). msgpack app-meta is treated as opaque bytes: parity unpinned there.
+ */
+#ifndef BCW_ORACLE_H
+#define BCW_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OC_BLOCK_SIZE 32768u
+#define OC_HEADER_SIZE 7u
+#define OC_SUPER_SIZE 40u
+#define OC_MAGIC 0x77616C64ull
+
+enum { OC_FULL = 1, OC_FIRST = 2, OC_MIDDLE = 3, OC_LAST = 4 };
+
+/* per-record parse status (record.go:140-239 / hint.go:50-84) */
+enum {
+  OC_ST_OK = 0,
+  OC_ST_INVALID = 1,     /* errors.New("invalid data") or ErrCorruptedHintRecord */
+  OC_ST_PANIC = 2,       /* the reference would panic (slice bounds) */
+  OC_ST_UNSUPPORTED = 3  /* a length >= 2^32: not representable in the device table */
+};
+/* segment-level error class (first failing fragment) */
+enum { OC_ERR_NONE = 0, OC_ERR_CRC = 1, OC_ERR_TYPE = 2, OC_ERR_PANIC = 3 };
+/* super block load errors (wal.go:362-398) */
+enum { OC_SB_OK = 0, OC_SB_SHORT = 1, OC_SB_CRC = 2, OC_SB_MAGIC = 3, OC_SB_BLOCKSIZE = 4 };
+
+typedef struct oc_frag {
+  uint64_t data_off;   /* file offset of the fragment data (header + 7) */
+  uint32_t len;        /* length after the clamp of wal_iterator.go:75 */
+  uint32_t stored_crc; /* header bytes [0,4) */
+  uint8_t type;        /* header byte 6 */
+  uint8_t crc_ok;
+  uint8_t pad[6];
+} oc_frag; /* 24 B */
+
+typedef struct oc_rec {
+  uint64_t foff;      /* iterator offset: data start of the record (wal_iterator.go:70-72) */
+  uint64_t size;      /* len(recordBytes) */
+  uint64_t expire;    /* decoded expire incl. baseTime (record.go:184-188); hint: fid */
+  uint64_t key_len;   /* record: keyLen; hint: keyLen */
+  uint64_t val_len;   /* record: valLen; hint: off */
+  uint64_t meta_len;  /* record: metaLen; hint: size */
+  uint32_t first_frag;/* first fragment whose data is part of the record */
+  uint32_t emit_frag; /* fragment that completed the record (Full or Last) */
+  uint8_t hdr_size;   /* record: data[0]; hint: key offset */
+  uint8_t flags;      /* record: flag byte; hint: 0 */
+  uint8_t etag_off;   /* record: offset of etag/expire fields; hint: 0 */
+  uint8_t status;     /* OC_ST_* */
+  uint8_t pad[4];
+} oc_rec; /* 64 B */
+
+typedef struct oc_super {
+  uint64_t magic, block_size;
+  uint32_t start_off;
+  uint64_t create_time, base_time;
+  uint32_t crc;
+} oc_super;
+
+/* ---- arithmetic core ---- */
+uint32_t oc_crc32c_update(uint32_t crc, const uint8_t* p, size_t n); /* raw reflected update */
+uint32_t oc_crc32c(const uint8_t* p, size_t n);                       /* standard CRC-32C */
+uint32_t oc_compute_crc32(const uint8_t* p, size_t n);                /* utils.go:24-29 */
+uint32_t oc_crc32c_hw(const uint8_t* p, size_t n);                    /* SSE4.2 3-way (baseline) */
+int oc_uvarint(const uint8_t* p, size_t n, uint64_t* v);              /* Go binary.Uvarint */
+int oc_put_uvarint(uint8_t* out, uint64_t v);                         /* Go binary.PutUvarint */
+
+/* ---- super block ---- */
+void oc_super_encode(uint8_t out[40], uint64_t create_time, uint64_t base_time);
+int oc_super_load(const uint8_t* p, size_t n, oc_super* out);
+
+/* ---- writer (wal.go:490-553), growable in-memory file image ---- */
+typedef struct oc_writer oc_writer;
+oc_writer* oc_writer_new(uint64_t create_time, uint64_t base_time);
+uint64_t oc_writer_write(oc_writer* w, const uint8_t* rec, size_t n); /* returns record offset */
+uint64_t oc_writer_size(const oc_writer* w);
+const uint8_t* oc_writer_data(const oc_writer* w);
+void oc_writer_free(oc_writer* w);
+
+/* ---- record / hint payload codecs ---- */
+/* Record.Encode (record.go:57-138); returns payload length, or -1 on "invalid expire". */
+int64_t oc_record_encode(uint8_t* out, const uint8_t* ns, size_t ns_len, const uint8_t* key, size_t key_len,
+                         const uint8_t* val, size_t val_len, const uint8_t* etag, size_t etag_len,
+                         uint64_t expire, int tombstone, const uint8_t* meta, size_t meta_len,
+                         uint64_t base_time);
+/* RecordFromBytes (record.go:140-239) into r (fields + status) */
+void oc_record_parse(const uint8_t* data, size_t len, size_t cap, uint64_t base_time, uint32_t ns_size,
+                     uint32_t etag_size, oc_rec* r);
+/* HintRecord.Encode (hint.go:32-48) */
+size_t oc_hint_encode(uint8_t* out, const uint8_t* ns, size_t ns_len, const uint8_t* key, size_t key_len,
+                      uint64_t fid, uint64_t off, uint64_t size);
+/* HintRecord.Decode (hint.go:50-84) into r */
+void oc_hint_parse(const uint8_t* data, size_t len, uint32_t ns_size, oc_rec* r);
+
+/* ---- segment decode: WalIterator.Next + RecordFromBytes / HintRecord.Decode ---- */
+typedef struct oc_decode oc_decode;
+/* mode 0: data WAL (records), 1: hint WAL. Iterates from start_off to EOF or the first fragment
+ * error; every emitted record is parsed (parse errors do not stop this raw iteration). */
+oc_decode* oc_decode_segment(const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                             uint32_t ns_size, uint32_t etag_size, int mode);
+void oc_decode_counts(const oc_decode* d, uint64_t* n_frags, uint64_t* n_recs, uint64_t* err_frag,
+                      int32_t* err_class, uint64_t* rec_bytes);
+void oc_decode_frags(const oc_decode* d, oc_frag* dst);
+void oc_decode_recs(const oc_decode* d, oc_rec* dst);
+void oc_decode_bytes(const oc_decode* d, uint8_t* dst, uint64_t* offs); /* payloads, concatenated */
+void oc_decode_free(oc_decode* d);
+
+/* fast restated decode loop used as the CPU baseline (hardware CRC, no allocation per record):
+ * returns records delivered; *err_class gets OC_ERR_*. */
+uint64_t oc_decode_fast(const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                        uint32_t ns_size, uint32_t etag_size, int32_t* err_class, uint64_t* checksum);
+
+/* ---- compaction re-encode (compactOneWal) and hint rebuild (NewHintByWal) ----
+ * Appends every delivered source record with keep[i] != 0 to dst/hint writers.
+ * Returns 0, or -1 - i if record i fails Record.Encode ("invalid expire"). offs[i] = dst offset. */
+int64_t oc_compact_append(oc_writer* dst, oc_writer* hint, uint64_t dst_fid, const uint8_t* seg,
+                          uint64_t len, uint32_t start_off, uint64_t src_base, uint64_t dst_base,
+                          uint32_t ns_size, uint32_t etag_size, const uint8_t* keep, uint64_t n_keep,
+                          uint64_t* offs);
+int64_t oc_hint_by_wal(oc_writer* hint, uint64_t fid, const uint8_t* seg, uint64_t len, uint32_t start_off,
+                       uint64_t base_time, uint32_t ns_size, uint32_t etag_size);
+
+/* ---- synthetic segments for configs A-E (deterministic, seeded) ---- */
+/* value_mode 0: fixed value_len; 1: 128*k, k ~ Zipf(s=1.1) on [1,512] */
+oc_writer* oc_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_t seed, uint32_t ns_size,
+                            uint32_t key_len, uint32_t value_len, int value_mode, uint64_t base_time);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,192 @@
+"""ctypes binding of the CPU parity oracle (oracle/liboracle.so). TEST INFRASTRUCTURE ONLY."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+FRAG_DT = np.dtype([("data_off", "<u8"), ("len", "<u4"), ("stored_crc", "<u4"), ("type", "u1"), ("crc_ok", "u1"),
+                    ("pad", "u1", 6)])
+REC_DT = np.dtype([("foff", "<u8"), ("size", "<u8"), ("expire", "<u8"), ("key_len", "<u8"), ("val_len", "<u8"),
+                   ("meta_len", "<u8"), ("first_frag", "<u4"), ("emit_frag", "<u4"), ("hdr_size", "u1"),
+                   ("flags", "u1"), ("etag_off", "u1"), ("status", "u1"), ("pad", "u1", 4)])
+assert FRAG_DT.itemsize == 24 and REC_DT.itemsize == 64
+
+
+def _build():
+    src = os.path.join(ORACLE_DIR, "bcw_oracle.c")
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+
+
+_build()
+lib = C.CDLL(LIB)
+vp = C.c_void_p
+lib.oc_compute_crc32.restype = C.c_uint32
+lib.oc_compute_crc32.argtypes = [vp, C.c_size_t]
+lib.oc_crc32c.restype = C.c_uint32
+lib.oc_crc32c.argtypes = [vp, C.c_size_t]
+lib.oc_crc32c_hw.restype = C.c_uint32
+lib.oc_crc32c_hw.argtypes = [vp, C.c_size_t]
+lib.oc_uvarint.restype = C.c_int
+lib.oc_uvarint.argtypes = [vp, C.c_size_t, C.POINTER(C.c_uint64)]
+lib.oc_put_uvarint.restype = C.c_int
+lib.oc_put_uvarint.argtypes = [vp, C.c_uint64]
+lib.oc_super_encode.argtypes = [vp, C.c_uint64, C.c_uint64]
+lib.oc_writer_new.restype = vp
+lib.oc_writer_new.argtypes = [C.c_uint64, C.c_uint64]
+lib.oc_writer_write.restype = C.c_uint64
+lib.oc_writer_write.argtypes = [vp, vp, C.c_size_t]
+lib.oc_writer_size.restype = C.c_uint64
+lib.oc_writer_size.argtypes = [vp]
+lib.oc_writer_data.restype = vp
+lib.oc_writer_data.argtypes = [vp]
+lib.oc_writer_free.argtypes = [vp]
+lib.oc_record_encode.restype = C.c_int64
+lib.oc_record_encode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, vp, C.c_size_t, vp, C.c_size_t, C.c_uint64,
+                                 C.c_int, vp, C.c_size_t, C.c_uint64]
+lib.oc_hint_encode.restype = C.c_size_t
+lib.oc_hint_encode.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, C.c_uint64, C.c_uint64, C.c_uint64]
+lib.oc_decode_segment.restype = vp
+lib.oc_decode_segment.argtypes = [vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int]
+lib.oc_decode_counts.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
+lib.oc_decode_frags.argtypes = [vp, vp]
+lib.oc_decode_recs.argtypes = [vp, vp]
+lib.oc_decode_bytes.argtypes = [vp, vp, vp]
+lib.oc_decode_free.argtypes = [vp]
+lib.oc_decode_fast.restype = C.c_uint64
+lib.oc_decode_fast.argtypes = [vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                               C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
+lib.oc_compact_append.restype = C.c_int64
+lib.oc_compact_append.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32,
+                                  C.c_uint32, vp, C.c_uint64, vp]
+lib.oc_hint_by_wal.restype = C.c_int64
+lib.oc_hint_by_wal.argtypes = [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
+lib.oc_synth_segment.restype = vp
+lib.oc_synth_segment.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                 C.c_uint64]
+
+
+def _ptr(a):
+    if isinstance(a, (bytes, bytearray)):
+        a = np.frombuffer(a, dtype=np.uint8)
+    return a.ctypes.data_as(vp) if a.size else None
+
+
+def compute_crc32(b: bytes) -> int:
+    return int(lib.oc_compute_crc32(_ptr(b), len(b)))
+
+
+def crc32c(b: bytes) -> int:
+    return int(lib.oc_crc32c(_ptr(b), len(b)))
+
+
+def crc32c_hw(b: bytes) -> int:
+    return int(lib.oc_crc32c_hw(_ptr(b), len(b)))
+
+
+def uvarint(b: bytes):
+    v = C.c_uint64()
+    n = lib.oc_uvarint(_ptr(b), len(b), C.byref(v))
+    return int(v.value), int(n)
+
+
+def put_uvarint(v: int) -> bytes:
+    buf = (C.c_uint8 * 10)()
+    n = lib.oc_put_uvarint(buf, v)
+    return bytes(buf[:n])
+
+
+class Writer:
+    """oc_writer: WAL file image (wal.go:490-553)."""
+
+    def __init__(self, create_time: int, base_time: int):
+        self.h = lib.oc_writer_new(create_time, base_time)
+
+    def write(self, rec: bytes) -> int:
+        return int(lib.oc_writer_write(self.h, _ptr(rec), len(rec)))
+
+    def size(self) -> int:
+        return int(lib.oc_writer_size(self.h))
+
+    def data(self) -> bytes:
+        n = self.size()
+        return C.string_at(lib.oc_writer_data(self.h), n)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib.oc_writer_free(self.h)
+            self.h = None
+
+
+def record_encode(ns: bytes, key: bytes, val: bytes, etag: bytes = b"", expire: int = 0, tombstone: bool = False,
+                  meta: bytes = b"", base_time: int = 0):
+    out = np.zeros(len(ns) + len(key) + len(val) + len(etag) + len(meta) + 64, dtype=np.uint8)
+    n = lib.oc_record_encode(_ptr(out), _ptr(ns), len(ns), _ptr(key), len(key), _ptr(val), len(val), _ptr(etag),
+                             len(etag), expire, int(tombstone), _ptr(meta), len(meta), base_time)
+    return None if n < 0 else bytes(out[:n])
+
+
+def hint_encode(ns: bytes, key: bytes, fid: int, off: int, size: int) -> bytes:
+    out = np.zeros(len(ns) + len(key) + 64, dtype=np.uint8)
+    n = lib.oc_hint_encode(_ptr(out), _ptr(ns), len(ns), _ptr(key), len(key), fid, off, size)
+    return bytes(out[:n])
+
+
+class Decoded:
+    def __init__(self, frags, recs, err_frag, err_class, payloads):
+        self.frags, self.recs, self.err_frag, self.err_class, self.payloads = frags, recs, err_frag, err_class, payloads
+
+
+def decode(seg, start_off: int, base_time: int, ns_size: int, etag_size: int, mode: int = 0,
+           want_bytes: bool = True) -> Decoded:
+    seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+    h = lib.oc_decode_segment(_ptr(seg), seg.size, start_off, base_time, ns_size, etag_size, mode)
+    nf, nr, ef, nb = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+    ec = C.c_int32()
+    lib.oc_decode_counts(h, C.byref(nf), C.byref(nr), C.byref(ef), C.byref(ec), C.byref(nb))
+    frags = np.zeros(nf.value, dtype=FRAG_DT)
+    recs = np.zeros(nr.value, dtype=REC_DT)
+    if nf.value:
+        lib.oc_decode_frags(h, frags.ctypes.data_as(vp))
+    if nr.value:
+        lib.oc_decode_recs(h, recs.ctypes.data_as(vp))
+    payloads = None
+    if want_bytes:
+        buf = np.zeros(max(nb.value, 1), dtype=np.uint8)
+        offs = np.zeros(nr.value + 1, dtype=np.uint64)
+        lib.oc_decode_bytes(h, buf.ctypes.data_as(vp), offs.ctypes.data_as(vp))
+        payloads = [bytes(buf[offs[i]:offs[i + 1]]) for i in range(nr.value)]
+    lib.oc_decode_free(h)
+    return Decoded(frags, recs, int(ef.value), int(ec.value), payloads)
+
+
+def decode_fast(seg, start_off, base_time, ns_size, etag_size):
+    seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+    ec = C.c_int32()
+    cs = C.c_uint64()
+    n = lib.oc_decode_fast(_ptr(seg), seg.size, start_off, base_time, ns_size, etag_size, C.byref(ec), C.byref(cs))
+    return int(n), int(ec.value), int(cs.value)
+
+
+def synth(target_bytes: int, max_records: int, seed: int, ns_size: int = 20, key_len: int = 100,
+          value_len: int = 4096, value_mode: int = 0, base_time: int = 1_700_000_000) -> bytes:
+    h = lib.oc_synth_segment(target_bytes, max_records, seed, ns_size, key_len, value_len, value_mode, base_time)
+    n = int(lib.oc_writer_size(h))
+    out = C.string_at(lib.oc_writer_data(h), n)
+    lib.oc_writer_free(h)
+    return out
+
+
+def hint_by_wal(seg, fid, start_off, base_time, ns_size, etag_size, create_time=None):
+    w = Writer(create_time if create_time is not None else base_time, base_time)
+    seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+    rc = lib.oc_hint_by_wal(w.h, fid, _ptr(seg), seg.size, start_off, base_time, ns_size, etag_size)
+    return rc, w.data()

@@ -1,0 +1,30 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libbcw.so on the device)")
+
+
+def gpu_available() -> bool:
+    try:
+        from bitcaskdb_amd import _lib
+        return _lib.lib.bcw_device_count() > 0
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    if not gpu_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    from bitcaskdb_amd import Context
+    c = Context(0)
+    yield c
+    c.close()

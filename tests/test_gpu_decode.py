@@ -1,0 +1,96 @@
+"""GPU decode parity: libbcw.so on the MI355X against the CPU oracle, bit-exact.
+
+Every comparison goes through the C-ABI (bcw_decode_segment / bcw_decode_fragments) on cuda:0."""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import cases
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_decode(ctx, data, p):
+    return ctx.decode(np.frombuffer(data, dtype=np.uint8), p["start_off"], p["base_time"], p["ns_size"],
+                      p["etag_size"], p["mode"], with_frags=True)
+
+
+def assert_parity(ctx, data, p, name=""):
+    ref = O.decode(data, p["start_off"], p["base_time"], p["ns_size"], p["etag_size"], p["mode"])
+    got = gpu_decode(ctx, data, p)
+    res = got.result
+    # segment level
+    assert res.err_class == ref.err_class, (name, res.err_class, ref.err_class)
+    if ref.err_class in (1, 2):
+        assert res.err_frag == ref.err_frag, (name, res.err_frag, ref.err_frag)
+        fr = ref.frags[ref.err_frag]
+        assert res.err_file_off == fr["data_off"] - 7
+    assert res.n_records == len(ref.recs), (name, res.n_records, len(ref.recs))
+    # fragments parsed by the iterator
+    nf = len(ref.frags)
+    gf = got.frags
+    if nf:
+        assert len(gf["data_off"]) >= nf
+        for col in ("data_off", "len", "stored_crc", "type"):
+            np.testing.assert_array_equal(gf[col][:nf], ref.frags[col], err_msg=f"{name}: frag {col}")
+        np.testing.assert_array_equal(gf["crc_ok"][:nf], ref.frags["crc_ok"], err_msg=f"{name}: frag crc_ok")
+    # records
+    t = got.table
+    r = ref.recs
+    for col in ("foff", "size", "first_frag", "emit_frag", "status", "hdr_size", "flags", "etag_off", "expire"):
+        np.testing.assert_array_equal(t[col].astype(np.uint64), r[col].astype(np.uint64), err_msg=f"{name}: {col}")
+    if p["mode"] == 0:
+        for col in ("key_len", "val_len", "meta_len"):
+            np.testing.assert_array_equal(t[col].astype(np.uint64), r[col] & 0xFFFFFFFF, err_msg=f"{name}: {col}")
+    else:
+        np.testing.assert_array_equal(t["key_len"].astype(np.uint64), r["key_len"] & 0xFFFFFFFF)
+        np.testing.assert_array_equal(t["aux0"], r["val_len"], err_msg=f"{name}: hint off")
+        np.testing.assert_array_equal(t["aux1"], r["meta_len"], err_msg=f"{name}: hint size")
+    # payload bytes of every record
+    for i in range(len(r)):
+        assert got.record_bytes(i) == ref.payloads[i], (name, i)
+    bad = np.nonzero(r["status"] != 0)[0]
+    assert res.first_bad_record == (int(bad[0]) if len(bad) else -1)
+    return got, ref
+
+
+@pytest.mark.parametrize("name", list(cases.ALL))
+def test_cases(ctx, name):
+    data, p = cases.ALL[name]()
+    assert_parity(ctx, data, p, name)
+
+
+def test_synth_config_a_fragment(ctx):
+    """config A shape (64 MiB would take the oracle ~0.3 s; use 8 MiB here)."""
+    data = O.synth(8 << 20, 0, 0x5EED)
+    got, ref = assert_parity(ctx, data, cases.params(), "synth8m")
+    assert got.result.err_class == 0 and (got.table["status"] == 0).all()
+
+
+def test_synth_zipf(ctx):
+    data = O.synth(24 << 20, 0, 42, value_mode=1)
+    assert_parity(ctx, data, cases.params(), "zipf24m")
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_corruption_fuzz(ctx, seed):
+    """random bit flips: same first failing fragment, error class and delivered records."""
+    rng = random.Random(seed)
+    base, p = cases.case_zipf(120, seed) if seed % 2 else cases.case_config_shape(120, 2000)
+    data = cases.corrupt(base, rng, nflips=1 + seed % 3)
+    assert_parity(ctx, data, p, f"fuzz{seed}")
+
+
+@pytest.mark.parametrize("cut", [0, 1, 6, 7, 39, 40, 41, 47, 48, 100, 32807, 32808, 32809])
+def test_truncations(ctx, cut):
+    data, p = cases.case_config_shape(20, 3000)
+    assert_parity(ctx, data[:cut] if cut < len(data) else data, p, f"cut{cut}")
+
+
+def test_empty_and_small(ctx):
+    for data in (b"", bytes(40), bytes(46), bytes(47)):
+        assert_parity(ctx, data, cases.params(), f"small{len(data)}")

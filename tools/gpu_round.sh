@@ -1,0 +1,44 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel-trace stats. Every GPU step has its
+# own time limit and the chain stops at the first failure.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+OUT=$R/gpurun_out
+mkdir -p "$OUT"
+STEPS=${STEPS:-tests,smoke,bench,prof}
+run() { echo "== $1 ($(date +%T))"; }
+if [[ $STEPS == *tests* ]]; then
+  run tests
+  timeout -k 10 420 python -m pytest tests -m gpu -x -q > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
+  tail -3 "$OUT/gpu_tests.log"
+fi
+if [[ $STEPS == *smoke* ]]; then
+  run smoke
+  timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -30 "$OUT/smoke.log"; exit 1; }
+  tail -2 "$OUT/smoke.log"
+fi
+if [[ $STEPS == *bench* ]]; then
+  run bench
+  timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1 || { tail -30 "$OUT/bench.log"; exit 1; }
+  tail -1 "$OUT/bench.log"
+fi
+if [[ $STEPS == *prof* ]]; then
+  run prof
+  export TMPDIR=/tmp
+  rm -rf "$OUT/prof"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 1; }
+  find "$OUT/prof" -name "*stats*" | head
+fi
+if [[ $STEPS == *pmc* ]]; then
+  run pmc
+  export TMPDIR=/tmp
+  for c in FETCH_SIZE WRITE_SIZE; do
+    rm -rf "$OUT/pmc_$c"
+    timeout -k 10 300 rocprofv3 --pmc $c -d "$OUT/pmc_$c" -o run --output-format csv -- \
+      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1 || { tail -30 "$OUT/pmc_$c.log"; exit 1; }
+  done
+  find "$OUT" -name "*counter_collection*" | head
+fi
+echo "== done ($(date +%T))"
