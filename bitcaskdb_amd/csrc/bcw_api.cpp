@@ -45,8 +45,9 @@ static inline uint32_t apply_basis(const uint32_t* img, uint32_t x) {
   return r;
 }
 
-// fwd[l][i][n] = F_l(n << 4i), F_l = A_{8*128*(63-l)};  carry[i][n] = A_{8*8192}(n << 4i)
-void build_lane_tables(uint32_t* fwd, uint32_t* carry) {
+// fwd[l][i][n] = F_l(n << 4i), F_l = A_{8*128*(63-l)};  carry[i][n] = A_{8*8192}(n << 4i);
+// half[i][n] = A_{8*64}(n << 4i)
+void build_lane_tables(uint32_t* fwd, uint32_t* carry, uint32_t* half) {
   uint32_t t0[256];
   byte_table(t0);
   uint32_t step128[32];
@@ -62,6 +63,10 @@ void build_lane_tables(uint32_t* fwd, uint32_t* carry) {
   shift_basis(t0, 8192, c8k);
   for (int i = 0; i < 8; ++i)
     for (uint32_t n = 0; n < 16; ++n) carry[i * 16 + n] = apply_basis(c8k, n << (4 * i));
+  uint32_t h64[32];
+  shift_basis(t0, 64, h64);
+  for (int i = 0; i < 8; ++i)
+    for (uint32_t n = 0; n < 16; ++n) half[i * 16 + n] = apply_basis(h64, n << (4 * i));
 }
 
 // initc[L] = A_{8L}(0xFFFFFFFF): the contribution of the CRC init value after L data bytes
@@ -197,18 +202,20 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
     c->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return BCW_E_HIP; }
   c->cur = c->own;
-  std::vector<uint32_t> slice(512), fwd(64 * 128), carry(128), initc(kBlock + 1);
+  std::vector<uint32_t> slice(512), fwd(64 * 128), carry(128), half(128), initc(kBlock + 1);
   build_slice_tables(slice.data());
-  build_lane_tables(fwd.data(), carry.data());
+  build_lane_tables(fwd.data(), carry.data(), half.data());
   build_initc(initc.data());
   bool ok = hipMalloc(&c->tabs.slice, slice.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.fwd, fwd.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.carry, carry.size() * 4) == hipSuccess &&
+            hipMalloc(&c->tabs.half, half.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.initc, initc.size() * 4) == hipSuccess &&
             hipMalloc(&c->d_result, sizeof(bcw_decode_result)) == hipSuccess;
   ok = ok && hipMemcpy(c->tabs.slice, slice.data(), slice.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.fwd, fwd.data(), fwd.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.carry, carry.data(), carry.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(c->tabs.half, half.data(), half.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.initc, initc.data(), initc.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
   if (!ok) { bcw_ctx_destroy(c); return BCW_E_NOMEM; }
   *out = c;
@@ -216,11 +223,11 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
 }
 
 static void free_scratch(Scratch& s) {
-  (void)hipFree(s.nfrag);
   (void)hipFree(s.fbase);
+  (void)hipFree(s.wgsum);
   (void)hipFree(s.frags);
-  (void)hipFree(s.sums);
-  (void)hipFree(s.ins);
+  (void)hipFree(s.pre);
+  (void)hipFree(s.wgagg);
   (void)hipFree(s.misc);
   s = Scratch{};
 }
@@ -233,6 +240,7 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   (void)hipFree(c->tabs.slice);
   (void)hipFree(c->tabs.fwd);
   (void)hipFree(c->tabs.carry);
+  (void)hipFree(c->tabs.half);
   (void)hipFree(c->tabs.initc);
   (void)hipFree(c->d_seg);
   (void)hipFree(c->d_tab_mem);
@@ -263,10 +271,11 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   const uint64_t nb = std::max(nblocks, s.nblocks_cap);
   const uint64_t fc = std::max(frag_cap, s.frag_cap);
   free_scratch(s);
-  bool ok = hipMalloc(&s.nfrag, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess &&
+  const uint64_t nwg = nb / 256 + 2;
+  bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.wgsum, nwg * 4) == hipSuccess &&
             hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
-            hipMalloc(&s.sums, (nb + 1) * sizeof(BlockSum)) == hipSuccess &&
-            hipMalloc(&s.ins, (nb + 1) * sizeof(BlockIn)) == hipSuccess &&
+            hipMalloc(&s.pre, (nb + 1) * sizeof(Xf)) == hipSuccess &&
+            hipMalloc(&s.wgagg, nwg * sizeof(Xf)) == hipSuccess &&
             hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;
@@ -318,8 +327,8 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
   return launch_export_frags(c->s, *d_frags, c->last_start_off, c->cur, n) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_chase_count", "k_scan_u32", "k_chase_write", "k_crc",
-                                          "k_blocksum", "k_blockscan", "k_records", "k_finalize"};
+static const char* kKernelNames[K_NUM] = {"k_chase_count", "k_scan_wg", "k_chase_write", "k_crc",
+                                          "k_blocksum", "k_xscan_wg", "k_records", "k_finalize"};
 
 int bcw_ctx_set_profiling(bcw_ctx* c, int on) {
   if (!c) return BCW_E_INVAL;

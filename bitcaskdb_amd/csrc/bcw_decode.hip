@@ -1,14 +1,16 @@
 // bcw_decode.hip -- MI355X (gfx950) kernels for bitcaskDB WAL segment decode + CRC verify.
 //
 // Pipeline (one HIP stream, no host synchronisation inside; DESIGN.md "decode pipeline"):
-//   k_chase(count)   one lane per 32 KiB block: header chase        wal_iterator.go:45-77
-//   k_scan_u32       exclusive scan of fragments per block -> global fragment index
-//   k_chase(write)   second chase (headers now cache-resident): compact fragment table
+//   k_chase_count    one lane per 32 KiB block: header chase, workgroup scan of fragment counts
+//                    (wal_iterator.go:45-77)
+//   k_scan_wg        scan of the workgroup totals -> global fragment index of every block
+//   k_chase_write    second chase (headers now cache-resident): compact fragment table
 //   k_crc            per-fragment masked CRC-32C verify as a zero test  wal_iterator.go:79 /
 //                    utils.go:24-29 (LDS slice-by-2 tables, 128 B window per lane, lane
 //                    shift operators + segmented XOR scan across lanes)
 //   k_blocksum       per-block transform of the iterator's record state machine wal_iterator.go:69-96
-//   k_blockscan      composes the block transforms (one workgroup): record bases, first error
+//                    + workgroup scan of the transforms
+//   k_xscan_wg       scan of the workgroup aggregates: record bases, first error
 //   k_records        record emission + RecordFromBytes / HintRecord.Decode   record.go:140-239,
 //                    hint.go:50-84, one wave per block
 //   k_finalize       bcw_decode_result
@@ -50,25 +52,45 @@ __device__ __forceinline__ void read_header(const uint8_t* __restrict__ seg, uin
 }
 
 // ------------------------------------------------------------------------------------------
-// k_chase: WalIterator refill + header chase of one block (wal_iterator.go:45-77). The block's
-// buffer is min(32768, Size - fileOff) bytes; a header is parsed while bufOff + 7 <= bufSize;
-// the data length is clamped to the buffer. Pass 0 counts, pass 1 writes the compact table.
-__global__ __launch_bounds__(256) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len,
-                                               uint32_t start_off, uint64_t nblocks, uint32_t* __restrict__ nfrag,
-                                               const uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
-                                               uint64_t frag_cap, int write) {
-  const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
+// Workgroup-level exclusive scan helpers (256 threads = 4 waves).
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+// returns the exclusive prefix of v over the workgroup; *total = workgroup sum
+__device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t incl = wave_incl_scan_u32(v, lane);
+  if (lane == 63) sm4[wave] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t k = 0; k < wave; ++k) base += sm4[k];
+  total = sm4[0] + sm4[1] + sm4[2] + sm4[3];
+  __syncthreads();
+  return base + incl - v;
+}
+
+// ------------------------------------------------------------------------------------------
+// Header chase of one block: WalIterator refill + header loop (wal_iterator.go:45-77). The block's
+// buffer is min(32768, Size - fileOff) bytes; a header is parsed while bufOff + 7 <= bufSize; the
+// data length is clamped to the buffer.
+template <bool WRITE>
+__device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg, uint64_t seg_len,
+                                                uint32_t start_off, uint64_t b, Frag* __restrict__ frags,
+                                                uint64_t g0, uint64_t frag_cap) {
   const uint64_t boff = (uint64_t)start_off + b * kBlock;
   const uint32_t bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
   uint32_t h = 0, n = 0;
-  const uint64_t g0 = write ? fbase[b] : 0;
   while (h + kHdr <= bufsize) {
     uint32_t crc, len, type;
     read_header(seg, seg_len, boff + h, crc, len, type);
     const uint32_t start = h + kHdr;
     if (len > bufsize - start) len = bufsize - start;
-    if (write && g0 + n < frag_cap) {
+    if (WRITE && g0 + n < frag_cap) {
       Frag f;
       f.blk = (uint32_t)b;
       f.start = (uint16_t)start;
@@ -82,20 +104,33 @@ __global__ __launch_bounds__(256) void k_chase(const uint8_t* __restrict__ seg, 
     h = start + len;
     ++n;
   }
-  if (!write) nfrag[b] = n;
+  return n;
 }
 
-// ------------------------------------------------------------------------------------------
-// exclusive scan of a u32 array (one workgroup of 1024 threads); out[n] = total (saturated).
-__global__ __launch_bounds__(1024) void k_scan_u32(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                   uint64_t n, uint64_t* __restrict__ total) {
+// pass 1: count fragments per block, workgroup-local exclusive prefix -> fbase[b], wg totals
+__global__ __launch_bounds__(256) void k_chase_count(const uint8_t* __restrict__ seg, uint64_t seg_len,
+                                                     uint32_t start_off, uint64_t nblocks,
+                                                     uint32_t* __restrict__ fbase, uint32_t* __restrict__ wgsum) {
+  __shared__ uint32_t sm4[4];
+  const uint64_t b = blockIdx.x * 256ull + threadIdx.x;
+  const uint32_t n = b < nblocks ? chase_block<false>(seg, seg_len, start_off, b, nullptr, 0, 0) : 0u;
+  uint32_t tot;
+  const uint32_t ex = wg256_excl_scan(n, sm4, tot);
+  if (b < nblocks) fbase[b] = ex;
+  if (threadIdx.x == 0) wgsum[blockIdx.x] = tot;
+}
+
+// exclusive scan of the per-workgroup totals (one workgroup); fbase[nblocks] = total
+__global__ __launch_bounds__(1024) void k_scan_wg(uint32_t* __restrict__ wgsum, uint64_t nwg,
+                                                  uint32_t* __restrict__ fbase, uint64_t nblocks,
+                                                  uint64_t* __restrict__ total) {
   __shared__ uint64_t sm[1024];
   const uint32_t t = threadIdx.x;
-  const uint64_t per = (n + 1023) / 1024;
+  const uint64_t per = (nwg + 1023) / 1024;
   const uint64_t lo = t * per;
-  const uint64_t hi = lo + per < n ? lo + per : n;
+  const uint64_t hi = lo + per < nwg ? lo + per : nwg;
   uint64_t s = 0;
-  for (uint64_t i = lo; i < hi; ++i) s += in[i];
+  for (uint64_t i = lo; i < hi; ++i) s += wgsum[i];
   sm[t] = s;
   __syncthreads();
   for (uint32_t d = 1; d < 1024; d <<= 1) {
@@ -106,25 +141,39 @@ __global__ __launch_bounds__(1024) void k_scan_u32(const uint32_t* __restrict__ 
   }
   uint64_t run = sm[t] - s;
   for (uint64_t i = lo; i < hi; ++i) {
-    out[i] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
-    run += in[i];
+    const uint32_t x = wgsum[i];
+    wgsum[i] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
+    run += x;
   }
   if (t == 1023) {
     const uint64_t tot = sm[1023];
-    out[n] = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
+    fbase[nblocks] = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
     *total = tot;
   }
+}
+
+// pass 2: fbase[b] = workgroup base + local prefix; chase again (headers cache-resident), write
+__global__ __launch_bounds__(256) void k_chase_write(const uint8_t* __restrict__ seg, uint64_t seg_len,
+                                                     uint32_t start_off, uint64_t nblocks,
+                                                     uint32_t* __restrict__ fbase, const uint32_t* __restrict__ wgbase,
+                                                     Frag* __restrict__ frags, uint64_t frag_cap) {
+  const uint64_t b = blockIdx.x * 256ull + threadIdx.x;
+  if (b >= nblocks) return;
+  const uint32_t g0 = fbase[b] + wgbase[blockIdx.x];
+  fbase[b] = g0;
+  chase_block<true>(seg, seg_len, start_off, b, frags, g0, frag_cap);
 }
 
 // ------------------------------------------------------------------------------------------
 // k_crc: per-fragment CRC verify.
 //
-// For fragment f with data [s, e) (block-relative) let E = 4*ceil(e/4) + 4 and tile [E-128C, E)
-// with C = ceil((E - s)/128) windows of 128 B. A raw (init 0) CRC-32C chain over the windows,
-// with the bytes before s zeroed and the bytes [e, e+4) replaced by
-//     J = ~unmask(stored) ^ A_{8L}(0xFFFFFFFF)          (L = e - s)
+// For fragment f with data at global offsets [gs, ge) let GE = 16*ceil((ge + 4)/16) and tile
+// [GE-128C, GE) with C = ceil((GE - gs)/128) windows of 128 B (16 B aligned). A raw (init 0)
+// CRC-32C chain over the windows, with the bytes before gs zeroed and the bytes [ge, ge+4)
+// replaced by
+//     J = ~unmask(stored) ^ A_{8L}(0xFFFFFFFF)          (L = ge - gs)
 // and zeros after, ends in state 0 exactly when ComputeCRC32(data) == stored (linearity of CRC:
-// the init 0xFFFFFFFF contributes A_{8L}(~0) at e, the XOR-out is folded into ~unmask). So the
+// the init 0xFFFFFFFF contributes A_{8L}(~0) at ge, the XOR-out is folded into ~unmask). So the
 // CRC check becomes a zero test of a linear functional, and windows can be computed by separate
 // lanes and combined with fixed shift operators:
 //   * head pass: lane i processes the first window of fragment i (prefix masking); if C == 1 it
@@ -135,15 +184,23 @@ __global__ __launch_bounds__(1024) void k_scan_u32(const uint32_t* __restrict__ 
 //     with F_l = A_{8*128*(63-l)} (lane-replicated nibble tables), a segmented XOR scan combines
 //     the fragment's windows, and the lane holding the last window tests the total for zero.
 //     A fragment continuing past lane 63 carries its value to the next pass (shift A_{8*8192}).
-constexpr int kCrcWaves = 16;
+//     Each window runs as two independent 64 B half-chains joined by A_{8*64}; the next pass's
+//     descriptors and window loads are issued before the current pass's chains (software pipeline).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kCrcWaves = 12;
+constexpr int kCrcThreads = kCrcWaves * 64;
 constexpr int kLdsSlice = 2 * 256 * 32;  // dwords, slice-by-2 tables replicated x32 (64 KiB)
 constexpr int kLdsFwd = 8 * 16 * 64;     // dwords, lane operators (32 KiB)
-constexpr int kLdsCarry = 8 * 16;        // dwords
-constexpr int kSlots = 128;              // fragment slots per wave (two windows of 64)
-constexpr int kSlotWords = 5;            // cpre, blk, se, J, V1
-constexpr size_t kCrcLds = (size_t)(kLdsSlice + kLdsFwd + kLdsCarry + kCrcWaves * kSlots * kSlotWords) * 4;
-
-__device__ __forceinline__ uint32_t lds_tab(const uint32_t* __restrict__ t, uint32_t idx) { return t[idx]; }
+constexpr int kLdsOps = 2 * 8 * 16;      // dwords, carry A_{8*8192} and half A_{8*64} operators
+constexpr int kRing = 128;               // ring of multi-window fragments per wave
+constexpr int kRingWords = 7;            // cpre, cend, blk, se, J, V1, fragment index
+constexpr int kWaveLds = kRing * kRingWords + 64;  // + 64 pass markers
+constexpr size_t kCrcLds = (size_t)(kLdsSlice + kLdsFwd + kLdsOps + kCrcWaves * kWaveLds) * 4;
 
 // slice-by-2 step on the low 16 bits of h: T0 = byte table, T1 = one byte further
 __device__ __forceinline__ uint32_t step16(const uint32_t* __restrict__ tab, uint32_t lo, uint32_t s, uint32_t h) {
@@ -156,10 +213,6 @@ __device__ __forceinline__ uint32_t step32(const uint32_t* __restrict__ tab, uin
   s = step16(tab, lo, s, w & 0xffffu);
   return step16(tab, lo, s, w >> 16);
 }
-// advance by one byte
-__device__ __forceinline__ uint32_t step8(const uint32_t* __restrict__ tab, uint32_t lo, uint32_t s, uint32_t b) {
-  return (s >> 8) ^ tab[(((s ^ b) & 0xffu)) << 5 | lo];
-}
 // F_l(x): lane-replicated nibble images, lane l reads its own copy (bank = l % 32)
 __device__ __forceinline__ uint32_t apply_fwd(const uint32_t* __restrict__ fwd, uint32_t lane, uint32_t x) {
   uint32_t r = 0;
@@ -167,81 +220,161 @@ __device__ __forceinline__ uint32_t apply_fwd(const uint32_t* __restrict__ fwd, 
   for (int i = 0; i < 8; ++i) r ^= fwd[((i * 16 + ((x >> (4 * i)) & 15u)) << 6) | lane];
   return r;
 }
-__device__ __forceinline__ uint32_t apply_carry(const uint32_t* __restrict__ c, uint32_t x) {
+// uniform operator (one 8x16 nibble table shared by all lanes: 16 distinct banks per lookup)
+__device__ __forceinline__ uint32_t apply_op(const uint32_t* __restrict__ c, uint32_t x) {
   uint32_t r = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) r ^= c[i * 16 + ((x >> (4 * i)) & 15u)];
   return r;
 }
 
-// 16 bytes at seg[o..o+16), zero outside [0, seg_len)
-__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t o) {
-  if (o >= 0 && (uint64_t)o + 16 <= seg_len) return *reinterpret_cast<const uint4*>(seg + o);
-  uint32_t w[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t p = o + 4 * k + i;
-      const uint32_t byte = (p >= 0 && (uint64_t)p < seg_len) ? seg[p] : 0u;
-      v |= byte << (8 * i);
-    }
-    w[k] = v;
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
+// ---- wave-level scans on DPP (row_shr 1/2/4/8, row_bcast 15/31), no LDS round trips ----
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
 }
-
-__device__ __forceinline__ void load_window(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t goff,
-                                            uint32_t (&w)[32]) {
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    const uint4 v = load16(seg, seg_len, goff + 16 * g);
-    w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
-  }
+__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v, uint32_t lane) {
+  const uint32_t rl = lane & 15u;
+  uint32_t t;
+  t = dpp_mov<0x111>(v); if (rl >= 1u) v = max(v, t);
+  t = dpp_mov<0x112>(v); if (rl >= 2u) v = max(v, t);
+  t = dpp_mov<0x114>(v); if (rl >= 4u) v = max(v, t);
+  t = dpp_mov<0x118>(v); if (rl >= 8u) v = max(v, t);
+  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v = max(v, t);
+  t = dpp_mov<0x143>(v); if (lane >= 32u) v = max(v, t);
+  return v;
 }
-
-// last-window fix: keep bytes < hi of words 30/31, put J at [hi, hi+4), zero the rest.
-__device__ __forceinline__ void fix_last(uint32_t (&w)[32], uint32_t hi, uint32_t J) {
-  const uint32_t r = hi - 120u;  // 1..4
-  uint64_t d = (uint64_t)w[30] | ((uint64_t)w[31] << 32);
-  const uint64_t keep = (1ull << (8 * r)) - 1ull;
-  d = (d & keep) | ((uint64_t)J << (8 * r));
-  w[30] = (uint32_t)d;
-  w[31] = (uint32_t)(d >> 32);
+// segmented inclusive XOR scan; seg = first lane of this lane's segment
+__device__ __forceinline__ uint32_t wave_seg_xor_scan(uint32_t v, uint32_t lane, uint32_t seg) {
+  const uint32_t rl = lane & 15u;
+  uint32_t t;
+  t = dpp_mov<0x111>(v); if (rl >= 1u && lane - 1u >= seg) v ^= t;
+  t = dpp_mov<0x112>(v); if (rl >= 2u && lane - 2u >= seg) v ^= t;
+  t = dpp_mov<0x114>(v); if (rl >= 4u && lane - 4u >= seg) v ^= t;
+  t = dpp_mov<0x118>(v); if (rl >= 8u && lane - 8u >= seg) v ^= t;
+  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u && (lane & ~15u) - 1u >= seg) v ^= t;  // from lane 15 / 47
+  t = dpp_mov<0x143>(v); if (lane >= 32u && 31u >= seg) v ^= t;                       // from lane 31
+  return v;
 }
-
-__device__ __forceinline__ uint32_t wave_incl_scan_add(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += t;
-  }
+__device__ __forceinline__ uint32_t wave_add_scan(uint32_t v, uint32_t lane) {
+  const uint32_t rl = lane & 15u;
+  uint32_t t;
+  t = dpp_mov<0x111>(v); if (rl >= 1u) v += t;
+  t = dpp_mov<0x112>(v); if (rl >= 2u) v += t;
+  t = dpp_mov<0x114>(v); if (rl >= 4u) v += t;
+  t = dpp_mov<0x118>(v); if (rl >= 8u) v += t;
+  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v += t;
+  t = dpp_mov<0x143>(v); if (lane >= 32u) v += t;
   return v;
 }
 
-__global__ __launch_bounds__(1024) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
-                                              uint64_t nblocks, const uint32_t* __restrict__ fbase,
-                                              Frag* __restrict__ frags, uint64_t frag_cap, Tables tabs) {
+// bounds-checked 16 B load, out of line (rare: the segment's first/last bytes)
+__device__ __noinline__ uint4 load16_slow(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t o) {
+  uint64_t lo = 0, hi = 0;
+#pragma unroll 1
+  for (int i = 0; i < 16; ++i) {
+    const int64_t q = o + i;
+    const uint64_t byte = (q >= 0 && (uint64_t)q < seg_len) ? seg[q] : 0u;
+    if (i < 8) lo |= byte << (8 * i); else hi |= byte << (8 * (i - 8));
+  }
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+__device__ __forceinline__ uint4 load16_safe(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t o) {
+  if (o >= 0 && (uint64_t)o + 16 <= seg_len) return *reinterpret_cast<const uint4*>(seg + o);
+  return load16_slow(seg, seg_len, o);
+}
+
+// 128 B window at seg + goff into w[32]; `inb` (wave-uniform): every active lane's window is in bounds
+__device__ __forceinline__ void load_window(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t goff, bool inb,
+                                            uint32_t (&w)[32]) {
+  if (inb) {
+    const uint4* q = reinterpret_cast<const uint4*>(seg + goff);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const uint4 v = q[g];
+      w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const uint4 v = load16_safe(seg, seg_len, goff + 16 * g);
+      w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+    }
+  }
+}
+
+// last-window fix: keep bytes < hi (hi in [109,124]), put J at [hi, hi+4), zero the rest
+// (touches words 27..31 only); branch-free per word
+__device__ __forceinline__ void fix_last(uint32_t (&w)[32], uint32_t hi, uint32_t J) {
+#pragma unroll
+  for (int k = 27; k < 32; ++k) {
+    const int t = (int)hi - 4 * k;                       // byte index of hi relative to the word
+    const int tk = t < 0 ? 0 : (t > 4 ? 4 : t);           // bytes kept
+    const uint32_t keep = (uint32_t)((1ull << (8 * tk)) - 1ull);
+    const uint64_t jw = (uint64_t)J << 32;                // J at byte 4 of a 64-bit lane
+    const int sh = 32 - 8 * t;                            // J byte 0 lands at byte t
+    const uint32_t jp = (t > -4 && t < 4) ? (uint32_t)(sh >= 0 ? (jw >> sh) : (jw << -sh)) : 0u;
+    w[k] = (w[k] & keep) | jp;
+  }
+}
+
+// global window geometry of a fragment (block-relative s, e)
+struct FragGeo {
+  int64_t gs, GE;
+  uint32_t C;
+};
+__device__ __forceinline__ FragGeo frag_geo(uint32_t start_off, uint32_t blk, uint32_t s, uint32_t e) {
+  const int64_t boff = (int64_t)start_off + (int64_t)blk * kBlock;
+  FragGeo g;
+  g.gs = boff + s;
+  const int64_t ge = boff + e;
+  g.GE = (ge + 4 + 15) & ~(int64_t)15;
+  g.C = (uint32_t)((g.GE - g.gs + 127) >> 7);
+  return g;
+}
+
+// one body-pass lane: which window, where, how to seed and finish it
+struct BodyDesc {
+  int64_t goff;     // global offset of the 128 B window
+  uint32_t hi;      // last window: byte index of the data end (else 0)
+  uint32_t J;
+  uint32_t seed;    // first body window: head-window end state; else 0
+  uint32_t cfb;     // index among the fragment's body windows
+  uint64_t gfrag;   // global fragment index
+  bool active, last;
+};
+
+// ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
+// 4 no lane-operator / scan combine
+template <int ABL = 0>
+__global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
+                                                     uint32_t start_off, uint64_t nblocks,
+                                                     const uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
+                                                     uint64_t frag_cap, Tables tabs) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* s_slice = lds;
   uint32_t* s_fwd = lds + kLdsSlice;
   uint32_t* s_carry = s_fwd + kLdsFwd;
-  uint32_t* s_slots_all = s_carry + kLdsCarry;
+  uint32_t* s_half = s_carry + 128;
+  uint32_t* s_wave_all = s_carry + kLdsOps;
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < (uint32_t)kLdsSlice; i += 1024) s_slice[i] = tabs.slice[i >> 5];
-  for (uint32_t i = tid; i < (uint32_t)kLdsFwd; i += 1024) s_fwd[i] = tabs.fwd[(i & 63u) * 128u + (i >> 6)];
-  if (tid < (uint32_t)kLdsCarry) s_carry[tid] = tabs.carry[tid];
+  for (uint32_t i = tid; i < (uint32_t)kLdsSlice; i += kCrcThreads) s_slice[i] = tabs.slice[i >> 5];
+  for (uint32_t i = tid; i < (uint32_t)kLdsFwd; i += kCrcThreads) s_fwd[i] = tabs.fwd[(i & 63u) * 128u + (i >> 6)];
+  if (tid < 128u) s_carry[tid] = tabs.carry[tid];
+  else if (tid < 256u) s_half[tid - 128u] = tabs.half[tid - 128u];
   __syncthreads();
 
   const uint32_t lane = tid & 63u;
   const uint32_t lo = lane & 31u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t* s_cpre = s_slots_all + wave * kSlots * kSlotWords;
-  uint32_t* s_blk = s_cpre + kSlots;
-  uint32_t* s_se = s_blk + kSlots;
-  uint32_t* s_J = s_se + kSlots;
-  uint32_t* s_V1 = s_J + kSlots;
+  uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of multi-window fragments
+  uint32_t* r_cend = r_cpre + kRing;
+  uint32_t* r_blk = r_cend + kRing;
+  uint32_t* r_se = r_blk + kRing;
+  uint32_t* r_J = r_se + kRing;
+  uint32_t* r_V1 = r_J + kRing;
+  uint32_t* r_fi = r_V1 + kRing;
+  uint32_t* s_mark = r_fi + kRing;                   // 64 pass markers
 
   const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
   const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
@@ -253,185 +386,186 @@ __global__ __launch_bounds__(1024) void k_crc(const uint8_t* __restrict__ seg, u
   const uint32_t nfr = (uint32_t)(f1 - f0);
   const uint32_t nwin = (nfr + 63u) / 64u;
 
-  // load fragment window k (64 fragments) into slot half (k & 1); run its head pass.
-  // returns the exclusive body-chunk prefix after the window.
-  auto load_win = [&](uint32_t k, uint32_t cbase) -> uint32_t {
-    const uint32_t half = (k & 1u) * 64u;
-    const uint32_t fi = k * 64u + lane;
-    uint32_t cb = 0, s = 0, e = 0, E = 0, J = 0, blk = 0, C = 1;
+  uint32_t r_head = 0, r_tail = 0;  // absolute ring positions (wave-uniform)
+  uint32_t cbase = 0;               // body chunks appended so far
+  uint32_t kwin = 0;                // next fragment window to load
+
+  // Fragment window kwin (64 fragments): head pass for every fragment (first window; C == 1
+  // fragments are finished here), then the fragments with body windows are appended to the ring.
+  // w: a dead 32-word buffer (the pipeline buffer about to be refilled).
+  auto load_win = [&](uint32_t (&w)[32]) {
+    const uint32_t fi = kwin * 64u + lane;
+    ++kwin;
+    uint32_t cb = 0, s = 0, e = 0, J = 0, blk = 0;
+    FragGeo geo{0, 0, 1};
     const bool valid = fi < nfr;
-    Frag f;
     if (valid) {
-      f = frags[f0 + fi];
+      const Frag f = frags[f0 + fi];
       s = f.start;
       e = (uint32_t)f.start + f.len;
-      E = ((e + 3u) & ~3u) + 4u;
-      C = (E - s + 127u) >> 7;
-      cb = C - 1u;
+      blk = f.blk;
+      geo = frag_geo(start_off, blk, s, e);
+      cb = geo.C - 1u;
       const uint32_t crc = rotl32(f.crc - 0xa282ead8u, 15);
       J = ~crc ^ tabs.initc[f.len];
-      blk = f.blk;
     }
-    const uint32_t incl = wave_incl_scan_add(cb, lane);
-    const uint32_t tot = __shfl(incl, 63, 64);
-    s_cpre[half + lane] = valid ? cbase + incl - cb : 0xffffffffu;
-    s_blk[half + lane] = blk;
-    s_se[half + lane] = s | (e << 16);
-    s_J[half + lane] = J;
-    // head pass: first window [E - 128C, E - 128C + 128)
     uint32_t V = 0;
+    const int64_t wst = geo.GE - 128 * (int64_t)geo.C;
+    const bool inb = __all(!valid || (wst >= 0 && (uint64_t)wst + 128 <= seg_len));
     if (valid) {
-      const int64_t wst = (int64_t)E - 128 * (int64_t)C;
-      const int64_t goff = (int64_t)start_off + (int64_t)blk * kBlock + wst;
-      uint32_t w[32];
-      load_window(seg, seg_len, goff, w);
-      const int32_t lo8 = 8 * (int32_t)((int64_t)s - wst);  // 8 * lo, lo in [0,128)
+      load_window(seg, seg_len, wst, inb, w);
+      const int32_t lo8 = 8 * (int32_t)(geo.gs - wst);  // 8 * lo, lo in [0,128)
 #pragma unroll
       for (int k2 = 0; k2 < 32; ++k2) {
         int32_t sh = lo8 - 32 * k2;
         sh = sh < 0 ? 0 : (sh > 32 ? 32 : sh);
-        const uint32_t m = (uint32_t)(0xffffffffffffffffull << sh);
-        w[k2] &= m;
+        w[k2] &= (uint32_t)(0xffffffffffffffffull << sh);
       }
-      if (C == 1u) fix_last(w, (uint32_t)((int64_t)e - wst), J);
-      uint32_t S = 0;
+      if (geo.C == 1u) fix_last(w, (uint32_t)(geo.gs + (int64_t)(e - s) - wst), J);
+      uint32_t Sa = 0, Sb = 0;
 #pragma unroll
-      for (int k2 = 0; k2 < 32; ++k2) S = step32(s_slice, lo, S, w[k2]);
-      V = S;
-      if (C == 1u) frags[f0 + fi].ok = (S == 0u) ? 1 : 0;
+      for (int k2 = 0; k2 < 16; ++k2) {
+        Sa = step32(s_slice, lo, Sa, w[k2]);
+        Sb = step32(s_slice, lo, Sb, w[16 + k2]);
+      }
+      V = apply_op(s_half, Sa) ^ Sb;
+      if (geo.C == 1u) frags[f0 + fi].ok = (V == 0u) ? 1 : 0;
     }
-    s_V1[half + lane] = V;
-    return cbase + tot;
+    // append fragments with body windows to the ring
+    const bool multi = valid && cb > 0u;
+    const uint64_t mm = __ballot(multi);
+    const uint32_t below = lane == 0 ? 0u : (uint32_t)__builtin_popcountll(mm & (~0ull >> (64 - lane)));
+    const uint32_t incl = wave_add_scan(cb, lane);
+    const uint32_t tot = __shfl(incl, 63, 64);
+    if (multi) {
+      const uint32_t a = (r_tail + below) & (kRing - 1);
+      r_cpre[a] = cbase + incl - cb;
+      r_cend[a] = cbase + incl;
+      r_blk[a] = blk;
+      r_se[a] = s | (e << 16);
+      r_J[a] = J;
+      r_V1[a] = V;
+      r_fi[a] = fi;
+    }
+    r_tail += (uint32_t)__builtin_popcountll(mm);
+    cbase += __builtin_amdgcn_readfirstlane(tot);
+    wave_sync();
   };
 
-  uint32_t kA = 0;
-  uint32_t cA_end = load_win(0, 0);
-  uint32_t cB_end = nwin > 1 ? load_win(1, cA_end) : cA_end;
-  if (nwin <= 1) {
-    s_cpre[64 + lane] = 0xffffffffu;
-  }
-  uint32_t carry = 0;
-  for (uint32_t pass = 0;; pass += 64u) {
-    while (cA_end <= pass && kA + 1u < nwin) {
-      ++kA;
-      cA_end = cB_end;
-      if (kA + 1u < nwin) cB_end = load_win(kA + 1u, cB_end);
-      else s_cpre[((kA + 1u) & 1u) * 64u + lane] = 0xffffffffu;
+  // make the ring hold every fragment owning a chunk of [pass, pass+64)
+  auto advance = [&](uint32_t pass, uint32_t (&scratch)[32]) {
+    auto evict = [&]() {
+      while (r_head < r_tail && (uint32_t)__builtin_amdgcn_readfirstlane(r_cend[r_head & (kRing - 1)]) <= pass)
+        ++r_head;
+    };
+    evict();
+    while (kwin < nwin && cbase < pass + 64u) {
+      load_win(scratch);
+      evict();
     }
-    if (pass >= cB_end) break;
+  };
+
+  auto describe = [&](uint32_t pass) -> BodyDesc {
+    BodyDesc d{};
     const uint32_t j = pass + lane;
-    const bool active = j < cB_end;
-    const uint32_t hA = (kA & 1u) * 64u, hB = 64u - hA;
-    // largest virtual index i in [0,128) with cpre(i) <= j (window A first, then B)
-    uint32_t i = 0;
+    // markers: ring entries whose first body chunk falls in this pass
+    wave_sync();
+    s_mark[lane] = 0;
+    wave_sync();
 #pragma unroll
-    for (uint32_t st = 64; st >= 1; st >>= 1) {
-      const uint32_t c = i + st;
-      if (c < 128u) {
-        const uint32_t slot = c < 64u ? hA + c : hB + (c - 64u);
-        if (s_cpre[slot] <= j) i = c;
+    for (uint32_t q = 0; q < 2; ++q) {
+      const uint32_t a = r_head + lane + 64u * q;
+      if (a < r_tail) {
+        const uint32_t c = r_cpre[a & (kRing - 1)];
+        if (c >= pass && c < pass + 64u) s_mark[c - pass] = ((c - pass + 1u) << 16) | (a - r_head + 1u);
       }
     }
-    const uint32_t slot = i < 64u ? hA + i : hB + (i - 64u);
-    uint32_t v = 0, cfb = 0;
-    bool is_last = false;
-    if (active) {
-      const uint32_t cpre = s_cpre[slot];
-      const uint32_t se = s_se[slot];
-      const uint32_t s = se & 0xffffu, e = se >> 16;
-      const uint32_t E = ((e + 3u) & ~3u) + 4u;
-      const uint32_t C = (E - s + 127u) >> 7;
-      cfb = j - cpre;                 // index among body windows, from the first
-      const uint32_t c = C - 2u - cfb; // windows from the end (0 = last)
-      is_last = (c == 0u);
-      const int64_t wst = (int64_t)E - 128 * (int64_t)(c + 1u);
-      const int64_t goff = (int64_t)start_off + (int64_t)s_blk[slot] * kBlock + wst;
-      uint32_t w[32];
-      load_window(seg, seg_len, goff, w);
-      if (is_last) fix_last(w, (uint32_t)((int64_t)e - wst), s_J[slot]);
-      uint32_t S = cfb == 0u ? s_V1[slot] : 0u;
+    wave_sync();
+    const uint32_t m = s_mark[lane];
+    const uint32_t hm = wave_max_scan(m, lane);
+    // lanes before the first marker continue the ring head (the fragment carried from the last pass)
+    const uint32_t a = r_head + (hm ? (hm & 0xffffu) - 1u : 0u);
+    d.active = j < cbase && a < r_tail;
+    if (!d.active) return d;
+    const uint32_t slot = a & (kRing - 1);
+    const uint32_t se = r_se[slot];
+    const uint32_t cpre = r_cpre[slot];
+    const FragGeo geo = frag_geo(start_off, r_blk[slot], se & 0xffffu, se >> 16);
+    d.cfb = j - cpre;
+    const uint32_t c = geo.C - 2u - d.cfb;  // windows from the end (0 = last)
+    d.last = c == 0u;
+    d.goff = geo.GE - 128 * (int64_t)(c + 1u);
+    const int64_t ge = geo.gs + (int64_t)((se >> 16) - (se & 0xffffu));
+    d.hi = d.last ? (uint32_t)(ge - d.goff) : 0u;
+    d.J = r_J[slot];
+    d.seed = d.cfb == 0u ? r_V1[slot] : 0u;
+    d.gfrag = f0 + r_fi[slot];
+    return d;
+  };
+
+  auto issue = [&](const BodyDesc& d, uint32_t (&w)[32]) {
+    if (ABL & 2) return;
+    const bool inb = __all(!d.active || (d.goff >= 0 && (uint64_t)d.goff + 128 <= seg_len));
+    if (d.active) load_window(seg, seg_len, d.goff, inb, w);
+  };
+
+  uint32_t carry = 0;  // fragment state at the end of the previous pass (lane 63)
+  auto compute = [&](const BodyDesc& d, uint32_t (&w)[32]) {
+    uint32_t v = 0;
+    if (d.active) {
+      if (d.last) fix_last(w, d.hi, d.J);
+      if (!(ABL & 1)) {
+        uint32_t Sa = d.seed, Sb = 0;
 #pragma unroll
-      for (int k2 = 0; k2 < 32; ++k2) S = step32(s_slice, lo, S, w[k2]);
-      v = apply_fwd(s_fwd, lane, S);
-      if (lane == 0 && cfb > 0u) v ^= apply_carry(s_carry, carry);
+        for (int k2 = 0; k2 < 16; ++k2) {
+          Sa = step32(s_slice, lo, Sa, w[k2]);
+          Sb = step32(s_slice, lo, Sb, w[16 + k2]);
+        }
+        v = apply_op(s_half, Sa) ^ Sb;
+      } else {
+        v = d.seed ^ w[0] ^ w[31];
+      }
+      // U-domain: lane l holds A_{1024(63-l)} of its window state; the pass carry enters at lane 0
+      if (!(ABL & 4)) v = apply_fwd(s_fwd, lane, v);
+      if (lane == 0u && d.cfb > 0u) v ^= apply_op(s_carry, carry);
     }
-    // segmented inclusive XOR scan: a lane's segment starts at lane - cfb (clamped to 0)
-    const uint32_t seg_start = active ? (cfb > lane ? 0u : lane - cfb) : lane;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t t = __shfl_up(v, d, 64);
-      if (lane >= (uint32_t)d && lane - (uint32_t)d >= seg_start) v ^= t;
+    uint32_t U = v;
+    if (!(ABL & 4)) {
+      const uint32_t segl = d.active ? (d.cfb > lane ? 0u : lane - d.cfb) : lane;
+      U = wave_seg_xor_scan(v, lane, segl);
     }
-    if (active && is_last) frags[f0 + (uint64_t)kA * 64u + i].ok = (v == 0u) ? 1 : 0;
-    carry = __shfl(v, 63, 64);
+    if (d.active && d.last) frags[d.gfrag].ok = (U == 0u) ? 1 : 0;
+    carry = __builtin_amdgcn_readlane(U, 63);
+  };
+
+  // software pipeline: the next pass's windows are in flight while this pass chains
+  uint32_t wx[32], wy[32];
+  uint32_t pass = 0;
+  advance(0u, wx);
+  BodyDesc dx = describe(0u), dy;
+  issue(dx, wx);
+  while (pass < cbase) {
+    advance(pass + 64u, wy);
+    dy = describe(pass + 64u);
+    issue(dy, wy);
+    compute(dx, wx);
+    pass += 64u;
+    if (pass >= cbase) break;
+    advance(pass + 64u, wx);
+    dx = describe(pass + 64u);
+    issue(dx, wx);
+    compute(dy, wy);
+    pass += 64u;
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// k_blocksum: the iterator's record state machine (wal_iterator.go:69-96) summarised per block.
-__global__ __launch_bounds__(256) void k_blocksum(const Frag* __restrict__ frags, const uint32_t* __restrict__ fbase,
-                                                  uint64_t nblocks, uint32_t start_off, uint64_t frag_cap,
-                                                  BlockSum* __restrict__ sums) {
-  const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
-  uint64_t g0 = fbase[b], g1 = fbase[b + 1];
-  if (g1 > frag_cap) g1 = frag_cap;
-  if (g0 > g1) g0 = g1;
-  BlockSum S{};
-  S.err_frag = 0xffffffffu;
-  bool in_pre = true;
-  uint64_t acc = 0, off = 0;
-  uint32_t first = 0;
-  for (uint64_t g = g0; g < g1; ++g) {
-    const Frag f = frags[g];
-    if (!f.ok) { S.err_class = BCW_ERR_CRC; S.err_frag = (uint32_t)g; break; }        // wal_iterator.go:79-82
-    if (f.type < 1 || f.type > 4) { S.err_class = BCW_ERR_TYPE; S.err_frag = (uint32_t)g; break; }  // :94-95
-    const uint64_t doff = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
-    if (in_pre) {
-      if (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST) {
-        in_pre = false;
-        S.has_emit = 1;
-        S.n_emit = 1;
-        acc = 0;
-        continue;
-      }
-      if (f.len > 0 && !S.pre_nz) { S.pre_nz = 1; S.pre_off = doff; S.pre_first = (uint32_t)g; }
-      S.pre_len += f.len;
-    } else {
-      if (acc == 0) { off = doff; first = (uint32_t)g; }
-      if (f.type == BCW_RECORD_FULL) { S.n_emit++; acc = 0; }
-      else if (f.type == BCW_RECORD_LAST) { S.n_emit++; acc = 0; }
-      else acc += f.len;
-    }
-  }
-  S.out_acc = acc;
-  S.out_off = off;
-  S.out_first = first;
-  sums[b] = S;
-}
+// Record assembly. The iterator's per-fragment state machine (wal_iterator.go:69-96: `off` is
+// captured while the accumulated record is empty; Full emits the Full's data with that offset;
+// First/Middle append; Last appends and emits; any other type is an error) is summarised per block
+// as a transform Xf of the incoming state (acc_len, off, first). Transforms compose associatively,
+// so block states come from a workgroup scan (k_blocksum) plus a scan of workgroup aggregates.
 
-// ------------------------------------------------------------------------------------------
-// k_blockscan: exclusive composition of block transforms (one workgroup).
-struct Xf {
-  uint64_t n_emit;
-  uint64_t a;      // has_emit: out acc    else: pre len
-  uint64_t off;    // has_emit: out off    else: pre off
-  uint32_t first;
-  uint32_t err_frag;
-  uint8_t has_emit, nz, err, err_class;
-};
-
-__device__ __forceinline__ Xf xf_of(const BlockSum& s) {
-  Xf x;
-  x.n_emit = s.n_emit;
-  x.has_emit = s.has_emit;
-  x.err = s.err_class != 0;
-  x.err_class = s.err_class;
-  x.err_frag = s.err_frag;
-  if (s.has_emit) { x.a = s.out_acc; x.off = s.out_off; x.first = s.out_first; x.nz = 0; }
-  else { x.a = s.pre_len; x.off = s.pre_off; x.first = s.pre_first; x.nz = s.pre_nz; }
-  return x;
-}
 __device__ __forceinline__ Xf xf_identity() {
   Xf x{};
   x.err_frag = 0xffffffffu;
@@ -441,6 +575,7 @@ __device__ __forceinline__ Xf xf_identity() {
 __device__ __forceinline__ Xf xf_compose(const Xf& A, const Xf& B) {
   if (A.err) return A;
   Xf R;
+  R.pad = 0;
   R.n_emit = A.n_emit + B.n_emit;
   R.err = B.err;
   R.err_class = B.err_class;
@@ -461,35 +596,90 @@ __device__ __forceinline__ Xf xf_compose(const Xf& A, const Xf& B) {
   return R;
 }
 
-__global__ __launch_bounds__(1024) void k_blockscan(const BlockSum* __restrict__ sums, uint64_t nblocks,
-                                                    BlockIn* __restrict__ ins, uint64_t* __restrict__ misc) {
-  __shared__ Xf sm[1024];
+// one block's transform (stops at the block's first failing fragment)
+__device__ Xf block_xf(const Frag* __restrict__ frags, uint64_t g0, uint64_t g1, uint32_t start_off) {
+  Xf S = xf_identity();
+  bool in_pre = true;
+  uint64_t acc = 0, off = 0;
+  uint32_t first = 0;
+  for (uint64_t g = g0; g < g1; ++g) {
+    const Frag f = frags[g];
+    if (!f.ok) { S.err = 1; S.err_class = BCW_ERR_CRC; S.err_frag = (uint32_t)g; break; }   // wal_iterator.go:79-82
+    if (f.type < 1 || f.type > 4) { S.err = 1; S.err_class = BCW_ERR_TYPE; S.err_frag = (uint32_t)g; break; }  // :94-95
+    const uint64_t doff = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
+    if (in_pre) {
+      if (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST) {
+        in_pre = false;
+        S.has_emit = 1;
+        S.n_emit = 1;
+        acc = 0;
+        continue;
+      }
+      if (f.len > 0 && !S.nz) { S.nz = 1; S.off = doff; S.first = (uint32_t)g; }
+      S.a += f.len;
+    } else {
+      if (acc == 0) { off = doff; first = (uint32_t)g; }
+      if (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST) { S.n_emit++; acc = 0; }
+      else acc += f.len;
+    }
+  }
+  if (S.has_emit) { S.a = acc; S.off = off; S.first = first; S.nz = 0; }
+  return S;
+}
+
+// per-block transform + workgroup exclusive scan: pre[b] = composition of earlier blocks of the WG
+__global__ __launch_bounds__(256) void k_blocksum(const Frag* __restrict__ frags, const uint32_t* __restrict__ fbase,
+                                                  uint64_t nblocks, uint32_t start_off, uint64_t frag_cap,
+                                                  Xf* __restrict__ pre, Xf* __restrict__ wgagg) {
+  __shared__ Xf sm[2][256];
   const uint32_t t = threadIdx.x;
-  const uint64_t per = (nblocks + 1023) / 1024;
+  const uint64_t b = blockIdx.x * 256ull + t;
+  Xf x = xf_identity();
+  if (b < nblocks) {
+    uint64_t g0 = fbase[b], g1 = fbase[b + 1];
+    if (g1 > frag_cap) g1 = frag_cap;
+    if (g0 > g1) g0 = g1;
+    x = block_xf(frags, g0, g1, start_off);
+  }
+  int cur = 0;
+  sm[0][t] = x;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    const Xf v = t >= d ? xf_compose(sm[cur][t - d], sm[cur][t]) : sm[cur][t];
+    sm[cur ^ 1][t] = v;
+    cur ^= 1;
+    __syncthreads();
+  }
+  if (b < nblocks) pre[b] = t > 0 ? sm[cur][t - 1] : xf_identity();
+  if (t == 255) wgagg[blockIdx.x] = sm[cur][255];
+}
+
+// exclusive scan of workgroup aggregates (one workgroup); totals -> misc
+__global__ __launch_bounds__(1024) void k_xscan_wg(Xf* __restrict__ wgagg, uint64_t nwg, uint64_t* __restrict__ misc) {
+  __shared__ Xf sm[2][1024];
+  const uint32_t t = threadIdx.x;
+  const uint64_t per = (nwg + 1023) / 1024;
   const uint64_t lo = t * per;
-  const uint64_t hi = lo + per < nblocks ? lo + per : nblocks;
+  const uint64_t hi = lo + per < nwg ? lo + per : nwg;
   Xf mine = xf_identity();
-  for (uint64_t b = lo; b < hi; ++b) mine = xf_compose(mine, xf_of(sums[b]));
-  sm[t] = mine;
+  for (uint64_t i = lo; i < hi; ++i) mine = xf_compose(mine, wgagg[i]);
+  int cur = 0;
+  sm[0][t] = mine;
   __syncthreads();
   for (uint32_t d = 1; d < 1024; d <<= 1) {
-    Xf left = t >= d ? sm[t - d] : xf_identity();
-    __syncthreads();
-    if (t >= d) sm[t] = xf_compose(left, sm[t]);
+    const Xf v = t >= d ? xf_compose(sm[cur][t - d], sm[cur][t]) : sm[cur][t];
+    sm[cur ^ 1][t] = v;
+    cur ^= 1;
     __syncthreads();
   }
-  Xf run = t > 0 ? sm[t - 1] : xf_identity();
-  for (uint64_t b = lo; b < hi; ++b) {
-    BlockIn in;
-    in.rec_base = run.n_emit;
-    in.live = run.err ? 0u : 1u;
-    if (run.has_emit) { in.acc = run.a; in.off = run.off; in.first = run.first; }
-    else { in.acc = run.a; in.off = run.off; in.first = run.first; }
-    ins[b] = in;
-    run = xf_compose(run, xf_of(sums[b]));
+  Xf run = t > 0 ? sm[cur][t - 1] : xf_identity();
+  for (uint64_t i = lo; i < hi; ++i) {
+    const Xf x = wgagg[i];
+    wgagg[i] = run;
+    run = xf_compose(run, x);
   }
   if (t == 1023) {
-    const Xf tot = sm[1023];
+    const Xf tot = sm[cur][1023];
     misc[M_NREC] = tot.n_emit;
     misc[M_ERR_FRAG] = tot.err ? tot.err_frag : ~0ull;
     misc[M_ERR_CLASS] = tot.err ? tot.err_class : 0;
@@ -498,11 +688,8 @@ __global__ __launch_bounds__(1024) void k_blockscan(const BlockSum* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------
-// k_records: record emission per block (one wave per block) + RecordFromBytes / HintRecord.Decode.
-struct Emit {
-  uint64_t foff, size;
-  uint32_t first, emit;
-};
+// k_records: record emission (one wave per block, fragments in chunks of 64 lanes) and
+// RecordFromBytes (record.go:140-239) / HintRecord.Decode (hint.go:50-84) per record, one lane each.
 
 // Go encoding/binary.Uvarint over a byte accessor; DecodeUvarint maps errors to (0,0).
 template <typename RD>
@@ -525,28 +712,28 @@ __device__ __forceinline__ uint64_t uvarint(RD& rd, uint64_t pos, uint64_t len, 
 }
 
 constexpr int kRecWaves = 4;
+constexpr uint32_t kStage = 128;      // staged record-prefix bytes per lane
+constexpr uint32_t kStageArea = 144;  // 9 x 16 B aligned loads
 
-// intra-wave LDS hand-off (lanes of one wave run in lockstep; this orders the compiler)
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-constexpr uint32_t kStage = 128;  // staged record-prefix bytes per lane
-
+// logical byte reader of one record: staged prefix in LDS, then a walk over its fragments
 struct RecReader {
   const uint8_t* seg;
   const Frag* frags;
   uint32_t start_off;
-  const uint8_t* stage;  // LDS, kStage bytes (valid for pos < nstaged)
+  const uint8_t* stage;
   uint32_t nstaged;
   uint32_t f_first, f_last;
-  // cache of the current fragment for the slow path
   uint32_t cf;
   uint64_t cbeg, clen, caddr;
-  __device__ uint32_t operator()(uint64_t pos) {
+  __device__ __forceinline__ uint32_t operator()(uint64_t pos) {
     if (pos < nstaged) return stage[pos];
-    if (pos < cbeg) { cf = f_first; cbeg = 0; const Frag f = frags[cf]; clen = f.len; caddr = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start; }
+    if (pos < cbeg) {
+      cf = f_first;
+      cbeg = 0;
+      const Frag f = frags[cf];
+      clen = f.len;
+      caddr = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
+    }
     while (pos >= cbeg + clen && cf < f_last) {
       cbeg += clen;
       ++cf;
@@ -558,145 +745,164 @@ struct RecReader {
   }
 };
 
+__device__ __forceinline__ void parse_record(const bcw_decode_params& p, RecReader& rd, uint64_t len, uint8_t& status,
+                                             uint8_t& hdr, uint8_t& flags, uint8_t& etag_off, uint64_t& key_len,
+                                             uint64_t& val_len, uint64_t& meta_len, uint64_t& expire, uint64_t& aux0,
+                                             uint64_t& aux1) {
+  uint32_t used;
+  status = BCW_ST_OK;
+  hdr = flags = etag_off = 0;
+  key_len = val_len = meta_len = expire = aux0 = aux1 = 0;
+  if (p.mode == BCW_MODE_RECORD) {
+    // RecordFromBytes, record.go:140-239
+    const uint64_t min_hdr = 1ull + p.ns_size + 1ull + 3ull;
+    if (len < min_hdr) { status = BCW_ST_INVALID; return; }
+    const uint64_t header = rd(0);
+    uint64_t o = 1 + p.ns_size;
+    const uint32_t flag = rd(o);
+    ++o;
+    key_len = uvarint(rd, o, len, used); o += used;
+    val_len = uvarint(rd, o, len, used); o += used;
+    meta_len = uvarint(rd, o, len, used); o += used;
+    const uint64_t etag_len = (flag & 1u) ? 0 : p.etag_size;
+    uint64_t expire_size = 0;
+    hdr = (uint8_t)header; flags = (uint8_t)flag; etag_off = (uint8_t)o;
+    if ((flag & 2u) == 0) {
+      if (o + etag_len > len) { status = BCW_ST_PANIC; return; }  // data[offset+etagLen:] (record.go:186)
+      expire = uvarint(rd, o + etag_len, len, used);
+      expire_size = used;
+      expire += p.base_time;
+    }
+    const int64_t cur_hdr = (int64_t)o + (int64_t)etag_len + (int64_t)expire_size;
+    const int64_t cur_total = cur_hdr + (int64_t)(key_len + val_len + meta_len);
+    if ((uint64_t)cur_hdr != header || cur_total != (int64_t)len) { status = BCW_ST_INVALID; return; }
+    const uint64_t s1 = key_len + val_len;
+    const uint64_t s2 = s1 + meta_len;
+    const bool wrapped = (s1 < key_len) || (s2 < s1);
+    if ((int64_t)key_len < 0 || (int64_t)val_len < 0 || (int64_t)meta_len < 0 || wrapped) status = BCW_ST_PANIC;
+    else if (key_len > 0xffffffffull || val_len > 0xffffffffull || meta_len > 0xffffffffull || len > 0xffffffffull)
+      status = BCW_ST_UNSUPPORTED;
+  } else {
+    // HintRecord.Decode, hint.go:50-84
+    if (len < (uint64_t)p.ns_size + 5ull) { status = BCW_ST_INVALID; return; }
+    int64_t o = p.ns_size;
+    key_len = uvarint(rd, (uint64_t)o, len, used);
+    o += used;
+    const int64_t key_off = o;
+    o = (int64_t)((uint64_t)o + key_len);
+    hdr = (uint8_t)key_off;
+    if (o < 0 || o > (int64_t)len) { status = BCW_ST_PANIC; return; }
+    expire = uvarint(rd, (uint64_t)o, len, used); o += used;  // fid
+    aux0 = uvarint(rd, (uint64_t)o, len, used); o += used;    // off
+    aux1 = uvarint(rd, (uint64_t)o, len, used); o += used;    // size
+    if (o != (int64_t)len) status = BCW_ST_INVALID;
+    else if ((int64_t)key_len < 0) status = BCW_ST_PANIC;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                  bcw_decode_params p, const Frag* __restrict__ frags,
                                                  const uint32_t* __restrict__ fbase, uint64_t nblocks,
-                                                 uint64_t frag_cap, const BlockIn* __restrict__ ins,
-                                                 bcw_record_table tab, uint64_t* __restrict__ misc) {
-  __shared__ Emit s_emit[kRecWaves][64];
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[kRecWaves][64][kStage];
+                                                 uint64_t frag_cap, const Xf* __restrict__ pre,
+                                                 const Xf* __restrict__ wgpre, bcw_record_table tab,
+                                                 uint64_t* __restrict__ misc) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[kRecWaves][64][kStageArea];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
   const uint64_t b = (uint64_t)blockIdx.x * kRecWaves + wave;
   if (b >= nblocks) return;
-  const BlockIn in = ins[b];
-  if (!in.live) return;
+  // incoming state: composition of all earlier blocks, applied to the empty initial state
+  const Xf in = xf_compose(wgpre[b >> 8], pre[b]);
+  if (in.err) return;
+  uint64_t acc = in.a, off = in.off;
+  uint32_t first = in.first;
+  uint64_t rec = in.n_emit;
   uint64_t g0 = fbase[b], g1 = fbase[b + 1];
   if (g1 > frag_cap) g1 = frag_cap;
   const uint64_t err_frag = misc[M_ERR_FRAG];
   if (g1 > err_frag) g1 = err_frag;  // nothing at or after the first failing fragment is emitted
-  uint64_t acc = in.acc, off = in.off;
-  uint32_t first = in.first;
-  uint64_t rec = in.rec_base;
-  uint64_t g = g0;
-  // lane 0 walks fragments and emits records in batches of 64; the wave parses the batch
-  while (true) {
-    uint32_t ne = 0;
-    if (lane == 0) {
-      while (g < g1 && ne < 64) {
-        const Frag f = frags[g];
-        const uint64_t doff = (uint64_t)p.start_off + (uint64_t)f.blk * kBlock + f.start;
-        if (acc == 0) { off = doff; first = (uint32_t)g; }
-        if (f.type == BCW_RECORD_FULL) {
-          s_emit[wave][ne++] = Emit{off, f.len, (uint32_t)g, (uint32_t)g};
-          acc = 0;
-        } else if (f.type == BCW_RECORD_LAST) {
-          acc += f.len;
-          s_emit[wave][ne++] = Emit{off, acc, first, (uint32_t)g};
-          acc = 0;
-        } else {
-          acc += f.len;
-        }
-        ++g;
+  uint8_t* st = s_stage[wave][lane];
+  for (uint64_t c0 = g0; c0 < g1; c0 += 64) {
+    const uint64_t g = c0 + lane;
+    const bool valid = g < g1;
+    Frag f{};
+    if (valid) f = frags[g];
+    const uint32_t len = valid ? f.len : 0u;
+    const uint64_t D = (uint64_t)p.start_off + (uint64_t)f.blk * kBlock + f.start;
+    const bool isE = valid && (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST);
+    const uint64_t E = __ballot(isE);
+    const uint64_t NZ = __ballot(valid && len > 0);
+    const uint32_t S = wave_incl_scan_u32(len, lane);  // inclusive prefix of lengths
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t pm = E & below;
+    const int prev = pm ? 63 - __builtin_clzll(pm) : -1;
+    const uint32_t S_prev = __shfl(S, prev < 0 ? 0 : prev, 64);
+    const uint64_t between = (uint64_t)(S - len) - (prev < 0 ? 0u : S_prev);  // lengths in (prev, lane)
+    const uint64_t acc_before = (prev < 0 ? acc : 0ull) + between;
+    const uint64_t range = prev < 0 ? below : (below & ~(~0ull >> (63 - prev)));
+    const uint64_t nzr = NZ & range;
+    const int fnz = nzr ? __builtin_ctzll(nzr) : 0;
+    const uint64_t D_fnz = __shfl(D, fnz, 64);
+    // chunk carry-out (state after the last emission of the chunk, or extended incoming state)
+    const uint64_t V = __ballot(valid);
+    const int last_valid = V ? 63 - __builtin_clzll(V) : -1;
+    const uint32_t S_tot = __shfl(S, last_valid < 0 ? 0 : last_valid, 64);
+    const int lastE = E ? 63 - __builtin_clzll(E) : -1;
+    uint64_t acc2, off2;
+    uint32_t first2;
+    {
+      const uint32_t S_lastE = __shfl(S, lastE < 0 ? 0 : lastE, 64);
+      const uint64_t after = lastE < 0 ? V : (V & ~(~0ull >> (63 - lastE)));
+      const uint64_t nza = NZ & after;
+      const int fa = nza ? __builtin_ctzll(nza) : 0;
+      const uint64_t D_fa = __shfl(D, fa, 64);
+      if (lastE >= 0) {
+        acc2 = (uint64_t)(S_tot - S_lastE);
+        off2 = D_fa;
+        first2 = (uint32_t)(c0 + fa);
+      } else {
+        acc2 = acc + S_tot;
+        if (acc > 0 || !nza) { off2 = off; first2 = first; }
+        else { off2 = D_fa; first2 = (uint32_t)(c0 + fa); }
       }
     }
-    ne = __shfl(ne, 0, 64);
-    wave_sync();
-    if (lane < ne) {
-      const Emit em = s_emit[wave][lane];
-      const uint64_t r = rec + lane;
-      // stage the record prefix: fast path when its first fragment holds it
-      const Frag f0 = frags[em.first];
+    if (isE) {
+      uint64_t foff;
+      uint32_t ffrag;
+      if (acc_before == 0) { foff = D; ffrag = (uint32_t)g; }
+      else if (prev < 0 && acc > 0) { foff = off; ffrag = first; }
+      else { foff = D_fnz; ffrag = (uint32_t)(c0 + fnz); }
+      const bool full = f.type == BCW_RECORD_FULL;
+      const uint64_t size = full ? (uint64_t)len : acc_before + len;
+      const uint32_t src = full ? (uint32_t)g : ffrag;  // the record's bytes start in fragment src
+      const uint64_t r = rec + __builtin_popcountll(E & below);
+      // stage the record prefix (when its first fragment holds it) with aligned 16 B loads
+      const Frag f0 = full ? f : frags[src];
       const uint64_t a0 = (uint64_t)p.start_off + (uint64_t)f0.blk * kBlock + f0.start;
-      uint64_t want = em.size < kStage ? em.size : kStage;
-      uint32_t nst = 0;
-      uint8_t* st = s_stage[wave][lane];
-      if (f0.len >= want) {
-        nst = (uint32_t)want;
-        for (uint32_t k = 0; k < nst; ++k) st[k] = seg[a0 + k];
+      uint64_t want = size < kStage ? size : kStage;
+      if (want > f0.len) want = f0.len;
+      const uint64_t base = a0 & ~15ull;
+      const uint32_t sh = (uint32_t)(a0 - base);
+      const uint32_t nld = (uint32_t)((sh + want + 15) >> 4);
+      for (uint32_t k = 0; k < nld; ++k) {
+        const uint64_t o = base + 16 * k;
+        *reinterpret_cast<uint4*>(st + 16 * k) = load16_safe(seg, seg_len, (int64_t)o);
       }
-      RecReader rd{seg, frags, p.start_off, st, nst, em.first, em.emit, em.first, 0, f0.len, a0};
-      const uint64_t len = em.size;
-      uint8_t status = BCW_ST_OK, hdr = 0, flags = 0, etag_off = 0;
-      uint64_t key_len = 0, val_len = 0, meta_len = 0, expire = 0, aux0 = 0, aux1 = 0;
-      uint32_t used;
-      if (p.mode == BCW_MODE_RECORD) {
-        // RecordFromBytes, record.go:140-239
-        const uint64_t min_hdr = 1ull + p.ns_size + 1ull + 3ull;
-        if (len < min_hdr) {
-          status = BCW_ST_INVALID;
-        } else {
-          uint64_t o = 0;
-          const uint64_t header = rd(0);
-          o = 1 + p.ns_size;
-          const uint32_t flag = rd(o);
-          ++o;
-          key_len = uvarint(rd, o, len, used); o += used;
-          val_len = uvarint(rd, o, len, used); o += used;
-          meta_len = uvarint(rd, o, len, used); o += used;
-          const uint64_t etag_len = (flag & 1u) ? 0 : p.etag_size;
-          uint64_t expire_size = 0;
-          hdr = (uint8_t)header; flags = (uint8_t)flag; etag_off = (uint8_t)o;
-          if ((flag & 2u) == 0) {
-            if (o + etag_len > len) {
-              status = BCW_ST_PANIC;  // data[offset+etagLen:] out of range (record.go:186)
-            } else {
-              expire = uvarint(rd, o + etag_len, len, used);
-              expire_size = used;
-              expire += p.base_time;
-            }
-          }
-          if (status == BCW_ST_OK) {
-            const int64_t cur_hdr = (int64_t)o + (int64_t)etag_len + (int64_t)expire_size;
-            const int64_t cur_total = cur_hdr + (int64_t)(key_len + val_len + meta_len);
-            if ((uint64_t)cur_hdr != header || cur_total != (int64_t)len) {
-              status = BCW_ST_INVALID;
-            } else {
-              const uint64_t s1 = key_len + val_len;
-              const uint64_t s2 = s1 + meta_len;
-              const bool wrapped = (s1 < key_len) || (s2 < s1);
-              if ((int64_t)key_len < 0 || (int64_t)val_len < 0 || (int64_t)meta_len < 0 || wrapped)
-                status = BCW_ST_PANIC;
-              else if (key_len > 0xffffffffull || val_len > 0xffffffffull || meta_len > 0xffffffffull ||
-                       len > 0xffffffffull)
-                status = BCW_ST_UNSUPPORTED;
-            }
-          }
-        }
-      } else {
-        // HintRecord.Decode, hint.go:50-84
-        const uint64_t min_sz = (uint64_t)p.ns_size + 5ull;
-        if (len < min_sz) {
-          status = BCW_ST_INVALID;
-        } else {
-          int64_t o = p.ns_size;
-          key_len = uvarint(rd, (uint64_t)o, len, used);
-          o += used;
-          const int64_t key_off = o;
-          o = (int64_t)((uint64_t)o + key_len);
-          hdr = (uint8_t)key_off;
-          if (o < 0 || o > (int64_t)len) {
-            status = BCW_ST_PANIC;
-          } else {
-            expire = uvarint(rd, (uint64_t)o, len, used); o += used;  // fid
-            aux0 = uvarint(rd, (uint64_t)o, len, used); o += used;    // off
-            aux1 = uvarint(rd, (uint64_t)o, len, used); o += used;    // size
-            if (o != (int64_t)len) status = BCW_ST_INVALID;
-            else if ((int64_t)key_len < 0) status = BCW_ST_PANIC;
-          }
-        }
-      }
+      RecReader rd{seg, frags, p.start_off, st + sh, (uint32_t)want, src, (uint32_t)g, src, 0, f0.len, a0};
+      uint8_t status, hdr, flags, etag_off;
+      uint64_t key_len, val_len, meta_len, expire, aux0, aux1;
+      parse_record(p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
       if (r < tab.capacity) {
-        tab.foff[r] = em.foff;
-        tab.size[r] = em.size;
+        tab.foff[r] = foff;
+        tab.size[r] = size;
         tab.expire[r] = expire;
         if (tab.aux0) tab.aux0[r] = aux0;
         if (tab.aux1) tab.aux1[r] = aux1;
         tab.key_len[r] = (uint32_t)key_len;
         tab.val_len[r] = (uint32_t)val_len;
         tab.meta_len[r] = (uint32_t)meta_len;
-        tab.first_frag[r] = em.first;
-        tab.emit_frag[r] = em.emit;
+        tab.first_frag[r] = src;
+        tab.emit_frag[r] = (uint32_t)g;
         tab.hdr_size[r] = hdr;
         tab.flags[r] = flags;
         tab.etag_off[r] = etag_off;
@@ -704,9 +910,11 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
       }
       if (status != BCW_ST_OK) atomicMin((unsigned long long*)&misc[M_FIRST_BAD], (unsigned long long)r);
     }
-    rec += ne;
+    rec += __builtin_popcountll(E);
+    acc = acc2;
+    off = off2;
+    first = first2;
     wave_sync();
-    if (ne < 64) break;
   }
 }
 
@@ -759,29 +967,30 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   Prof& pr = prof ? *prof : dummy;
   hipEvent_t ev = nullptr;
   const uint32_t nb_grid = (uint32_t)((nblocks + 255) / 256);
+  const uint64_t nwg = (nblocks + 255) / 256;
   pr.begin(K_CHASE_COUNT, stream, ev);
-  k_chase<<<nb_grid, 256, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.nfrag, nullptr, nullptr, 0, 0);
+  k_chase_count<<<nb_grid, 256, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.wgsum);
   pr.end(K_CHASE_COUNT, stream, ev);
   pr.begin(K_SCAN, stream, ev);
-  k_scan_u32<<<1, 1024, 0, stream>>>(s.nfrag, s.fbase, nblocks, &s.misc[M_NFRAGS]);
+  k_scan_wg<<<1, 1024, 0, stream>>>(s.wgsum, nwg, s.fbase, nblocks, &s.misc[M_NFRAGS]);
   pr.end(K_SCAN, stream, ev);
   pr.begin(K_CHASE_WRITE, stream, ev);
-  k_chase<<<nb_grid, 256, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.nfrag, s.fbase, s.frags,
-                                       s.frag_cap, 1);
+  k_chase_write<<<nb_grid, 256, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.wgsum, s.frags,
+                                             s.frag_cap);
   pr.end(K_CHASE_WRITE, stream, ev);
   pr.begin(K_CRC, stream, ev);
-  k_crc<<<(uint32_t)num_cus, 1024, kCrcLds, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
+  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, kCrcLds, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
                                                       s.frag_cap, tabs);
   pr.end(K_CRC, stream, ev);
   pr.begin(K_BLOCKSUM, stream, ev);
-  k_blocksum<<<nb_grid, 256, 0, stream>>>(s.frags, s.fbase, nblocks, p.start_off, s.frag_cap, s.sums);
+  k_blocksum<<<nb_grid, 256, 0, stream>>>(s.frags, s.fbase, nblocks, p.start_off, s.frag_cap, s.pre, s.wgagg);
   pr.end(K_BLOCKSUM, stream, ev);
-  pr.begin(K_BLOCKSCAN, stream, ev);
-  k_blockscan<<<1, 1024, 0, stream>>>(s.sums, nblocks, s.ins, s.misc);
-  pr.end(K_BLOCKSCAN, stream, ev);
+  pr.begin(K_XSCAN, stream, ev);
+  k_xscan_wg<<<1, 1024, 0, stream>>>(s.wgagg, nwg, s.misc);
+  pr.end(K_XSCAN, stream, ev);
   pr.begin(K_RECORDS, stream, ev);
   k_records<<<(uint32_t)((nblocks + kRecWaves - 1) / kRecWaves), 64 * kRecWaves, 0, stream>>>(
-      d_seg, p.seg_len, p, s.frags, s.fbase, nblocks, s.frag_cap, s.ins, t, s.misc);
+      d_seg, p.seg_len, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg, t, s.misc);
   pr.end(K_RECORDS, stream, ev);
   const uint64_t tail = (p.seg_len - p.start_off) % kBlock;
   const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;

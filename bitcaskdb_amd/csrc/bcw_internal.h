@@ -25,56 +25,42 @@ struct Frag {
 };
 static_assert(sizeof(Frag) == 16, "Frag layout");
 
-// Per-block record-state transform (the composition of the iterator's per-fragment state
-// machine over one block, wal_iterator.go:69-96). See DESIGN.md "record assembly".
-struct BlockSum {
-  uint64_t pre_len;   // sum of lengths of fragments before the first emission (or all, if none)
-  uint64_t pre_off;   // data offset of the first non-empty fragment among them
-  uint64_t out_acc;   // state after the last emission: accumulated length
-  uint64_t out_off;   // ... its iterator offset
-  uint32_t pre_first; // global fragment index of that first non-empty fragment
-  uint32_t out_first; // ... first fragment of the pending record
-  uint32_t n_emit;    // emissions in the block before the error (if any)
-  uint32_t err_frag;  // global index of the first failing fragment in the block, or ~0u
-  uint8_t has_emit;
-  uint8_t pre_nz;
-  uint8_t err_class;
-  uint8_t pad[5];
+// Record-state transform of a range of blocks: the composition of the iterator's per-fragment
+// state machine (wal_iterator.go:69-96). See bcw_decode.hip "Record assembly".
+struct Xf {
+  uint64_t n_emit;
+  uint64_t a;      // has_emit: state after the last emission (acc)   else: sum of lengths
+  uint64_t off;    //           ... its offset                         else: first non-empty offset
+  uint32_t first;  //           ... its first fragment                 else: first non-empty fragment
+  uint32_t err_frag;
+  uint8_t has_emit, nz, err, err_class;
+  uint32_t pad;
 };
-static_assert(sizeof(BlockSum) == 56, "BlockSum layout");
-
-// Incoming state of a block after the scan.
-struct BlockIn {
-  uint64_t acc;
-  uint64_t off;
-  uint64_t rec_base;  // global record index of the block's first emission
-  uint32_t first;
-  uint32_t live;      // 0 if an earlier block already failed
-};
-static_assert(sizeof(BlockIn) == 32, "BlockIn layout");
+static_assert(sizeof(Xf) == 40, "Xf layout");
 
 // Device-side constant tables, built on the host once per context.
 struct Tables {
   uint32_t* slice;   // [2][256] slice-by-2 CRC-32C tables (T0 = byte table, T1)
   uint32_t* fwd;     // [64][8][16] lane shift operators F_l = A_{8*128*(63-l)} (nibble images)
   uint32_t* carry;   // [8][16] A_{8*8192} (nibble images)
+  uint32_t* half;    // [8][16] A_{8*64} (nibble images)
   uint32_t* initc;   // [kBlock+1] A_{8L}(0xFFFFFFFF)
 };
 
 struct Scratch {
   uint64_t nblocks_cap = 0;
   uint64_t frag_cap = 0;
-  uint32_t* nfrag = nullptr;   // [nblocks]
-  uint32_t* fbase = nullptr;   // [nblocks+1]
+  uint32_t* fbase = nullptr;   // [nblocks+1] global index of each block's first fragment
+  uint32_t* wgsum = nullptr;   // [nblocks/256+1] per-workgroup fragment counts -> bases
   Frag* frags = nullptr;       // [frag_cap]
-  BlockSum* sums = nullptr;    // [nblocks]
-  BlockIn* ins = nullptr;      // [nblocks]
+  Xf* pre = nullptr;           // [nblocks] workgroup-exclusive record-state prefix per block
+  Xf* wgagg = nullptr;         // [nblocks/256+1] workgroup aggregates -> exclusive prefixes
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
 };
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
 // stream around every kernel of the pipeline.
-enum KernelId { K_CHASE_COUNT = 0, K_SCAN, K_CHASE_WRITE, K_CRC, K_BLOCKSUM, K_BLOCKSCAN, K_RECORDS, K_FINALIZE,
+enum KernelId { K_CHASE_COUNT = 0, K_SCAN, K_CHASE_WRITE, K_CRC, K_BLOCKSUM, K_XSCAN, K_RECORDS, K_FINALIZE,
                 K_NUM };
 struct Prof {
   bool on = false;
@@ -105,7 +91,7 @@ hipError_t launch_export_frags(const Scratch& s, const bcw_frag_table& out, uint
 
 // Host-side table builders (bcw_api.cpp).
 void build_slice_tables(uint32_t* t2x256);
-void build_lane_tables(uint32_t* fwd64x8x16, uint32_t* carry8x16);
+void build_lane_tables(uint32_t* fwd64x8x16, uint32_t* carry8x16, uint32_t* half8x16);
 void build_initc(uint32_t* initc);
 
 }  // namespace bcw

@@ -99,6 +99,19 @@ def case_zipf(n=600, seed=42):
     return data, params()
 
 
+def case_sparse_multi(n=6000, seed=7):
+    """Long runs of single-window fragments between rare multi-window ones: a 64-fragment window
+    can hold few body windows, so one CRC pass spans many fragment windows."""
+    rng = np.random.default_rng(seed)
+    ps = []
+    for i in range(n):
+        r = rng.random()
+        v = int(rng.integers(200, 70000)) if r < 0.03 else int(rng.integers(1, 60))
+        ps.append(rec(i, v, klen=int(rng.integers(1, 40))))
+    data, _ = wal_of(ps)
+    return data, params()
+
+
 def case_tail_garbage():
     """file with < 7 trailing bytes after the last fragment (ignored) and a truncated last block."""
     data, _ = wal_of([rec(i, 300) for i in range(20)])
@@ -202,6 +215,8 @@ ALL = {
     "padding": case_padding,
     "zero_first": case_zero_first,
     "zipf": case_zipf,
+    "sparse_multi": case_sparse_multi,
+    "sparse_multi_dense": lambda: case_sparse_multi(4000, 11),
     "tail_garbage": case_tail_garbage,
     "truncated_record": case_truncated_record,
     "zero_tail": case_zero_tail,
