@@ -206,17 +206,30 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
   build_slice_tables(slice.data());
   build_lane_tables(fwd.data(), carry.data(), half.data());
   build_initc(initc.data());
+  std::vector<uint32_t> image(kLdsImage);
+  for (int e = 0; e < 256; ++e)
+    for (int r = 0; r < 32; ++r) {
+      image[e * 64 + r] = slice[256 + e];  // T1: applied to the low byte of x
+      image[e * 64 + 32 + r] = slice[e];   // T0: applied to byte 1 of x
+    }
+  for (int i = 0; i < kLdsFwd; ++i) image[kLdsSlice + i] = fwd[(i & 63) * 128 + (i >> 6)];
+  for (int i = 0; i < 128; ++i) {
+    image[kLdsSlice + kLdsFwd + i] = carry[i];
+    image[kLdsSlice + kLdsFwd + 128 + i] = half[i];
+  }
   bool ok = hipMalloc(&c->tabs.slice, slice.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.fwd, fwd.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.carry, carry.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.half, half.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.initc, initc.size() * 4) == hipSuccess &&
+            hipMalloc(&c->tabs.lds_image, image.size() * 4) == hipSuccess &&
             hipMalloc(&c->d_result, sizeof(bcw_decode_result)) == hipSuccess;
   ok = ok && hipMemcpy(c->tabs.slice, slice.data(), slice.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.fwd, fwd.data(), fwd.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.carry, carry.data(), carry.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.half, half.data(), half.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemcpy(c->tabs.initc, initc.data(), initc.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+       hipMemcpy(c->tabs.initc, initc.data(), initc.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(c->tabs.lds_image, image.data(), image.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
   if (!ok) { bcw_ctx_destroy(c); return BCW_E_NOMEM; }
   *out = c;
   return BCW_OK;
@@ -242,6 +255,7 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   (void)hipFree(c->tabs.carry);
   (void)hipFree(c->tabs.half);
   (void)hipFree(c->tabs.initc);
+  (void)hipFree(c->tabs.lds_image);
   (void)hipFree(c->d_seg);
   (void)hipFree(c->d_tab_mem);
   (void)hipFree(c->d_result);
@@ -330,9 +344,9 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
 static const char* kKernelNames[K_NUM] = {"k_chase_count", "k_scan_wg", "k_chase_write", "k_crc",
                                           "k_blocksum", "k_xscan_wg", "k_records", "k_finalize"};
 
-int bcw_ctx_set_profiling(bcw_ctx* c, int on) {
+int bcw_ctx_set_profiling(bcw_ctx* c, int mask) {
   if (!c) return BCW_E_INVAL;
-  c->prof.on = on != 0;
+  c->prof.mask = (uint32_t)mask;
   return BCW_OK;
 }
 

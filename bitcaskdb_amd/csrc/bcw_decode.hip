@@ -192,26 +192,41 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr int kCrcWaves = 12;
+constexpr int kCrcWaves = 16;
 constexpr int kCrcThreads = kCrcWaves * 64;
-constexpr int kLdsSlice = 2 * 256 * 32;  // dwords, slice-by-2 tables replicated x32 (64 KiB)
-constexpr int kLdsFwd = 8 * 16 * 64;     // dwords, lane operators (32 KiB)
-constexpr int kLdsOps = 2 * 8 * 16;      // dwords, carry A_{8*8192} and half A_{8*64} operators
 constexpr int kRing = 128;               // ring of multi-window fragments per wave
 constexpr int kRingWords = 7;            // cpre, cend, blk, se, J, V1, fragment index
 constexpr int kWaveLds = kRing * kRingWords + 64;  // + 64 pass markers
 constexpr size_t kCrcLds = (size_t)(kLdsSlice + kLdsFwd + kLdsOps + kCrcWaves * kWaveLds) * 4;
 
-// slice-by-2 step on the low 16 bits of h: T0 = byte table, T1 = one byte further
-__device__ __forceinline__ uint32_t step16(const uint32_t* __restrict__ tab, uint32_t lo, uint32_t s, uint32_t h) {
-  const uint32_t x = s ^ h;
-  const uint32_t a = tab[((256u + (x & 0xffu)) << 5) | lo];
-  const uint32_t b = tab[((((x >> 8) & 0xffu)) << 5) | lo];
-  return (s >> 16) ^ a ^ b;
-}
-__device__ __forceinline__ uint32_t step32(const uint32_t* __restrict__ tab, uint32_t lo, uint32_t s, uint32_t w) {
-  s = step16(tab, lo, s, w & 0xffffu);
-  return step16(tab, lo, s, w >> 16);
+// CRC-32C (zero xor-out, no final inversion) of one 128 B window from state `seed`: two slice-by-2
+// chains over the two 64 B halves, joined with the half operator A_{8*64}.
+// LDS slice layout: 256-B rows, row e = { T1[e] x32 lanes, T0[e] x32 lanes }, so the byte address of a
+// lookup is (index byte << 8) | lane slot, built by one v_perm_b32 and always on bank lane % 32.
+// Each chain carries x = state ^ next halfword: a step is perm, perm, ds_read x2, xor3.
+__device__ __forceinline__ uint32_t crc_window(const uint32_t* __restrict__ tab, const uint32_t* __restrict__ half,
+                                               uint32_t lb, uint32_t seed, const uint32_t (&w)[32]) {
+  const uint8_t* tb = reinterpret_cast<const uint8_t*>(tab);
+  uint32_t xa = seed ^ (w[0] & 0xffffu);
+  uint32_t xb = w[16] & 0xffffu;
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    uint32_t ha = 0, hb = 0;  // next halfword of each half
+    if (q < 31) {
+      ha = (q & 1) ? (w[(q + 1) >> 1] & 0xffffu) : (w[q >> 1] >> 16);
+      hb = (q & 1) ? (w[16 + ((q + 1) >> 1)] & 0xffffu) : (w[16 + (q >> 1)] >> 16);
+    }
+    const uint32_t a0 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(xa, lb, 0x0c0c0400u));
+    const uint32_t a1 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(xa, lb, 0x0c0c0500u) + 128u);
+    const uint32_t b0 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(xb, lb, 0x0c0c0400u));
+    const uint32_t b1 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(xb, lb, 0x0c0c0500u) + 128u);
+    xa = a0 ^ a1 ^ ((xa >> 16) ^ ha);
+    xb = b0 ^ b1 ^ ((xb >> 16) ^ hb);
+  }
+  uint32_t r = xb;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r ^= half[i * 16 + ((xa >> (4 * i)) & 15u)];
+  return r;
 }
 // F_l(x): lane-replicated nibble images, lane l reads its own copy (bank = l % 32)
 __device__ __forceinline__ uint32_t apply_fwd(const uint32_t* __restrict__ fwd, uint32_t lane, uint32_t x) {
@@ -268,8 +283,8 @@ __device__ __forceinline__ uint32_t wave_add_scan(uint32_t v, uint32_t lane) {
   return v;
 }
 
-// bounds-checked 16 B load, out of line (rare: the segment's first/last bytes)
-__device__ __noinline__ uint4 load16_slow(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t o) {
+// bounds-checked 16 B load (rare: the segment's first/last bytes); a rolled loop keeps it small
+__device__ __forceinline__ uint4 load16_slow(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t o) {
   uint64_t lo = 0, hi = 0;
 #pragma unroll 1
   for (int i = 0; i < 16; ++i) {
@@ -351,21 +366,31 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
                                                      uint32_t start_off, uint64_t nblocks,
                                                      const uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
                                                      uint64_t frag_cap, Tables tabs) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kCrcLds / 4];
   uint32_t* s_slice = lds;
   uint32_t* s_fwd = lds + kLdsSlice;
   uint32_t* s_carry = s_fwd + kLdsFwd;
   uint32_t* s_half = s_carry + 128;
   uint32_t* s_wave_all = s_carry + kLdsOps;
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < (uint32_t)kLdsSlice; i += kCrcThreads) s_slice[i] = tabs.slice[i >> 5];
-  for (uint32_t i = tid; i < (uint32_t)kLdsFwd; i += kCrcThreads) s_fwd[i] = tabs.fwd[(i & 63u) * 128u + (i >> 6)];
-  if (tid < 128u) s_carry[tid] = tabs.carry[tid];
-  else if (tid < 256u) s_half[tid - 128u] = tabs.half[tid - 128u];
+  {  // table image -> LDS: all 16 B loads in flight before the first store
+    constexpr uint32_t kVec = kLdsImage / 4;
+    constexpr int kFull = (int)(kVec / kCrcThreads);
+    const uint4* src = reinterpret_cast<const uint4*>(tabs.lds_image);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    uint4 v[kFull];
+#pragma unroll
+    for (int k2 = 0; k2 < kFull; ++k2) v[k2] = src[tid + k2 * kCrcThreads];
+    const uint32_t tail = tid + kFull * kCrcThreads;
+    if (tail < kVec) dst[tail] = src[tail];
+#pragma unroll
+    for (int k2 = 0; k2 < kFull; ++k2) dst[tid + k2 * kCrcThreads] = v[k2];
+  }
   __syncthreads();
 
   const uint32_t lane = tid & 63u;
   const uint32_t lo = lane & 31u;
+  const uint32_t lb = lo * 4u;  // lane slot in a slice-table row
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of multi-window fragments
   uint32_t* r_cend = r_cpre + kRing;
@@ -422,13 +447,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
         w[k2] &= (uint32_t)(0xffffffffffffffffull << sh);
       }
       if (geo.C == 1u) fix_last(w, (uint32_t)(geo.gs + (int64_t)(e - s) - wst), J);
-      uint32_t Sa = 0, Sb = 0;
-#pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) {
-        Sa = step32(s_slice, lo, Sa, w[k2]);
-        Sb = step32(s_slice, lo, Sb, w[16 + k2]);
-      }
-      V = apply_op(s_half, Sa) ^ Sb;
+      V = crc_window(s_slice, s_half, lb, 0u, w);
       if (geo.C == 1u) frags[f0 + fi].ok = (V == 0u) ? 1 : 0;
     }
     // append fragments with body windows to the ring
@@ -515,13 +534,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     if (d.active) {
       if (d.last) fix_last(w, d.hi, d.J);
       if (!(ABL & 1)) {
-        uint32_t Sa = d.seed, Sb = 0;
-#pragma unroll
-        for (int k2 = 0; k2 < 16; ++k2) {
-          Sa = step32(s_slice, lo, Sa, w[k2]);
-          Sb = step32(s_slice, lo, Sb, w[16 + k2]);
-        }
-        v = apply_op(s_half, Sa) ^ Sb;
+        v = crc_window(s_slice, s_half, lb, d.seed, w);
       } else {
         v = d.seed ^ w[0] ^ w[31];
       }
@@ -688,7 +701,7 @@ __global__ __launch_bounds__(1024) void k_xscan_wg(Xf* __restrict__ wgagg, uint6
 }
 
 // ------------------------------------------------------------------------------------------
-// k_records: record emission (one wave per block, fragments in chunks of 64 lanes) and
+// k_records: record emission (one wave per run of blocks, fragments in chunks of 64 lanes) and
 // RecordFromBytes (record.go:140-239) / HintRecord.Decode (hint.go:50-84) per record, one lane each.
 
 // Go encoding/binary.Uvarint over a byte accessor; DecodeUvarint maps errors to (0,0).
@@ -809,15 +822,22 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
   __shared__ __attribute__((aligned(16))) uint8_t s_stage[kRecWaves][64][kStageArea];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
-  const uint64_t b = (uint64_t)blockIdx.x * kRecWaves + wave;
+  // a wave takes a run of consecutive blocks holding about 64 fragments (one chunk); the grid is
+  // sized for one block per wave and the surplus waves exit
+  uint64_t nf = misc[M_NFRAGS];
+  if (nf > frag_cap) nf = frag_cap;
+  uint64_t bpw = nf ? (64 * nblocks) / nf : nblocks;
+  if (bpw < 1) bpw = 1;
+  const uint64_t b = ((uint64_t)blockIdx.x * kRecWaves + wave) * bpw;
   if (b >= nblocks) return;
+  const uint64_t b_end = b + bpw < nblocks ? b + bpw : nblocks;
   // incoming state: composition of all earlier blocks, applied to the empty initial state
   const Xf in = xf_compose(wgpre[b >> 8], pre[b]);
   if (in.err) return;
   uint64_t acc = in.a, off = in.off;
   uint32_t first = in.first;
   uint64_t rec = in.n_emit;
-  uint64_t g0 = fbase[b], g1 = fbase[b + 1];
+  uint64_t g0 = fbase[b], g1 = fbase[b_end];
   if (g1 > frag_cap) g1 = frag_cap;
   const uint64_t err_frag = misc[M_ERR_FRAG];
   if (g1 > err_frag) g1 = err_frag;  // nothing at or after the first failing fragment is emitted
@@ -979,7 +999,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
                                              s.frag_cap);
   pr.end(K_CHASE_WRITE, stream, ev);
   pr.begin(K_CRC, stream, ev);
-  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, kCrcLds, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
+  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
                                                       s.frag_cap, tabs);
   pr.end(K_CRC, stream, ev);
   pr.begin(K_BLOCKSUM, stream, ev);

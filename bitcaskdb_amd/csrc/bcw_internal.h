@@ -45,7 +45,15 @@ struct Tables {
   uint32_t* carry;   // [8][16] A_{8*8192} (nibble images)
   uint32_t* half;    // [8][16] A_{8*64} (nibble images)
   uint32_t* initc;   // [kBlock+1] A_{8L}(0xFFFFFFFF)
+  uint32_t* lds_image;  // k_crc's LDS table image, laid out exactly as in LDS (see kLdsImage)
 };
+
+// k_crc LDS table image (dwords): slice-by-2 tables as 256-B rows {T1[e] x32, T0[e] x32} (lane l
+// reads bank l % 32), lane operators transposed to [8][16][64 lanes], then the carry and half operators.
+constexpr int kLdsSlice = 2 * 256 * 32;
+constexpr int kLdsFwd = 8 * 16 * 64;
+constexpr int kLdsOps = 2 * 8 * 16;
+constexpr int kLdsImage = kLdsSlice + kLdsFwd + kLdsOps;
 
 struct Scratch {
   uint64_t nblocks_cap = 0;
@@ -63,7 +71,7 @@ struct Scratch {
 enum KernelId { K_CHASE_COUNT = 0, K_SCAN, K_CHASE_WRITE, K_CRC, K_BLOCKSUM, K_XSCAN, K_RECORDS, K_FINALIZE,
                 K_NUM };
 struct Prof {
-  bool on = false;
+  uint32_t mask = 0;  // bit k: time kernel id k
   struct Mark { int kid; hipEvent_t a, b; };
   std::vector<Mark> marks;
   std::vector<hipEvent_t> pool;
@@ -73,9 +81,10 @@ struct Prof {
     (void)hipEventCreate(&e);
     return e;
   }
-  void begin(int kid, hipStream_t s, hipEvent_t& a) { if (on) { a = get(); (void)hipEventRecord(a, s); } (void)kid; }
+  bool on(int kid) const { return (mask >> kid) & 1u; }
+  void begin(int kid, hipStream_t s, hipEvent_t& a) { if (on(kid)) { a = get(); (void)hipEventRecord(a, s); } }
   void end(int kid, hipStream_t s, hipEvent_t a) {
-    if (!on) return;
+    if (!on(kid)) return;
     hipEvent_t b = get();
     (void)hipEventRecord(b, s);
     marks.push_back({kid, a, b});

@@ -164,9 +164,10 @@ void* bcw_ctx_stream(bcw_ctx* ctx);
 int bcw_ctx_sync(bcw_ctx* ctx);
 int bcw_ctx_device(bcw_ctx* ctx);
 /* Per-kernel HIP-event timing of the decode pipeline (events on the launch stream around each
- * kernel). bcw_ctx_kernel_times synchronises, fills total_ms[k] / launches[k] for kernel ids
- * k < n accumulated since the last call, resets, and returns the number of kernel ids. */
-int bcw_ctx_set_profiling(bcw_ctx* ctx, int on);
+ * selected kernel). `mask`: bit k times kernel id k (see bcw_kernel_name), -1 = all, 0 = off.
+ * bcw_ctx_kernel_times synchronises, fills total_ms[k] / launches[k] for kernel ids k < n
+ * accumulated since the last call, resets, and returns the number of kernel ids. */
+int bcw_ctx_set_profiling(bcw_ctx* ctx, int mask);
 int bcw_ctx_kernel_times(bcw_ctx* ctx, double* total_ms, uint64_t* launches, int n);
 const char* bcw_kernel_name(int kernel_id);
 

@@ -58,7 +58,7 @@ int main(int argc, char** argv) {
   const int reps = 20;
   float full = timeit([&] { bcw_decode_segment_async(ctx, d, &p, &t, dres); }, reps, st);
   printf("full pipeline   %.4f ms  %.1f GB/s\n", full, n / (full * 1e-3) / 1e9);
-  bcw_ctx_set_profiling(ctx, 1);
+  bcw_ctx_set_profiling(ctx, -1);
   for (int i = 0; i < reps; ++i) bcw_decode_segment_async(ctx, d, &p, &t, dres);
   double tot[8]; uint64_t cnt[8];
   bcw_ctx_kernel_times(ctx, tot, cnt, 8);
@@ -67,7 +67,7 @@ int main(int argc, char** argv) {
   Scratch& s = ctx->s;
   const uint64_t nblocks = (n - 40 + kBlock - 1) / kBlock;
   auto run = [&](auto kern, int grid) {
-    return timeit([&] { kern<<<grid, kCrcThreads, kCrcLds, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs); },
+    return timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs); },
                   reps, st);
   };
   const int cus = ctx->num_cus;
