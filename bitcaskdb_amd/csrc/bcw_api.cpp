@@ -241,6 +241,7 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.frags);
   (void)hipFree(s.pre);
   (void)hipFree(s.wgagg);
+  (void)hipFree(s.wgx);
   (void)hipFree(s.misc);
   s = Scratch{};
 }
@@ -280,7 +281,8 @@ int bcw_ctx_sync(bcw_ctx* c) {
 
 static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   Scratch& s = c->s;
-  if (nblocks <= s.nblocks_cap && frag_cap <= s.frag_cap && s.misc) return BCW_OK;
+  const uint64_t nwave = (uint64_t)c->num_cus * kCrcWaves;
+  if (nblocks <= s.nblocks_cap && frag_cap <= s.frag_cap && nwave <= s.nwave_cap && s.misc) return BCW_OK;
   (void)hipStreamSynchronize(c->cur);
   const uint64_t nb = std::max(nblocks, s.nblocks_cap);
   const uint64_t fc = std::max(frag_cap, s.frag_cap);
@@ -289,11 +291,13 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.wgsum, nwg * 4) == hipSuccess &&
             hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
             hipMalloc(&s.pre, (nb + 1) * sizeof(Xf)) == hipSuccess &&
-            hipMalloc(&s.wgagg, nwg * sizeof(Xf)) == hipSuccess &&
+            hipMalloc(&s.wgagg, nwave * sizeof(Xf)) == hipSuccess &&
+            hipMalloc(&s.wgx, (nwave / kCrcWaves + 1) * sizeof(Xf)) == hipSuccess &&
             hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;
   s.frag_cap = fc;
+  s.nwave_cap = nwave;
   return BCW_OK;
 }
 
@@ -341,8 +345,7 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
   return launch_export_frags(c->s, *d_frags, c->last_start_off, c->cur, n) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_chase_count", "k_scan_wg", "k_chase_write", "k_crc",
-                                          "k_blocksum", "k_xscan_wg", "k_records", "k_finalize"};
+static const char* kKernelNames[K_NUM] = {"k_chase_count", "k_scan_wg", "k_chase_write", "k_crc", "k_records"};
 
 int bcw_ctx_set_profiling(bcw_ctx* c, int mask) {
   if (!c) return BCW_E_INVAL;

@@ -24,7 +24,8 @@ namespace bcw {
 
 // ------------------------------------------------------------------------------------------
 // misc counters (Scratch::misc)
-enum { M_FIRST_BAD = 0, M_NREC = 1, M_ERR_FRAG = 2, M_ERR_CLASS = 3, M_NFRAGS = 4 };
+enum { M_FIRST_BAD = 0, M_NREC = 1, M_ERR_FRAG = 2, M_ERR_CLASS = 3, M_NFRAGS = 4, M_DONE_CRC = 5, M_DONE_REC = 6,
+       M_T_CRC0 = 10, M_T_SCAN0 = 11, M_T_SCAN1 = 12 };  // wall_clock64 stamps (diagnostics)
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
@@ -61,6 +62,46 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane
   }
   return v;
 }
+// ---- wave-level scans on DPP (row_shr 1/2/4/8, row_bcast 15/31), no LDS round trips ----
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v, uint32_t lane) {
+  const uint32_t rl = lane & 15u;
+  uint32_t t;
+  t = dpp_mov<0x111>(v); if (rl >= 1u) v = max(v, t);
+  t = dpp_mov<0x112>(v); if (rl >= 2u) v = max(v, t);
+  t = dpp_mov<0x114>(v); if (rl >= 4u) v = max(v, t);
+  t = dpp_mov<0x118>(v); if (rl >= 8u) v = max(v, t);
+  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v = max(v, t);
+  t = dpp_mov<0x143>(v); if (lane >= 32u) v = max(v, t);
+  return v;
+}
+// segmented inclusive XOR scan; seg = first lane of this lane's segment
+__device__ __forceinline__ uint32_t wave_seg_xor_scan(uint32_t v, uint32_t lane, uint32_t seg) {
+  const uint32_t rl = lane & 15u;
+  uint32_t t;
+  t = dpp_mov<0x111>(v); if (rl >= 1u && lane - 1u >= seg) v ^= t;
+  t = dpp_mov<0x112>(v); if (rl >= 2u && lane - 2u >= seg) v ^= t;
+  t = dpp_mov<0x114>(v); if (rl >= 4u && lane - 4u >= seg) v ^= t;
+  t = dpp_mov<0x118>(v); if (rl >= 8u && lane - 8u >= seg) v ^= t;
+  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u && (lane & ~15u) - 1u >= seg) v ^= t;  // from lane 15 / 47
+  t = dpp_mov<0x143>(v); if (lane >= 32u && 31u >= seg) v ^= t;                       // from lane 31
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_add_scan(uint32_t v, uint32_t lane) {
+  const uint32_t rl = lane & 15u;
+  uint32_t t;
+  t = dpp_mov<0x111>(v); if (rl >= 1u) v += t;
+  t = dpp_mov<0x112>(v); if (rl >= 2u) v += t;
+  t = dpp_mov<0x114>(v); if (rl >= 4u) v += t;
+  t = dpp_mov<0x118>(v); if (rl >= 8u) v += t;
+  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v += t;
+  t = dpp_mov<0x143>(v); if (lane >= 32u) v += t;
+  return v;
+}
+
 // returns the exclusive prefix of v over the workgroup; *total = workgroup sum
 __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, uint32_t& total) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -148,7 +189,8 @@ __global__ __launch_bounds__(1024) void k_scan_wg(uint32_t* __restrict__ wgsum, 
   if (t == 1023) {
     const uint64_t tot = sm[1023];
     fbase[nblocks] = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
-    *total = tot;
+    total[0] = tot;                        // misc[M_NFRAGS]
+    total[M_DONE_CRC - M_NFRAGS] = 0;      // k_crc's workgroup completion counter
   }
 }
 
@@ -162,6 +204,223 @@ __global__ __launch_bounds__(256) void k_chase_write(const uint8_t* __restrict__
   const uint32_t g0 = fbase[b] + wgbase[blockIdx.x];
   fbase[b] = g0;
   chase_block<true>(seg, seg_len, start_off, b, frags, g0, frag_cap);
+}
+
+// ------------------------------------------------------------------------------------------
+// Record assembly. The iterator's per-fragment state machine (wal_iterator.go:69-96: `off` is
+// captured while the accumulated record is empty; Full emits the Full's data with that offset;
+// First/Middle append; Last appends and emits; any other type is an error) is summarised per block
+// as a transform Xf of the incoming state (acc_len, off, first). Transforms compose associatively:
+// each k_crc wave builds its blocks' transforms and their wave-local exclusive prefixes once its
+// fragments are verified, the last k_crc workgroup scans the wave aggregates, and k_records
+// composes the two for the incoming state of any block.
+
+__device__ __forceinline__ Xf xf_identity() {
+  Xf x{};
+  x.err_frag = 0xffffffffu;
+  return x;
+}
+// A then B
+__device__ __forceinline__ Xf xf_compose(const Xf& A, const Xf& B) {
+  if (A.err) return A;
+  Xf R;
+  R.pad = 0;
+  R.n_emit = A.n_emit + B.n_emit;
+  R.err = B.err;
+  R.err_class = B.err_class;
+  R.err_frag = B.err_frag;
+  if (B.has_emit) {
+    R.has_emit = 1; R.a = B.a; R.off = B.off; R.first = B.first; R.nz = 0;
+  } else if (A.has_emit) {
+    R.has_emit = 1; R.nz = 0;
+    R.a = A.a + B.a;
+    if (A.a > 0 || !B.nz) { R.off = A.off; R.first = A.first; }
+    else { R.off = B.off; R.first = B.first; }
+  } else {
+    R.has_emit = 0;
+    R.a = A.a + B.a;
+    R.nz = A.nz | B.nz;
+    if (A.nz) { R.off = A.off; R.first = A.first; } else { R.off = B.off; R.first = B.first; }
+  }
+  return R;
+}
+
+
+// Xf published to / read from other workgroups of the same launch: agent-scope atomic 8-byte
+// words, so no L2 writeback/invalidate fence is needed (the per-XCD L2s are not coherent)
+__device__ __forceinline__ void xf_store_agent(Xf* dst, const Xf& x) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(&x);
+  uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ Xf xf_load_agent(const Xf* src) {
+  Xf x;
+  uint64_t* w = reinterpret_cast<uint64_t*>(&x);
+  const uint64_t* s = reinterpret_cast<const uint64_t*>(src);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) w[i] = __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return x;
+}
+
+// contiguous lane mask [i, j], i <= j < 64
+__device__ __forceinline__ uint64_t lane_range(uint32_t i, uint32_t j) { return (~0ull >> (63u - j)) & (~0ull << i); }
+
+// Per-chunk view of 64 consecutive fragments (lane = fragment) for the record state machine.
+struct FragChunk {
+  uint64_t c0;                   // global index of lane 0's fragment
+  uint64_t bad, crcbad, E, NZ;   // ballots: failing (CRC or type), CRC failing, Full/Last, non-empty
+  uint32_t S, len;               // per lane: inclusive prefix of lengths, own length
+  uint64_t D;                    // per lane: data offset
+  __device__ __forceinline__ uint64_t sum(uint64_t m) const {  // lengths over a contiguous mask
+    if (!m) return 0;
+    const uint32_t i = __builtin_ctzll(m), j = 63u - __builtin_clzll(m);
+    return (uint64_t)(__builtin_amdgcn_readlane(S, j) - __builtin_amdgcn_readlane(S, i) +
+                      __builtin_amdgcn_readlane(len, i));
+  }
+  __device__ __forceinline__ uint64_t doff(uint32_t i) const {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)D, i) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(D >> 32), i) << 32);
+  }
+  // transform of the contiguous run of fragments M (wal_iterator.go:69-96, stops at the run's
+  // first CRC (:79-82) or type (:94-95) failure)
+  __device__ __forceinline__ Xf run(uint64_t M) const {
+    Xf x = xf_identity();
+    uint64_t Mv = M;
+    const uint64_t b = bad & M;
+    if (b) {
+      const uint32_t fb = __builtin_ctzll(b);
+      Mv = M & ((1ull << fb) - 1ull);
+      x.err = 1;
+      x.err_class = ((crcbad >> fb) & 1ull) ? BCW_ERR_CRC : BCW_ERR_TYPE;
+      x.err_frag = (uint32_t)(c0 + fb);
+    }
+    const uint64_t Em = E & Mv;
+    uint64_t rest = Mv;  // fragments whose lengths are pending at the end of the run
+    if (Em) {
+      const uint32_t lastE = 63u - __builtin_clzll(Em);
+      rest = lastE == 63u ? 0ull : (Mv & (~0ull << (lastE + 1u)));
+      x.has_emit = 1;
+      x.n_emit = (uint64_t)__builtin_popcountll(Em);
+    }
+    x.a = sum(rest);
+    const uint64_t nzr = NZ & rest;
+    x.nz = (!Em && nzr) ? 1 : 0;
+    if (nzr) {
+      const uint32_t i = __builtin_ctzll(nzr);
+      x.off = doff(i);
+      x.first = (uint32_t)(c0 + i);
+    }
+    return x;
+  }
+};
+
+// One k_crc wave, after verifying fragments [f0, f1) of blocks [b0, b1): the record-state
+// transform of each block, written as the wave-exclusive prefix lpre[b]; returns the wave aggregate.
+__device__ Xf wave_block_xf(const Frag* __restrict__ frags, uint64_t f0, uint64_t f1, uint64_t b0, uint64_t b1,
+                            uint32_t start_off, uint32_t lane, Xf* __restrict__ lpre) {
+  Xf R = xf_identity();    // closed blocks
+  Xf cur = xf_identity();  // the open block
+  if (b0 >= b1) return R;
+  uint64_t ob = b0;
+  if (lane == 0) lpre[b0] = R;
+  for (uint64_t c0 = f0; c0 < f1; c0 += 64) {
+    const uint64_t g = c0 + lane;
+    const bool valid = g < f1;
+    Frag f{};
+    if (valid) f = frags[g];
+    FragChunk ch;
+    ch.c0 = c0;
+    ch.crcbad = __ballot(valid && !f.ok);
+    ch.bad = __ballot(valid && (!f.ok || f.type < BCW_RECORD_FULL || f.type > BCW_RECORD_LAST));
+    ch.E = __ballot(valid && (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST));
+    ch.NZ = __ballot(valid && f.len > 0);
+    ch.len = valid ? f.len : 0u;
+    ch.S = wave_add_scan(ch.len, lane);
+    ch.D = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
+    const uint64_t V = __ballot(valid);
+    const uint32_t blk = f.blk;
+    const uint32_t pblk = __shfl_up(blk, 1, 64);
+    uint64_t starts = __ballot(valid && (lane == 0 || blk != pblk));
+    const uint32_t last = 63u - __builtin_clzll(V);
+    while (starts) {
+      const uint32_t s = __builtin_ctzll(starts);
+      starts &= starts - 1ull;
+      const uint32_t e = starts ? __builtin_ctzll(starts) - 1u : last;
+      const uint64_t bb = (uint32_t)__builtin_amdgcn_readlane(blk, s);
+      const Xf x = ch.run(lane_range(s, e));
+      if (bb != ob) {
+        R = xf_compose(R, cur);
+        for (uint64_t q = ob + 1 + lane; q < bb; q += 64) lpre[q] = R;  // blocks without fragments
+        ob = bb;
+        cur = x;
+        if (lane == 0) lpre[bb] = R;
+      } else {
+        cur = xf_compose(cur, x);
+      }
+    }
+  }
+  R = xf_compose(R, cur);
+  for (uint64_t q = ob + 1 + lane; q < b1; q += 64) lpre[q] = R;
+  return R;
+}
+
+// Xf moved between lanes (10 dwords)
+__device__ __forceinline__ Xf xf_shfl(const Xf& x, int src) {
+  Xf r;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(&x);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) o[i] = (uint32_t)__shfl((int)a[i], src, 64);
+  return r;
+}
+__device__ __forceinline__ Xf xf_readlane(const Xf& x, uint32_t src) {
+  Xf r;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(&x);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) o[i] = (uint32_t)__builtin_amdgcn_readlane((int)a[i], src);
+  return r;
+}
+// inclusive wave scan of Xf over lanes [0, n) (n a power of two <= 64), lane-order composition
+__device__ __forceinline__ Xf wave_xf_scan(Xf x, uint32_t lane, uint32_t n) {
+  for (uint32_t d = 1; d < n; d <<= 1) {
+    const Xf y = xf_shfl(x, (int)(lane >= d ? lane - d : lane));
+    if (lane >= d) x = xf_compose(y, x);
+  }
+  return x;
+}
+
+// Exclusive scan of the k_crc workgroup aggregates by the last wave to finish (one wave,
+// kAggPer consecutive aggregates per lane per round, loaded back to back); totals -> misc.
+constexpr int kAggPer = 4;
+__device__ void scan_wg_aggregates(Xf* __restrict__ wgx, uint64_t n, uint64_t* __restrict__ misc, uint32_t lane) {
+  Xf carry = xf_identity();  // aggregate of earlier rounds
+  for (uint64_t r0 = 0; r0 < n; r0 += 64 * kAggPer) {
+    const uint64_t lo = r0 + (uint64_t)lane * kAggPer;
+    Xf x[kAggPer];
+#pragma unroll
+    for (int k = 0; k < kAggPer; ++k) x[k] = lo + k < n ? xf_load_agent(&wgx[lo + k]) : xf_identity();
+    Xf mine = x[0];
+#pragma unroll
+    for (int k = 1; k < kAggPer; ++k) mine = xf_compose(mine, x[k]);
+    const Xf incl = wave_xf_scan(mine, lane, 64);
+    const Xf prev = xf_shfl(incl, lane > 0 ? (int)lane - 1 : 0);
+    Xf run = lane > 0 ? xf_compose(carry, prev) : carry;
+#pragma unroll
+    for (int k = 0; k < kAggPer; ++k) {
+      if (lo + k < n) wgx[lo + k] = run;
+      run = xf_compose(run, x[k]);
+    }
+    carry = xf_compose(carry, xf_readlane(incl, 63));
+  }
+  if (lane == 0) {
+    misc[M_NREC] = carry.n_emit;
+    misc[M_ERR_FRAG] = carry.err ? carry.err_frag : ~0ull;
+    misc[M_ERR_CLASS] = carry.err ? carry.err_class : 0;
+    misc[M_FIRST_BAD] = ~0ull;
+    misc[M_DONE_REC] = 0;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -192,8 +451,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr int kCrcWaves = 16;
-constexpr int kCrcThreads = kCrcWaves * 64;
 constexpr int kRing = 128;               // ring of multi-window fragments per wave
 constexpr int kRingWords = 7;            // cpre, cend, blk, se, J, V1, fragment index
 constexpr int kWaveLds = kRing * kRingWords + 64;  // + 64 pass markers
@@ -241,46 +498,6 @@ __device__ __forceinline__ uint32_t apply_op(const uint32_t* __restrict__ c, uin
 #pragma unroll
   for (int i = 0; i < 8; ++i) r ^= c[i * 16 + ((x >> (4 * i)) & 15u)];
   return r;
-}
-
-// ---- wave-level scans on DPP (row_shr 1/2/4/8, row_bcast 15/31), no LDS round trips ----
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
-}
-__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v, uint32_t lane) {
-  const uint32_t rl = lane & 15u;
-  uint32_t t;
-  t = dpp_mov<0x111>(v); if (rl >= 1u) v = max(v, t);
-  t = dpp_mov<0x112>(v); if (rl >= 2u) v = max(v, t);
-  t = dpp_mov<0x114>(v); if (rl >= 4u) v = max(v, t);
-  t = dpp_mov<0x118>(v); if (rl >= 8u) v = max(v, t);
-  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v = max(v, t);
-  t = dpp_mov<0x143>(v); if (lane >= 32u) v = max(v, t);
-  return v;
-}
-// segmented inclusive XOR scan; seg = first lane of this lane's segment
-__device__ __forceinline__ uint32_t wave_seg_xor_scan(uint32_t v, uint32_t lane, uint32_t seg) {
-  const uint32_t rl = lane & 15u;
-  uint32_t t;
-  t = dpp_mov<0x111>(v); if (rl >= 1u && lane - 1u >= seg) v ^= t;
-  t = dpp_mov<0x112>(v); if (rl >= 2u && lane - 2u >= seg) v ^= t;
-  t = dpp_mov<0x114>(v); if (rl >= 4u && lane - 4u >= seg) v ^= t;
-  t = dpp_mov<0x118>(v); if (rl >= 8u && lane - 8u >= seg) v ^= t;
-  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u && (lane & ~15u) - 1u >= seg) v ^= t;  // from lane 15 / 47
-  t = dpp_mov<0x143>(v); if (lane >= 32u && 31u >= seg) v ^= t;                       // from lane 31
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_add_scan(uint32_t v, uint32_t lane) {
-  const uint32_t rl = lane & 15u;
-  uint32_t t;
-  t = dpp_mov<0x111>(v); if (rl >= 1u) v += t;
-  t = dpp_mov<0x112>(v); if (rl >= 2u) v += t;
-  t = dpp_mov<0x114>(v); if (rl >= 4u) v += t;
-  t = dpp_mov<0x118>(v); if (rl >= 8u) v += t;
-  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v += t;
-  t = dpp_mov<0x143>(v); if (lane >= 32u) v += t;
-  return v;
 }
 
 // bounds-checked 16 B load (rare: the segment's first/last bytes); a rolled loop keeps it small
@@ -360,12 +577,14 @@ struct BodyDesc {
 };
 
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
-// 4 no lane-operator / scan combine
+// 4 no lane-operator / scan combine, 8 no record-state tail
 template <int ABL = 0>
 __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                      uint32_t start_off, uint64_t nblocks,
                                                      const uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
-                                                     uint64_t frag_cap, Tables tabs) {
+                                                     uint64_t frag_cap, Tables tabs, Xf* __restrict__ lpre,
+                                                     Xf* __restrict__ wpre, Xf* __restrict__ wgx,
+                                                     uint64_t* __restrict__ misc) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kCrcLds / 4];
   uint32_t* s_slice = lds;
   uint32_t* s_fwd = lds + kLdsSlice;
@@ -373,6 +592,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   uint32_t* s_half = s_carry + 128;
   uint32_t* s_wave_all = s_carry + kLdsOps;
   const uint32_t tid = threadIdx.x;
+  __shared__ Xf s_wagg[kCrcWaves];  // wave aggregates of this workgroup
+  __shared__ uint32_t s_wdone;      // waves of this workgroup done
+  if (tid == 0) s_wdone = 0;
   {  // table image -> LDS: all 16 B loads in flight before the first store
     constexpr uint32_t kVec = kLdsImage / 4;
     constexpr int kFull = (int)(kVec / kCrcThreads);
@@ -388,6 +610,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   }
   __syncthreads();
 
+  if (blockIdx.x == 0 && tid == 0) misc[M_T_CRC0] = wall_clock64();
   const uint32_t lane = tid & 63u;
   const uint32_t lo = lane & 31u;
   const uint32_t lb = lo * 4u;  // lane slot in a slice-table row
@@ -407,8 +630,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint64_t f0 = fbase[b0];
   uint64_t f1 = fbase[b1];
   if (f1 > frag_cap) f1 = frag_cap;
-  if (f0 >= f1) return;
-  const uint32_t nfr = (uint32_t)(f1 - f0);
+  const uint32_t nfr = f1 > f0 ? (uint32_t)(f1 - f0) : 0u;
   const uint32_t nwin = (nfr + 63u) / 64u;
 
   uint32_t r_head = 0, r_tail = 0;  // absolute ring positions (wave-uniform)
@@ -570,134 +792,37 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     compute(dy, wy);
     pass += 64u;
   }
-}
 
-// ------------------------------------------------------------------------------------------
-// Record assembly. The iterator's per-fragment state machine (wal_iterator.go:69-96: `off` is
-// captured while the accumulated record is empty; Full emits the Full's data with that offset;
-// First/Middle append; Last appends and emits; any other type is an error) is summarised per block
-// as a transform Xf of the incoming state (acc_len, off, first). Transforms compose associatively,
-// so block states come from a workgroup scan (k_blocksum) plus a scan of workgroup aggregates.
+  if (ABL & 8) return;
+  // ---- record-state transforms of this wave's blocks (the verdicts were written by its lanes) ----
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const Xf wx_agg = wave_block_xf(frags, f0, f1, b0, b1, start_off, lane, lpre);
 
-__device__ __forceinline__ Xf xf_identity() {
-  Xf x{};
-  x.err_frag = 0xffffffffu;
-  return x;
-}
-// A then B
-__device__ __forceinline__ Xf xf_compose(const Xf& A, const Xf& B) {
-  if (A.err) return A;
-  Xf R;
-  R.pad = 0;
-  R.n_emit = A.n_emit + B.n_emit;
-  R.err = B.err;
-  R.err_class = B.err_class;
-  R.err_frag = B.err_frag;
-  if (B.has_emit) {
-    R.has_emit = 1; R.a = B.a; R.off = B.off; R.first = B.first; R.nz = 0;
-  } else if (A.has_emit) {
-    R.has_emit = 1; R.nz = 0;
-    R.a = A.a + B.a;
-    if (A.a > 0 || !B.nz) { R.off = A.off; R.first = A.first; }
-    else { R.off = B.off; R.first = B.first; }
-  } else {
-    R.has_emit = 0;
-    R.a = A.a + B.a;
-    R.nz = A.nz | B.nz;
-    if (A.nz) { R.off = A.off; R.first = A.first; } else { R.off = B.off; R.first = B.first; }
+  // ---- the last wave of the workgroup scans the 16 wave aggregates ----
+  if (lane == 0) s_wagg[wave] = wx_agg;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  uint32_t order = 0;
+  if (lane == 0) order = atomicAdd(&s_wdone, 1u);
+  order = __builtin_amdgcn_readlane(order, 0);
+  if (order != kCrcWaves - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  {
+    const Xf x = lane < (uint32_t)kCrcWaves ? s_wagg[lane] : xf_identity();
+    const Xf incl = wave_xf_scan(x, lane, kCrcWaves);
+    const Xf prev = xf_shfl(incl, lane > 0 ? (int)lane - 1 : 0);
+    if (lane < (uint32_t)kCrcWaves) wpre[(uint64_t)blockIdx.x * kCrcWaves + lane] = lane > 0 ? prev : xf_identity();
+    if (lane == (uint32_t)kCrcWaves - 1) xf_store_agent(&wgx[blockIdx.x], incl);
   }
-  return R;
-}
-
-// one block's transform (stops at the block's first failing fragment)
-__device__ Xf block_xf(const Frag* __restrict__ frags, uint64_t g0, uint64_t g1, uint32_t start_off) {
-  Xf S = xf_identity();
-  bool in_pre = true;
-  uint64_t acc = 0, off = 0;
-  uint32_t first = 0;
-  for (uint64_t g = g0; g < g1; ++g) {
-    const Frag f = frags[g];
-    if (!f.ok) { S.err = 1; S.err_class = BCW_ERR_CRC; S.err_frag = (uint32_t)g; break; }   // wal_iterator.go:79-82
-    if (f.type < 1 || f.type > 4) { S.err = 1; S.err_class = BCW_ERR_TYPE; S.err_frag = (uint32_t)g; break; }  // :94-95
-    const uint64_t doff = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
-    if (in_pre) {
-      if (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST) {
-        in_pre = false;
-        S.has_emit = 1;
-        S.n_emit = 1;
-        acc = 0;
-        continue;
-      }
-      if (f.len > 0 && !S.nz) { S.nz = 1; S.off = doff; S.first = (uint32_t)g; }
-      S.a += f.len;
-    } else {
-      if (acc == 0) { off = doff; first = (uint32_t)g; }
-      if (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST) { S.n_emit++; acc = 0; }
-      else acc += f.len;
-    }
-  }
-  if (S.has_emit) { S.a = acc; S.off = off; S.first = first; S.nz = 0; }
-  return S;
-}
-
-// per-block transform + workgroup exclusive scan: pre[b] = composition of earlier blocks of the WG
-__global__ __launch_bounds__(256) void k_blocksum(const Frag* __restrict__ frags, const uint32_t* __restrict__ fbase,
-                                                  uint64_t nblocks, uint32_t start_off, uint64_t frag_cap,
-                                                  Xf* __restrict__ pre, Xf* __restrict__ wgagg) {
-  __shared__ Xf sm[2][256];
-  const uint32_t t = threadIdx.x;
-  const uint64_t b = blockIdx.x * 256ull + t;
-  Xf x = xf_identity();
-  if (b < nblocks) {
-    uint64_t g0 = fbase[b], g1 = fbase[b + 1];
-    if (g1 > frag_cap) g1 = frag_cap;
-    if (g0 > g1) g0 = g1;
-    x = block_xf(frags, g0, g1, start_off);
-  }
-  int cur = 0;
-  sm[0][t] = x;
-  __syncthreads();
-  for (uint32_t d = 1; d < 256; d <<= 1) {
-    const Xf v = t >= d ? xf_compose(sm[cur][t - d], sm[cur][t]) : sm[cur][t];
-    sm[cur ^ 1][t] = v;
-    cur ^= 1;
-    __syncthreads();
-  }
-  if (b < nblocks) pre[b] = t > 0 ? sm[cur][t - 1] : xf_identity();
-  if (t == 255) wgagg[blockIdx.x] = sm[cur][255];
-}
-
-// exclusive scan of workgroup aggregates (one workgroup); totals -> misc
-__global__ __launch_bounds__(1024) void k_xscan_wg(Xf* __restrict__ wgagg, uint64_t nwg, uint64_t* __restrict__ misc) {
-  __shared__ Xf sm[2][1024];
-  const uint32_t t = threadIdx.x;
-  const uint64_t per = (nwg + 1023) / 1024;
-  const uint64_t lo = t * per;
-  const uint64_t hi = lo + per < nwg ? lo + per : nwg;
-  Xf mine = xf_identity();
-  for (uint64_t i = lo; i < hi; ++i) mine = xf_compose(mine, wgagg[i]);
-  int cur = 0;
-  sm[0][t] = mine;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    const Xf v = t >= d ? xf_compose(sm[cur][t - d], sm[cur][t]) : sm[cur][t];
-    sm[cur ^ 1][t] = v;
-    cur ^= 1;
-    __syncthreads();
-  }
-  Xf run = t > 0 ? sm[cur][t - 1] : xf_identity();
-  for (uint64_t i = lo; i < hi; ++i) {
-    const Xf x = wgagg[i];
-    wgagg[i] = run;
-    run = xf_compose(run, x);
-  }
-  if (t == 1023) {
-    const Xf tot = sm[cur][1023];
-    misc[M_NREC] = tot.n_emit;
-    misc[M_ERR_FRAG] = tot.err ? tot.err_frag : ~0ull;
-    misc[M_ERR_CLASS] = tot.err ? tot.err_class : 0;
-    misc[M_FIRST_BAD] = ~0ull;
-  }
+  // ---- the last workgroup scans the workgroup aggregates (stored with agent-scope atomics) ----
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  uint64_t gorder = 0;
+  if (lane == (uint32_t)kCrcWaves - 1) gorder = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_DONE_CRC]), 1ull);
+  gorder = (uint64_t)__shfl((long long)gorder, kCrcWaves - 1, 64);
+  if (gorder != gridDim.x - 1u) return;
+  if (lane == 0) misc[M_T_SCAN0] = wall_clock64();
+  scan_wg_aggregates(wgx, gridDim.x, misc, lane);
+  if (lane == 0) misc[M_T_SCAN1] = wall_clock64();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -813,27 +938,58 @@ __device__ __forceinline__ void parse_record(const bcw_decode_params& p, RecRead
   }
 }
 
+__device__ __forceinline__ void finalize(const uint64_t* __restrict__ misc, uint64_t nblocks, uint64_t frag_total,
+                           uint64_t frag_cap, const Frag* __restrict__ frags, uint32_t start_off, uint32_t tail_panic,
+                           bcw_decode_result* __restrict__ res) {
+  bcw_decode_result r{};
+  r.n_records = misc[M_NREC];
+  r.n_records_total = misc[M_NREC];
+  r.err_frag = misc[M_ERR_FRAG];
+  r.err_class = (int32_t)misc[M_ERR_CLASS];
+  r.n_frags = r.err_frag != ~0ull ? r.err_frag + 1 : frag_total;
+  // a last block of 1..6 bytes makes the reference iterator panic after every earlier record
+  // (wal_iterator.go:62-76 re-slices a header from its stale buffer, then buf[7:7+negative])
+  if (r.err_class == BCW_ERR_NONE && tail_panic) r.err_class = BCW_ERR_PANIC;
+  r.err_file_off = 0;
+  if (r.err_frag != ~0ull && r.err_frag < frag_cap) {
+    const Frag f = frags[r.err_frag];
+    r.err_file_off = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start - kHdr;
+  }
+  const uint64_t fb = __hip_atomic_load(&misc[M_FIRST_BAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.first_bad_record = fb == ~0ull ? -1 : (int32_t)(fb < 0x7fffffffull ? fb : 0x7fffffffull);
+  r.n_blocks = nblocks;
+  r.retry_frag_capacity = frag_total > frag_cap ? frag_total : 0;
+  *res = r;
+}
+
 __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                  bcw_decode_params p, const Frag* __restrict__ frags,
                                                  const uint32_t* __restrict__ fbase, uint64_t nblocks,
-                                                 uint64_t frag_cap, const Xf* __restrict__ pre,
-                                                 const Xf* __restrict__ wgpre, bcw_record_table tab,
-                                                 uint64_t* __restrict__ misc) {
+                                                 uint64_t frag_cap, const Xf* __restrict__ lpre,
+                                                 const Xf* __restrict__ wpre, const Xf* __restrict__ wgx, uint64_t nw,
+                                                 bcw_record_table tab,
+                                                 uint64_t* __restrict__ misc, uint32_t tail_panic,
+                                                 bcw_decode_result* __restrict__ res) {
   __shared__ __attribute__((aligned(16))) uint8_t s_stage[kRecWaves][64][kStageArea];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
-  // a wave takes a run of consecutive blocks holding about 64 fragments (one chunk); the grid is
-  // sized for one block per wave and the surplus waves exit
+  // work item = a run of consecutive blocks holding about 64 fragments (one chunk); waves stride
+  // over the items (persistent grid)
   uint64_t nf = misc[M_NFRAGS];
   if (nf > frag_cap) nf = frag_cap;
   uint64_t bpw = nf ? (64 * nblocks) / nf : nblocks;
   if (bpw < 1) bpw = 1;
-  const uint64_t b = ((uint64_t)blockIdx.x * kRecWaves + wave) * bpw;
-  if (b >= nblocks) return;
+  const uint64_t nitems = (nblocks + bpw - 1) / bpw;
+  for (uint64_t item = (uint64_t)blockIdx.x * kRecWaves + wave; item < nitems;
+       item += (uint64_t)gridDim.x * kRecWaves) {
+  const uint64_t b = item * bpw;
+  do {  // this item's record emission
+  if (b >= nblocks) break;
   const uint64_t b_end = b + bpw < nblocks ? b + bpw : nblocks;
-  // incoming state: composition of all earlier blocks, applied to the empty initial state
-  const Xf in = xf_compose(wgpre[b >> 8], pre[b]);
-  if (in.err) return;
+  // incoming state: the prefix of the k_crc wave holding block b, then that wave's blocks before b
+  const uint64_t gw = ((b + 1) * nw - 1) / nblocks;
+  const Xf in = xf_compose(xf_compose(wgx[gw / kCrcWaves], wpre[gw]), lpre[b]);
+  if (in.err) break;
   uint64_t acc = in.a, off = in.off;
   uint32_t first = in.first;
   uint64_t rec = in.n_emit;
@@ -936,30 +1092,18 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
     first = first2;
     wave_sync();
   }
-}
-
-__device__ void finalize(const uint64_t* __restrict__ misc, uint64_t nblocks, uint64_t frag_total,
-                           uint64_t frag_cap, const Frag* __restrict__ frags, uint32_t start_off, uint32_t tail_panic,
-                           bcw_decode_result* __restrict__ res) {
-  bcw_decode_result r{};
-  r.n_records = misc[M_NREC];
-  r.n_records_total = misc[M_NREC];
-  r.err_frag = misc[M_ERR_FRAG];
-  r.err_class = (int32_t)misc[M_ERR_CLASS];
-  r.n_frags = r.err_frag != ~0ull ? r.err_frag + 1 : frag_total;
-  // a last block of 1..6 bytes makes the reference iterator panic after every earlier record
-  // (wal_iterator.go:62-76 re-slices a header from its stale buffer, then buf[7:7+negative])
-  if (r.err_class == BCW_ERR_NONE && tail_panic) r.err_class = BCW_ERR_PANIC;
-  r.err_file_off = 0;
-  if (r.err_frag != ~0ull && r.err_frag < frag_cap) {
-    const Frag f = frags[r.err_frag];
-    r.err_file_off = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start - kHdr;
+  } while (0);
   }
-  const uint64_t fb = misc[M_FIRST_BAD];
-  r.first_bad_record = fb == ~0ull ? -1 : (int32_t)(fb < 0x7fffffffull ? fb : 0x7fffffffull);
-  r.n_blocks = nblocks;
-  r.retry_frag_capacity = frag_total > frag_cap ? frag_total : 0;
-  *res = r;
+  // the last workgroup to finish writes the segment result
+  __syncthreads();
+  __shared__ uint32_t s_last;
+  if (threadIdx.x == 0) {
+    // the finalizer only reads counters updated by atomics (M_FIRST_BAD) or by earlier kernels, so a
+    // workgroup-scope release (this workgroup's atomics have completed) is enough before counting
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    s_last = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_DONE_REC]), 1ull) == gridDim.x - 1u;
+    if (s_last) finalize(misc, nblocks, misc[M_NFRAGS], frag_cap, frags, p.start_off, tail_panic, res);
+  }
 }
 
 __global__ void k_export_frags(const Frag* __restrict__ frags, const uint64_t* __restrict__ misc, uint64_t cap,
@@ -975,9 +1119,7 @@ __global__ void k_export_frags(const Frag* __restrict__ frags, const uint64_t* _
   out.crc_ok[g] = f.ok;
 }
 
-__global__ void k_finalize_dev(const uint64_t* __restrict__ misc, uint64_t nblocks, uint64_t frag_cap,
-                               const Frag* __restrict__ frags, uint32_t start_off, uint32_t tail_panic,
-                               bcw_decode_result* __restrict__ res);
+
 
 // ------------------------------------------------------------------------------------------
 hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const bcw_record_table& t,
@@ -999,31 +1141,20 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
                                              s.frag_cap);
   pr.end(K_CHASE_WRITE, stream, ev);
   pr.begin(K_CRC, stream, ev);
+  const uint64_t nw = (uint64_t)num_cus * kCrcWaves;
   k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
-                                                      s.frag_cap, tabs);
+                                                         s.frag_cap, tabs, s.pre, s.wgagg, s.wgx, s.misc);
   pr.end(K_CRC, stream, ev);
-  pr.begin(K_BLOCKSUM, stream, ev);
-  k_blocksum<<<nb_grid, 256, 0, stream>>>(s.frags, s.fbase, nblocks, p.start_off, s.frag_cap, s.pre, s.wgagg);
-  pr.end(K_BLOCKSUM, stream, ev);
-  pr.begin(K_XSCAN, stream, ev);
-  k_xscan_wg<<<1, 1024, 0, stream>>>(s.wgagg, nwg, s.misc);
-  pr.end(K_XSCAN, stream, ev);
-  pr.begin(K_RECORDS, stream, ev);
-  k_records<<<(uint32_t)((nblocks + kRecWaves - 1) / kRecWaves), 64 * kRecWaves, 0, stream>>>(
-      d_seg, p.seg_len, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg, t, s.misc);
-  pr.end(K_RECORDS, stream, ev);
   const uint64_t tail = (p.seg_len - p.start_off) % kBlock;
   const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;
-  pr.begin(K_FINALIZE, stream, ev);
-  k_finalize_dev<<<1, 1, 0, stream>>>(s.misc, nblocks, s.frag_cap, s.frags, p.start_off, tail_panic, d_result);
-  pr.end(K_FINALIZE, stream, ev);
+  pr.begin(K_RECORDS, stream, ev);
+  uint64_t rec_wgs = (nblocks + kRecWaves - 1) / kRecWaves;
+  if (rec_wgs > (uint64_t)num_cus * 2) rec_wgs = (uint64_t)num_cus * 2;
+  k_records<<<(uint32_t)rec_wgs, 64 * kRecWaves, 0, stream>>>(
+      d_seg, p.seg_len, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg, s.wgx, nw, t, s.misc, tail_panic,
+      d_result);
+  pr.end(K_RECORDS, stream, ev);
   return hipGetLastError();
-}
-
-__global__ void k_finalize_dev(const uint64_t* __restrict__ misc, uint64_t nblocks, uint64_t frag_cap,
-                               const Frag* __restrict__ frags, uint32_t start_off, uint32_t tail_panic,
-                               bcw_decode_result* __restrict__ res) {
-  finalize(misc, nblocks, misc[M_NFRAGS], frag_cap, frags, start_off, tail_panic, res);
 }
 
 hipError_t launch_export_frags(const Scratch& s, const bcw_frag_table& out, uint32_t start_off, hipStream_t stream,

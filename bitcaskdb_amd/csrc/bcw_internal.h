@@ -54,6 +54,8 @@ constexpr int kLdsSlice = 2 * 256 * 32;
 constexpr int kLdsFwd = 8 * 16 * 64;
 constexpr int kLdsOps = 2 * 8 * 16;
 constexpr int kLdsImage = kLdsSlice + kLdsFwd + kLdsOps;
+constexpr int kCrcWaves = 16;  // waves per k_crc workgroup (one workgroup per CU)
+constexpr int kCrcThreads = kCrcWaves * 64;
 
 struct Scratch {
   uint64_t nblocks_cap = 0;
@@ -61,15 +63,16 @@ struct Scratch {
   uint32_t* fbase = nullptr;   // [nblocks+1] global index of each block's first fragment
   uint32_t* wgsum = nullptr;   // [nblocks/256+1] per-workgroup fragment counts -> bases
   Frag* frags = nullptr;       // [frag_cap]
-  Xf* pre = nullptr;           // [nblocks] workgroup-exclusive record-state prefix per block
-  Xf* wgagg = nullptr;         // [nblocks/256+1] workgroup aggregates -> exclusive prefixes
+  Xf* pre = nullptr;           // [nblocks] record-state prefix of each block within its k_crc wave
+  Xf* wgagg = nullptr;         // [k_crc waves] wave-exclusive prefix within the k_crc workgroup
+  Xf* wgx = nullptr;           // [k_crc workgroups] workgroup aggregates -> exclusive prefixes
+  uint64_t nwave_cap = 0;
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
 };
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
 // stream around every kernel of the pipeline.
-enum KernelId { K_CHASE_COUNT = 0, K_SCAN, K_CHASE_WRITE, K_CRC, K_BLOCKSUM, K_XSCAN, K_RECORDS, K_FINALIZE,
-                K_NUM };
+enum KernelId { K_CHASE_COUNT = 0, K_SCAN, K_CHASE_WRITE, K_CRC, K_RECORDS, K_NUM };
 struct Prof {
   uint32_t mask = 0;  // bit k: time kernel id k
   struct Mark { int kid; hipEvent_t a, b; };
