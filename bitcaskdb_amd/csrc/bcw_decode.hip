@@ -442,7 +442,7 @@ __device__ void scan_wg_aggregates(Xf* __restrict__ wgx, uint64_t n, uint64_t* _
 //     windows of a fragment on consecutive lanes. Lane l maps its end state into a common frame
 //     with F_l = A_{8*128*(63-l)} (lane-replicated nibble tables), a segmented XOR scan combines
 //     the fragment's windows, and the lane holding the last window tests the total for zero.
-//     A fragment continuing past lane 63 carries its value to the next pass (shift A_{8*8192}).
+//     A fragment continuing past lane 63 carries its state to the next pass, where it seeds lane 0's chain.
 //     Each window runs as two independent 64 B half-chains joined by A_{8*64}; the next pass's
 //     descriptors and window loads are issued before the current pass's chains (software pipeline).
 __device__ __forceinline__ void wave_sync() {
@@ -452,7 +452,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 constexpr int kRing = 128;               // ring of multi-window fragments per wave
-constexpr int kRingWords = 7;            // cpre, cend, blk, se, J, V1, fragment index
+constexpr int kRingWords = 7;            // cpre, cend, window end, C | last hi, J, V1, fragment index
 constexpr int kWaveLds = kRing * kRingWords + 64;  // + 64 pass markers
 constexpr size_t kCrcLds = (size_t)(kLdsSlice + kLdsFwd + kLdsOps + kCrcWaves * kWaveLds) * 4;
 
@@ -550,6 +550,54 @@ __device__ __forceinline__ void fix_last(uint32_t (&w)[32], uint32_t hi, uint32_
   }
 }
 
+// Quad-coalesced window loads. Loading each lane's own 128 B window (lane l: 8 x 16 B at its
+// window) touches 64 windows per load instruction and streams at ~60% of HBM; instead load g
+// (g = 4*p2 + 2*w1 + w0) gives the 4 lanes of quad a the 16 B pieces 4*p2 .. 4*p2+3 of window
+// 4a + (g & 3): 64 contiguous bytes per quad. Two lane-bit <-> register-bit exchanges (DPP
+// quad_perm) then leave piece p of window W in w[4p..4p+3] of lane W.
+template <int K>
+__device__ __forceinline__ void swap_lane_reg_bit(uint32_t (&w)[32], uint32_t lane) {
+  constexpr int CTRL = K == 0 ? 0xB1 : 0x4E;  // quad_perm partner lane ^ 1 / lane ^ 2
+  const bool hi = (lane >> K) & 1u;
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    if (x & (1 << K)) continue;
+    const int y = x | (1 << K);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t rx = w[4 * x + d], ry = w[4 * y + d];
+      const uint32_t px = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rx, CTRL, 0xf, 0xf, true);
+      const uint32_t py = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ry, CTRL, 0xf, 0xf, true);
+      w[4 * x + d] = hi ? py : rx;
+      w[4 * y + d] = hi ? ry : px;
+    }
+  }
+}
+__device__ __forceinline__ void quad_windows_transpose(uint32_t (&w)[32], uint32_t lane) {
+  swap_lane_reg_bit<0>(w, lane);
+  swap_lane_reg_bit<1>(w, lane);
+}
+// loads of the quad layout; woff/act: this lane's window offset (from wbase) and active flag;
+// SAFE: bounds-checked 16 B loads (windows touching the segment's ends)
+template <bool SAFE>
+__device__ __forceinline__ void load_windows_quad(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t wbase,
+                                                  uint32_t woff, bool act, uint32_t lane, uint32_t (&w)[32]) {
+  uint32_t wo[4], ac[4];
+  const uint32_t a = act ? 1u : 0u;
+  wo[0] = dpp_mov<0x00>(woff); wo[1] = dpp_mov<0x55>(woff); wo[2] = dpp_mov<0xAA>(woff); wo[3] = dpp_mov<0xFF>(woff);
+  ac[0] = dpp_mov<0x00>(a); ac[1] = dpp_mov<0x55>(a); ac[2] = dpp_mov<0xAA>(a); ac[3] = dpp_mov<0xFF>(a);
+  const uint32_t q = 16u * (lane & 3u);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    if (ac[g & 3]) {
+      const uint32_t o = wo[g & 3] + 64u * (g >> 2) + q;
+      const uint4 v = SAFE ? load16_safe(seg, seg_len, wbase + (int64_t)o)
+                           : *reinterpret_cast<const uint4*>(seg + wbase + o);
+      w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+    }
+  }
+}
+
 // global window geometry of a fragment (block-relative s, e)
 struct FragGeo {
   int64_t gs, GE;
@@ -567,17 +615,20 @@ __device__ __forceinline__ FragGeo frag_geo(uint32_t start_off, uint32_t blk, ui
 
 // one body-pass lane: which window, where, how to seed and finish it
 struct BodyDesc {
-  int64_t goff;     // global offset of the 128 B window
-  uint32_t hi;      // last window: byte index of the data end (else 0)
+  uint32_t woff;    // window offset relative to the wave's base (start of its first block - 128)
   uint32_t J;
   uint32_t seed;    // first body window: head-window end state; else 0
-  uint32_t cfb;     // index among the fragment's body windows
-  uint64_t gfrag;   // global fragment index
-  bool active, last;
+  uint32_t fi;      // fragment index relative to the wave's first fragment
+  uint32_t meta;    // hi (last window: data end within the window) | cfb << 8 | last << 17 | active << 18
+  __device__ __forceinline__ uint32_t hi() const { return meta & 0xffu; }
+  __device__ __forceinline__ uint32_t cfb() const { return (meta >> 8) & 0x1ffu; }  // body window index
+  __device__ __forceinline__ bool last() const { return (meta >> 17) & 1u; }
+  __device__ __forceinline__ bool active() const { return (meta >> 18) & 1u; }
 };
 
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
-// 4 no lane-operator / scan combine, 8 no record-state tail
+// 4 no lane-operator / scan combine, 8 no record-state tail, 16 phase stamps, 32 quad-layout loads
+// instead of per-lane windows, 64 no quad transpose
 template <int ABL = 0>
 __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                      uint32_t start_off, uint64_t nblocks,
@@ -615,11 +666,11 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint32_t lo = lane & 31u;
   const uint32_t lb = lo * 4u;  // lane slot in a slice-table row
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of multi-window fragments
-  uint32_t* r_cend = r_cpre + kRing;
-  uint32_t* r_blk = r_cend + kRing;
-  uint32_t* r_se = r_blk + kRing;
-  uint32_t* r_J = r_se + kRing;
+  uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of multi-window fragments: first body chunk
+  uint32_t* r_cend = r_cpre + kRing;                 //   chunk end
+  uint32_t* r_woe = r_cend + kRing;                  //   window end (GE) relative to wbase
+  uint32_t* r_chl = r_woe + kRing;                   //   C | hi of the last window << 16
+  uint32_t* r_J = r_chl + kRing;
   uint32_t* r_V1 = r_J + kRing;
   uint32_t* r_fi = r_V1 + kRing;
   uint32_t* s_mark = r_fi + kRing;                   // 64 pass markers
@@ -628,6 +679,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
   const uint64_t b0 = nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
   const uint64_t f0 = fbase[b0];
+  const int64_t wbase = (int64_t)start_off + (int64_t)b0 * kBlock - 128;  // below every window of the wave
   uint64_t f1 = fbase[b1];
   if (f1 > frag_cap) f1 = frag_cap;
   const uint32_t nfr = f1 > f0 ? (uint32_t)(f1 - f0) : 0u;
@@ -680,10 +732,11 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     const uint32_t tot = __shfl(incl, 63, 64);
     if (multi) {
       const uint32_t a = (r_tail + below) & (kRing - 1);
+      const int64_t ge = geo.gs + (int64_t)(e - s);
       r_cpre[a] = cbase + incl - cb;
       r_cend[a] = cbase + incl;
-      r_blk[a] = blk;
-      r_se[a] = s | (e << 16);
+      r_woe[a] = (uint32_t)(geo.GE - wbase);
+      r_chl[a] = geo.C | ((uint32_t)(ge - (geo.GE - 128)) << 16);
       r_J[a] = J;
       r_V1[a] = V;
       r_fi[a] = fi;
@@ -693,11 +746,17 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     wave_sync();
   };
 
-  // make the ring hold every fragment owning a chunk of [pass, pass+64)
+  // make the ring hold every fragment owning a chunk of [pass, pass+64): drop entries ending at or
+  // before `pass` (chunk ends increase along the ring, so the dead entries are a ballot prefix)
   auto advance = [&](uint32_t pass, uint32_t (&scratch)[32]) {
     auto evict = [&]() {
-      while (r_head < r_tail && (uint32_t)__builtin_amdgcn_readfirstlane(r_cend[r_head & (kRing - 1)]) <= pass)
-        ++r_head;
+      for (;;) {
+        const uint32_t a = r_head + lane;
+        const bool dead = a < r_tail && r_cend[a & (kRing - 1)] <= pass;
+        const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(dead));
+        r_head += n;
+        if (n < 64u) break;
+      }
     };
     evict();
     while (kwin < nwin && cbase < pass + 64u) {
@@ -726,71 +785,95 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     const uint32_t hm = wave_max_scan(m, lane);
     // lanes before the first marker continue the ring head (the fragment carried from the last pass)
     const uint32_t a = r_head + (hm ? (hm & 0xffffu) - 1u : 0u);
-    d.active = j < cbase && a < r_tail;
-    if (!d.active) return d;
+    if (!(j < cbase && a < r_tail)) return d;  // inactive (meta = 0)
     const uint32_t slot = a & (kRing - 1);
-    const uint32_t se = r_se[slot];
-    const uint32_t cpre = r_cpre[slot];
-    const FragGeo geo = frag_geo(start_off, r_blk[slot], se & 0xffffu, se >> 16);
-    d.cfb = j - cpre;
-    const uint32_t c = geo.C - 2u - d.cfb;  // windows from the end (0 = last)
-    d.last = c == 0u;
-    d.goff = geo.GE - 128 * (int64_t)(c + 1u);
-    const int64_t ge = geo.gs + (int64_t)((se >> 16) - (se & 0xffffu));
-    d.hi = d.last ? (uint32_t)(ge - d.goff) : 0u;
+    const uint32_t chl = r_chl[slot];
+    const uint32_t cfb = j - r_cpre[slot];
+    const uint32_t c = (chl & 0xffffu) - 2u - cfb;  // windows from the end (0 = last)
+    d.woff = r_woe[slot] - 128u * (c + 1u);
+    d.meta = (c == 0u ? (chl >> 16) : 0u) | (cfb << 8) | ((c == 0u ? 1u : 0u) << 17) | (1u << 18);
     d.J = r_J[slot];
-    d.seed = d.cfb == 0u ? r_V1[slot] : 0u;
-    d.gfrag = f0 + r_fi[slot];
+    d.seed = cfb == 0u ? r_V1[slot] : 0u;
+    d.fi = r_fi[slot];
     return d;
   };
 
   auto issue = [&](const BodyDesc& d, uint32_t (&w)[32]) {
     if (ABL & 2) return;
-    const bool inb = __all(!d.active || (d.goff >= 0 && (uint64_t)d.goff + 128 <= seg_len));
-    if (d.active) load_window(seg, seg_len, d.goff, inb, w);
+    const int64_t goff = wbase + d.woff;
+    const bool inb = __all(!d.active() || (goff >= 0 && (uint64_t)goff + 128 <= seg_len));
+    if (!(ABL & 32)) {
+      if (d.active()) load_window(seg, seg_len, goff, inb, w);
+    } else if (inb) {
+      load_windows_quad<false>(seg, seg_len, wbase, d.woff, d.active(), lane, w);
+    } else {
+      load_windows_quad<true>(seg, seg_len, wbase, d.woff, d.active(), lane, w);
+    }
   };
 
   uint32_t carry = 0;  // fragment state at the end of the previous pass (lane 63)
   auto compute = [&](const BodyDesc& d, uint32_t (&w)[32]) {
     uint32_t v = 0;
-    if (d.active) {
-      if (d.last) fix_last(w, d.hi, d.J);
+    if ((ABL & 32) && !(ABL & 64)) quad_windows_transpose(w, lane);
+    if (d.active()) {
+      if (d.last()) fix_last(w, d.hi(), d.J);
+      // a fragment continuing from the previous pass: its state so far seeds lane 0's chain
+      const uint32_t seed = (lane == 0u && d.cfb() > 0u) ? carry : d.seed;
       if (!(ABL & 1)) {
-        v = crc_window(s_slice, s_half, lb, d.seed, w);
+        v = crc_window(s_slice, s_half, lb, seed, w);
       } else {
-        v = d.seed ^ w[0] ^ w[31];
+        v = seed ^ w[0] ^ w[31];
       }
-      // U-domain: lane l holds A_{1024(63-l)} of its window state; the pass carry enters at lane 0
+      // U-domain: lane l holds A_{1024(63-l)} of its window state
       if (!(ABL & 4)) v = apply_fwd(s_fwd, lane, v);
-      if (lane == 0u && d.cfb > 0u) v ^= apply_op(s_carry, carry);
     }
     uint32_t U = v;
     if (!(ABL & 4)) {
-      const uint32_t segl = d.active ? (d.cfb > lane ? 0u : lane - d.cfb) : lane;
+      const uint32_t segl = d.active() ? (d.cfb() > lane ? 0u : lane - d.cfb()) : lane;
       U = wave_seg_xor_scan(v, lane, segl);
     }
-    if (d.active && d.last) frags[d.gfrag].ok = (U == 0u) ? 1 : 0;
+    if (d.active() && d.last()) frags[f0 + d.fi].ok = (U == 0u) ? 1 : 0;
     carry = __builtin_amdgcn_readlane(U, 63);
   };
 
   // software pipeline: the next pass's windows are in flight while this pass chains
+  // (ABL & 16: per-phase cycle stamps for tools/kbench, summed into misc[7..9])
+  uint64_t t_desc = 0, t_issue = 0, t_comp = 0, tq = 0;
+  auto stamp = [&](uint64_t& acc) {
+    if (ABL & 16) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      acc += t - tq;
+      tq = t;
+    }
+  };
+  // One copy of the loop body (instruction-cache footprint): wx holds the pass being chained, wy the
+  // next pass in flight; after chaining, wx is the head-pass scratch of advance(), then takes wy.
+  // The first two iterations only fill the pipeline (p < 0).
   uint32_t wx[32], wy[32];
-  uint32_t pass = 0;
-  advance(0u, wx);
-  BodyDesc dx = describe(0u), dy;
-  issue(dx, wx);
-  while (pass < cbase) {
-    advance(pass + 64u, wy);
-    dy = describe(pass + 64u);
+  BodyDesc dx{}, dy{};
+  if (ABL & 16) tq = __builtin_amdgcn_s_memtime();
+  for (int64_t p = -128;;) {
+    if (p >= 0) {
+      stamp(t_issue);
+      compute(dx, wx);
+      stamp(t_comp);
+    }
+    p += 64;
+    if (p >= 0 && (uint64_t)p >= cbase) break;
+    const uint32_t pn = (uint32_t)(p + 64);  // pass to describe and load
+    advance(pn, wx);
+#pragma unroll
+    for (int k2 = 0; k2 < 32; ++k2) wx[k2] = wy[k2];
+    dx = dy;
+    dy = describe(pn);
+    stamp(t_desc);
     issue(dy, wy);
-    compute(dx, wx);
-    pass += 64u;
-    if (pass >= cbase) break;
-    advance(pass + 64u, wx);
-    dx = describe(pass + 64u);
-    issue(dx, wx);
-    compute(dy, wy);
-    pass += 64u;
+  }
+  stamp(t_comp);
+  if ((ABL & 16) && lane == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&misc[7]), (unsigned long long)t_desc);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&misc[8]), (unsigned long long)t_issue);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&misc[9]), (unsigned long long)t_comp);
   }
 
   if (ABL & 8) return;

@@ -18,6 +18,124 @@ __global__ __launch_bounds__(256) void k_stream(const uint4* __restrict__ p, uin
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+// access-pattern probe: each wave reads consecutive 8 KiB pieces = 64 windows x 8 pieces of 16 B;
+// G lanes share a window per instruction (G=1: window per lane, G=8: 1 KiB contiguous per instruction)
+template <int G, bool REGION = false>
+__global__ __launch_bounds__(1024) void k_pattern(const uint8_t* __restrict__ p, uint64_t n, uint32_t* out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = (uint64_t)gridDim.x * 16, w0 = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
+  const uint64_t npiece = n / 8192;
+  const uint64_t per = npiece / nw;  // REGION: wave w0 reads pieces [w0*per, (w0+1)*per) in order
+  constexpr int S = 64 / G, PG = 8 / G;
+  uint32_t acc = 0;
+  uint4 v[8];
+  for (uint64_t it = 0; it < (REGION ? per : (npiece - w0 + nw - 1) / nw); ++it) {
+    const uint64_t q = REGION ? w0 * per + it : w0 + it * nw;
+    const uint8_t* b = p + q * 8192;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const uint32_t win = lane / G + S * (g / PG), piece = G * (g % PG) + lane % G;
+      v[g] = *reinterpret_cast<const uint4*>(b + 128 * win + 16 * piece);
+    }
+#pragma unroll
+    for (int g = 0; g < 8; ++g) acc ^= v[g].x ^ v[g].y ^ v[g].z ^ v[g].w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// core probe: the k_crc pass loop stripped to quad loads (1 pass ahead) + transpose + CRC chain of
+// every 128 B window of a contiguous per-wave region; no fragments, descriptors or combine.
+// MODE bit 0: skip transpose, bit 1: lane-window (G1) loads instead of quad loads, bit 2: no loads
+// (registers seeded from the lane), bit 3: no chain (all 32 words folded with xor)
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_core(const uint8_t* __restrict__ p, uint64_t n, const uint32_t* img,
+                                                uint32_t* out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsImage];
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kLdsImage; i += 1024) lds[i] = img[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, lb = (lane & 31u) * 4u;
+  const uint64_t nw = (uint64_t)gridDim.x * 16, w0 = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
+  const uint64_t per = n / 8192 / nw;
+  const uint8_t* base = p + w0 * per * 8192;
+  uint32_t wx[32], wy[32], acc = 0;
+  auto issue = [&](uint64_t it, uint32_t (&w)[32]) {
+    if (it >= per) return;
+    if (MODE & 4) {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) w[k] = (uint32_t)(it * 2654435761u) ^ (lane * 40503u + k);
+      return;
+    }
+    const uint8_t* b = base + it * 8192;
+    if (MODE & 2) {
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const uint4 v = *reinterpret_cast<const uint4*>(b + 128 * lane + 16 * g);
+        w[4 * g] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+      }
+    } else {
+      bcw::load_windows_quad<false>(b, ~0ull, 0, 128u * lane, true, lane, w);
+    }
+  };
+  issue(0, wx);
+  for (uint64_t it = 0; it < per; ++it) {
+    issue(it + 1, wy);
+    if (!(MODE & 3)) bcw::quad_windows_transpose(wx, lane);
+    if (MODE & 8) {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) acc ^= wx[k];
+    } else {
+      acc ^= bcw::crc_window(lds, lds + kLdsSlice + kLdsFwd + 128, lb, acc, wx);
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) wx[k] = wy[k];
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// prefetch-depth probe: WAVES waves per CU, loads DEPTH passes ahead (DEPTH+1 window buffers), chain
+template <int WAVES, int DEPTH, bool QUAD, int ROT = 0, bool CHAIN = true>
+__global__ __launch_bounds__(WAVES * 64) void k_depth(const uint8_t* __restrict__ p, uint64_t n, const uint32_t* img,
+                                                       uint32_t* out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsImage];
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kLdsImage; i += WAVES * 64) lds[i] = img[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, lb = (lane & 31u) * 4u;
+  const uint64_t nw = (uint64_t)gridDim.x * WAVES, w0 = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  const uint64_t per = n / 8192 / nw;
+  const uint8_t* base = p + w0 * per * 8192;
+  uint32_t w[DEPTH + 1][32], acc = 0;
+  auto issue = [&](uint64_t it, uint32_t (&b)[32]) {
+    if (it >= per) return;
+    const uint8_t* q = base + ((it + (ROT ? w0 * ROT : 0)) % per) * 8192;
+    if (QUAD) {
+      bcw::load_windows_quad<false>(q, ~0ull, 0, 128u * lane, true, lane, b);
+    } else {
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const uint4 v = *reinterpret_cast<const uint4*>(q + 128 * lane + 16 * g);
+        b[4 * g] = v.x; b[4 * g + 1] = v.y; b[4 * g + 2] = v.z; b[4 * g + 3] = v.w;
+      }
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < DEPTH; ++k) issue(k, w[k]);
+  for (uint64_t it = 0; it < per; ++it) {
+    issue(it + DEPTH, w[DEPTH]);
+    if (QUAD) bcw::quad_windows_transpose(w[0], lane);
+    if (CHAIN) {
+      acc ^= bcw::crc_window(lds, lds + kLdsSlice + kLdsFwd + 128, lb, acc, w[0]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) acc ^= w[0][k];
+    }
+#pragma unroll
+    for (int b = 0; b < DEPTH; ++b)
+#pragma unroll
+      for (int k = 0; k < 32; ++k) w[b][k] = w[b + 1][k];
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 template <typename F>
 static float timeit(F f, int reps, hipStream_t st) {
   hipEvent_t a, b;
@@ -86,6 +204,51 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dout, 4));
     const float ms = timeit([&] { k_stream<<<cus * 16, 256, 0, st>>>((const uint4*)d, n / 16, dout); }, reps, st);
     printf("stream read     %.4f ms  %.1f GB/s\n", ms, n / (ms * 1e-3) / 1e9);
+    const float m1 = timeit([&] { k_pattern<1><<<cus, 1024, 0, st>>>(d, n, dout); }, reps, st);
+    const float m2 = timeit([&] { k_pattern<2><<<cus, 1024, 0, st>>>(d, n, dout); }, reps, st);
+    const float m4 = timeit([&] { k_pattern<4><<<cus, 1024, 0, st>>>(d, n, dout); }, reps, st);
+    const float m8 = timeit([&] { k_pattern<8><<<cus, 1024, 0, st>>>(d, n, dout); }, reps, st);
+    printf("pattern GB/s by lanes per window per instruction: G1 %.0f  G2 %.0f  G4 %.0f  G8 %.0f\n",
+           n / (m1 * 1e-3) / 1e9, n / (m2 * 1e-3) / 1e9, n / (m4 * 1e-3) / 1e9, n / (m8 * 1e-3) / 1e9);
+    const float r1 = timeit([&] { k_pattern<1, true><<<cus, 1024, 0, st>>>(d, n, dout); }, reps, st);
+    const float r4 = timeit([&] { k_pattern<4, true><<<cus, 1024, 0, st>>>(d, n, dout); }, reps, st);
+    const float r8 = timeit([&] { k_pattern<8, true><<<cus, 1024, 0, st>>>(d, n, dout); }, reps, st);
+    printf("pattern, contiguous region per wave: G1 %.0f  G4 %.0f  G8 %.0f GB/s\n", n / (r1 * 1e-3) / 1e9,
+           n / (r4 * 1e-3) / 1e9, n / (r8 * 1e-3) / 1e9);
+    const uint32_t* img = ctx->tabs.lds_image;
+    const float c0 = timeit([&] { k_core<0><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float c1 = timeit([&] { k_core<1><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float c2 = timeit([&] { k_core<2><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    printf("core (loads+chain): quad+transpose %.4f  quad no-transpose %.4f  lane-window %.4f ms\n", c0, c1, c2);
+    const float c3 = timeit([&] { k_core<2 | 4><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float c4 = timeit([&] { k_core<2 | 8><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float c5 = timeit([&] { k_core<1 | 8><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    printf("core parts: chain only %.4f  lane-window loads only %.4f  quad loads only %.4f ms\n", c3, c4, c5);
+    const float e1 = timeit([&] { k_depth<16, 1, false><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float e2 = timeit([&] { k_depth<12, 2, false><<<cus, 768, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float e3 = timeit([&] { k_depth<12, 2, true><<<cus, 768, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float e4 = timeit([&] { k_depth<8, 3, false><<<cus, 512, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float e5 = timeit([&] { k_depth<12, 1, false><<<cus, 768, 0, st>>>(d, n, img, dout); }, reps, st);
+    printf("depth: 16w d1 %.4f  12w d2 %.4f  12w d2 quad %.4f  8w d3 %.4f  12w d1 %.4f ms\n", e1, e2, e3, e4, e5);
+    const float f4 = timeit([&] { k_depth<4, 1, false><<<cus, 256, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float f6 = timeit([&] { k_depth<6, 1, false><<<cus, 384, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float f8 = timeit([&] { k_depth<8, 1, false><<<cus, 512, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float f10 = timeit([&] { k_depth<10, 1, false><<<cus, 640, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float f14 = timeit([&] { k_depth<14, 1, false><<<cus, 896, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float g8 = timeit([&] { k_depth<8, 2, false><<<cus, 512, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float g12 = timeit([&] { k_depth<12, 1, true><<<cus, 768, 0, st>>>(d, n, img, dout); }, reps, st);
+    printf("d1 by waves: 4 %.4f  6 %.4f  8 %.4f  10 %.4f  14 %.4f | 8w d2 %.4f | 12w d1 quad %.4f ms\n", f4, f6, f8,
+           f10, f14, g8, g12);
+    const float h1 = timeit([&] { k_depth<16, 1, false, 7><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float h2 = timeit([&] { k_depth<16, 1, false, 1><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float h3 = timeit([&] { k_depth<12, 1, false, 7><<<cus, 768, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float h4 = timeit([&] { k_depth<16, 1, true, 7><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    printf("rotated start: 16w rot7 %.4f  16w rot1 %.4f  12w rot7 %.4f  16w quad rot7 %.4f ms\n", h1, h2, h3, h4);
+    const float i1 = timeit([&] { k_depth<16, 1, false, 0, false><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float i2 = timeit([&] { k_depth<12, 1, false, 0, false><<<cus, 768, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float i3 = timeit([&] { k_depth<16, 1, true, 0, false><<<cus, 1024, 0, st>>>(d, n, img, dout); }, reps, st);
+    const float i4 = timeit([&] { k_depth<12, 1, true, 0, false><<<cus, 768, 0, st>>>(d, n, img, dout); }, reps, st);
+    printf("loads only d1: 16w %.4f  12w %.4f  16w quad %.4f  12w quad %.4f ms\n", i1, i2, i3, i4);
   }
   if (argc > 3) {  // counter-collection mode: only the product k_crc, a few launches
     const int k = atoi(argv[3]);
@@ -103,12 +266,23 @@ int main(int argc, char** argv) {
   printf("k_crc loads+comb only (no chain, no loads) %.4f ms\n", a3);
   printf("k_crc skeleton (1|2|4) %.4f ms\n", a7);
   printf("k_crc no tail   %.4f ms\n", a8);
+  const float q1 = run(k_crc<32>, cus);
+  printf("quad-layout loads: full %.4f ms\n", q1);
   const float as = timeit([&] {
     hipMemsetAsync(&s.misc[5], 0, 8, st);  // M_DONE_CRC: the last workgroup runs the aggregate scan
     k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, s.pre, s.wgagg,
                                           s.wgx, s.misc);
   }, reps, st);
   printf("k_crc + scan    %.4f ms\n", as);
+  {
+    CK(hipMemset(&s.misc[7], 0, 24));
+    run(k_crc<16 | 8>, cus);
+    uint64_t m[3];
+    CK(hipMemcpy(m, &s.misc[7], 24, hipMemcpyDeviceToHost));
+    const double w = (double)cus * kCrcWaves * (reps + 1);  // waves x launches
+    printf("  phase cycles per wave (s_memtime): describe %.0f  issue %.0f  compute %.0f\n", m[0] / w, m[1] / w,
+           m[2] / w);
+  }
   {
     uint64_t m[16];
     CK(hipMemcpy(m, s.misc, sizeof m, hipMemcpyDeviceToHost));
