@@ -78,6 +78,17 @@ __device__ __forceinline__ uint32_t wave_max_scan(uint32_t v, uint32_t lane) {
   t = dpp_mov<0x143>(v); if (lane >= 32u) v = max(v, t);
   return v;
 }
+__device__ __forceinline__ uint32_t wave_or_scan(uint32_t v, uint32_t lane) {
+  const uint32_t rl = lane & 15u;
+  uint32_t t;
+  t = dpp_mov<0x111>(v); if (rl >= 1u) v |= t;
+  t = dpp_mov<0x112>(v); if (rl >= 2u) v |= t;
+  t = dpp_mov<0x114>(v); if (rl >= 4u) v |= t;
+  t = dpp_mov<0x118>(v); if (rl >= 8u) v |= t;
+  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v |= t;
+  t = dpp_mov<0x143>(v); if (lane >= 32u) v |= t;
+  return v;
+}
 // segmented inclusive XOR scan; seg = first lane of this lane's segment
 __device__ __forceinline__ uint32_t wave_seg_xor_scan(uint32_t v, uint32_t lane, uint32_t seg) {
   const uint32_t rl = lane & 15u;
@@ -452,8 +463,8 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 constexpr int kRing = 128;               // ring of multi-window fragments per wave
-constexpr int kRingWords = 7;            // cpre, cend, window end, C | last hi, J, V1, fragment index
-constexpr int kWaveLds = kRing * kRingWords + 64;  // + 64 pass markers
+constexpr int kRingWords = 10;           // cpre, cend (SoA) + 8-word entry record (AoS)
+constexpr int kWaveLds = kRing * kRingWords;
 constexpr size_t kCrcLds = (size_t)(kLdsSlice + kLdsFwd + kLdsOps + kCrcWaves * kWaveLds) * 4;
 
 // CRC-32C (zero xor-out, no final inversion) of one 128 B window from state `seed`: two slice-by-2
@@ -668,13 +679,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of multi-window fragments: first body chunk
   uint32_t* r_cend = r_cpre + kRing;                 //   chunk end
-  uint32_t* r_woe = r_cend + kRing;                  //   window end (GE) relative to wbase
-  uint32_t* r_chl = r_woe + kRing;                   //   C | hi of the last window << 16
-  uint32_t* r_J = r_chl + kRing;
-  uint32_t* r_V1 = r_J + kRing;
-  uint32_t* r_fi = r_V1 + kRing;
-  uint32_t* s_mark = r_fi + kRing;                   // 64 pass markers
-
+  uint4* r_ent = reinterpret_cast<uint4*>(r_cend + kRing);  // {window end (GE) - wbase, C | last hi << 16, J, V1},
+                                                             // {fragment index, cpre, -, -}
   const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
   const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
   const uint64_t b0 = nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
@@ -735,11 +741,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       const int64_t ge = geo.gs + (int64_t)(e - s);
       r_cpre[a] = cbase + incl - cb;
       r_cend[a] = cbase + incl;
-      r_woe[a] = (uint32_t)(geo.GE - wbase);
-      r_chl[a] = geo.C | ((uint32_t)(ge - (geo.GE - 128)) << 16);
-      r_J[a] = J;
-      r_V1[a] = V;
-      r_fi[a] = fi;
+      r_ent[2 * a] = make_uint4((uint32_t)(geo.GE - wbase), geo.C | ((uint32_t)(ge - (geo.GE - 128)) << 16), J, V);
+      r_ent[2 * a + 1] = make_uint4(fi, cbase + incl - cb, 0u, 0u);
     }
     r_tail += (uint32_t)__builtin_popcountll(mm);
     cbase += __builtin_amdgcn_readfirstlane(tot);
@@ -765,36 +768,36 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     }
   };
 
+  // lane l's chunk pass + l belongs to the last ring entry whose first chunk is <= pass + l: entries
+  // starting inside the pass set bits of a 64-bit mask (OR over the wave), a popcount of the mask up
+  // to the lane counts them, and the ring head continues any fragment carried into the pass
   auto describe = [&](uint32_t pass) -> BodyDesc {
     BodyDesc d{};
     const uint32_t j = pass + lane;
-    // markers: ring entries whose first body chunk falls in this pass
-    wave_sync();
-    s_mark[lane] = 0;
-    wave_sync();
-#pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) {
-      const uint32_t a = r_head + lane + 64u * q;
-      if (a < r_tail) {
-        const uint32_t c = r_cpre[a & (kRing - 1)];
-        if (c >= pass && c < pass + 64u) s_mark[c - pass] = ((c - pass + 1u) << 16) | (a - r_head + 1u);
-      }
-    }
-    wave_sync();
-    const uint32_t m = s_mark[lane];
-    const uint32_t hm = wave_max_scan(m, lane);
-    // lanes before the first marker continue the ring head (the fragment carried from the last pass)
-    const uint32_t a = r_head + (hm ? (hm & 0xffffu) - 1u : 0u);
-    if (!(j < cbase && a < r_tail)) return d;  // inactive (meta = 0)
+    const uint32_t a0 = r_head + lane, a1 = a0 + 64u;
+    const uint32_t c0 = a0 < r_tail ? r_cpre[a0 & (kRing - 1)] : 0xffffffffu;
+    const uint32_t c1 = a1 < r_tail ? r_cpre[a1 & (kRing - 1)] : 0xffffffffu;
+    uint64_t bits = 0;
+    if (c0 >= pass && c0 - pass < 64u) bits |= 1ull << (c0 - pass);
+    if (c1 >= pass && c1 - pass < 64u) bits |= 1ull << (c1 - pass);
+    const uint32_t mlo = __builtin_amdgcn_readlane(wave_or_scan(( uint32_t)bits, lane), 63);
+    const uint32_t mhi = __builtin_amdgcn_readlane(wave_or_scan((uint32_t)(bits >> 32), lane), 63);
+    const uint64_t M = (uint64_t)mlo | ((uint64_t)mhi << 32);
+    const uint32_t carried = (r_head < r_tail && (uint32_t)__builtin_amdgcn_readfirstlane(c0) < pass) ? 1u : 0u;
+    const uint64_t upto = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+    const uint32_t cnt = carried + (uint32_t)__builtin_popcountll(M & upto);
+    const uint32_t a = r_head + cnt - 1u;
+    if (!(cnt > 0u && j < cbase && a < r_tail)) return d;  // inactive (meta = 0)
     const uint32_t slot = a & (kRing - 1);
-    const uint32_t chl = r_chl[slot];
-    const uint32_t cfb = j - r_cpre[slot];
+    const uint4 e0 = r_ent[2 * slot], e1 = r_ent[2 * slot + 1];
+    const uint32_t chl = e0.y;
+    const uint32_t cfb = j - e1.y;
     const uint32_t c = (chl & 0xffffu) - 2u - cfb;  // windows from the end (0 = last)
-    d.woff = r_woe[slot] - 128u * (c + 1u);
+    d.woff = e0.x - 128u * (c + 1u);
     d.meta = (c == 0u ? (chl >> 16) : 0u) | (cfb << 8) | ((c == 0u ? 1u : 0u) << 17) | (1u << 18);
-    d.J = r_J[slot];
-    d.seed = cfb == 0u ? r_V1[slot] : 0u;
-    d.fi = r_fi[slot];
+    d.J = e0.z;
+    d.seed = cfb == 0u ? e0.w : 0u;
+    d.fi = e1.x;
     return d;
   };
 
@@ -846,13 +849,15 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       tq = t;
     }
   };
-  // One copy of the loop body (instruction-cache footprint): wx holds the pass being chained, wy the
-  // next pass in flight; after chaining, wx is the head-pass scratch of advance(), then takes wy.
-  // The first two iterations only fill the pipeline (p < 0).
+  // One copy of the loop body (instruction-cache footprint). At the top of an iteration wx holds pass
+  // p (chained now), wy the loads of pass p+64 in flight, dz the descriptors of pass p+128. After
+  // the chain: advance the ring (wx is the head-pass scratch), take wy into wx, issue pass p+128's
+  // loads, then describe pass p+192 -- descriptor work is off the load-to-load critical path.
+  // The first three iterations only fill the pipeline (p < 0).
   uint32_t wx[32], wy[32];
-  BodyDesc dx{}, dy{};
+  BodyDesc dx{}, dy{}, dz{};
   if (ABL & 16) tq = __builtin_amdgcn_s_memtime();
-  for (int64_t p = -128;;) {
+  for (int64_t p = -192;;) {
     if (p >= 0) {
       stamp(t_issue);
       compute(dx, wx);
@@ -860,14 +865,14 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     }
     p += 64;
     if (p >= 0 && (uint64_t)p >= cbase) break;
-    const uint32_t pn = (uint32_t)(p + 64);  // pass to describe and load
-    advance(pn, wx);
+    advance((uint32_t)(p + 128), wx);
 #pragma unroll
     for (int k2 = 0; k2 < 32; ++k2) wx[k2] = wy[k2];
     dx = dy;
-    dy = describe(pn);
+    issue(dz, wy);
+    dy = dz;
     stamp(t_desc);
-    issue(dy, wy);
+    dz = describe((uint32_t)(p + 128));
   }
   stamp(t_comp);
   if ((ABL & 16) && lane == 0) {
