@@ -237,7 +237,7 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
 
 static void free_scratch(Scratch& s) {
   (void)hipFree(s.fbase);
-  (void)hipFree(s.wgsum);
+  (void)hipFree(s.lb);
   (void)hipFree(s.frags);
   (void)hipFree(s.pre);
   (void)hipFree(s.wgagg);
@@ -288,7 +288,7 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   const uint64_t fc = std::max(frag_cap, s.frag_cap);
   free_scratch(s);
   const uint64_t nwg = nb / 256 + 2;
-  bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.wgsum, nwg * 4) == hipSuccess &&
+  bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
             hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
             hipMalloc(&s.pre, (nb + 1) * sizeof(Xf)) == hipSuccess &&
             hipMalloc(&s.wgagg, nwave * sizeof(Xf)) == hipSuccess &&
@@ -298,6 +298,13 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   s.nblocks_cap = nb;
   s.frag_cap = fc;
   s.nwave_cap = nwave;
+  s.nlb = nwg;
+  s.tickets = 0;
+  s.epoch = 1;
+  if (hipMemset(s.lb, 0, nwg * 8) != hipSuccess || hipMemset(s.misc, 0, 16 * sizeof(uint64_t)) != hipSuccess) {
+    free_scratch(s);
+    return BCW_E_HIP;
+  }
   return BCW_OK;
 }
 
@@ -345,7 +352,7 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
   return launch_export_frags(c->s, *d_frags, c->last_start_off, c->cur, n) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_chase_count", "k_scan_wg", "k_chase_write", "k_crc", "k_records"};
+static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_records"};
 
 int bcw_ctx_set_profiling(bcw_ctx* c, int mask) {
   if (!c) return BCW_E_INVAL;

@@ -25,7 +25,8 @@ namespace bcw {
 // ------------------------------------------------------------------------------------------
 // misc counters (Scratch::misc)
 enum { M_FIRST_BAD = 0, M_NREC = 1, M_ERR_FRAG = 2, M_ERR_CLASS = 3, M_NFRAGS = 4, M_DONE_CRC = 5, M_DONE_REC = 6,
-       M_T_CRC0 = 10, M_T_SCAN0 = 11, M_T_SCAN1 = 12 };  // wall_clock64 stamps (diagnostics)
+       M_T_CRC0 = 10, M_T_SCAN0 = 11, M_T_SCAN1 = 12,  // wall_clock64 stamps (diagnostics)
+       M_TICKET = 13 };  // k_chase workgroup tickets (monotonic across launches)
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
@@ -127,94 +128,135 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 }
 
 // ------------------------------------------------------------------------------------------
-// Header chase of one block: WalIterator refill + header loop (wal_iterator.go:45-77). The block's
-// buffer is min(32768, Size - fileOff) bytes; a header is parsed while bufOff + 7 <= bufSize; the
-// data length is clamped to the buffer.
-template <bool WRITE>
-__device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg, uint64_t seg_len,
-                                                uint32_t start_off, uint64_t b, Frag* __restrict__ frags,
-                                                uint64_t g0, uint64_t frag_cap) {
-  const uint64_t boff = (uint64_t)start_off + b * kBlock;
-  const uint32_t bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
-  uint32_t h = 0, n = 0;
-  while (h + kHdr <= bufsize) {
+// Single-pass header chase with a decoupled look-back over workgroups: every thread chases one block
+// (holding its first kChaseHold headers in registers), the workgroup scans the counts, publishes its
+// aggregate and walks back over earlier workgroups' published values for its fragment base, then the
+// headers are written to the fragment table (blocks with more fragments chase their tail again).
+// Workgroups take tickets in launch order, so a workgroup only ever waits on ones already running.
+// Look-back words: epoch << 40 | flag << 38 | count (flag 1: aggregate, 2: inclusive prefix).
+constexpr int kChaseHold = 16;
+constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
+
+__device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, uint64_t frag_cap, uint32_t b,
+                                         uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
+  if (g >= frag_cap) return;
+  Frag f;
+  f.blk = b;
+  f.start = (uint16_t)start;
+  f.len = (uint16_t)len;
+  f.crc = crc;
+  f.type = (uint8_t)type;
+  f.ok = 0;
+  f.pad = 0;
+  frags[g] = f;
+}
+
+__global__ __launch_bounds__(256) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
+                                               uint64_t nblocks, uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
+                                               uint64_t frag_cap, uint64_t* __restrict__ lb, uint64_t* __restrict__ misc,
+                                               uint64_t ticket_base, uint64_t epoch) {
+  __shared__ uint32_t sm4[4];
+  __shared__ uint64_t s_wg, s_excl;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) s_wg = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_TICKET]), 1ull) - ticket_base;
+  __syncthreads();
+  const uint64_t wg = s_wg;
+  const uint64_t b = wg * 256 + tid;
+  // WalIterator refill + header loop (wal_iterator.go:45-77): the block's buffer is
+  // min(32768, Size - fileOff) bytes, a header is parsed while bufOff + 7 <= bufSize, and the data
+  // length is clamped to the buffer
+  uint32_t hs[kChaseHold], hc[kChaseHold], ht[kChaseHold / 4];
+  uint32_t n = 0, h = 0, h_hold = 0, bufsize = 0;
+  uint64_t boff = 0;
+  if (b < nblocks) {
+    boff = (uint64_t)start_off + b * kBlock;
+    bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
+  }
+#pragma unroll
+  for (int k = 0; k < kChaseHold / 4; ++k) ht[k] = 0;
+#pragma unroll
+  for (int k = 0; k < kChaseHold; ++k) {
+    hs[k] = 0;
+    hc[k] = 0;
+    if (h + kHdr <= bufsize) {
+      uint32_t crc, len, type;
+      read_header(seg, seg_len, boff + h, crc, len, type);
+      const uint32_t start = h + kHdr;
+      if (len > bufsize - start) len = bufsize - start;
+      hs[k] = start | (len << 16);
+      hc[k] = crc;
+      ht[k >> 2] |= type << (8 * (k & 3));
+      h = start + len;
+      ++n;
+    }
+  }
+  h_hold = h;
+  while (h + kHdr <= bufsize) {  // blocks with more fragments: count the rest
     uint32_t crc, len, type;
     read_header(seg, seg_len, boff + h, crc, len, type);
     const uint32_t start = h + kHdr;
     if (len > bufsize - start) len = bufsize - start;
-    if (WRITE && g0 + n < frag_cap) {
-      Frag f;
-      f.blk = (uint32_t)b;
-      f.start = (uint16_t)start;
-      f.len = (uint16_t)len;
-      f.crc = crc;
-      f.type = (uint8_t)type;
-      f.ok = 0;
-      f.pad = 0;
-      frags[g0 + n] = f;
-    }
     h = start + len;
     ++n;
   }
-  return n;
-}
-
-// pass 1: count fragments per block, workgroup-local exclusive prefix -> fbase[b], wg totals
-__global__ __launch_bounds__(256) void k_chase_count(const uint8_t* __restrict__ seg, uint64_t seg_len,
-                                                     uint32_t start_off, uint64_t nblocks,
-                                                     uint32_t* __restrict__ fbase, uint32_t* __restrict__ wgsum) {
-  __shared__ uint32_t sm4[4];
-  const uint64_t b = blockIdx.x * 256ull + threadIdx.x;
-  const uint32_t n = b < nblocks ? chase_block<false>(seg, seg_len, start_off, b, nullptr, 0, 0) : 0u;
   uint32_t tot;
   const uint32_t ex = wg256_excl_scan(n, sm4, tot);
-  if (b < nblocks) fbase[b] = ex;
-  if (threadIdx.x == 0) wgsum[blockIdx.x] = tot;
-}
-
-// exclusive scan of the per-workgroup totals (one workgroup); fbase[nblocks] = total
-__global__ __launch_bounds__(1024) void k_scan_wg(uint32_t* __restrict__ wgsum, uint64_t nwg,
-                                                  uint32_t* __restrict__ fbase, uint64_t nblocks,
-                                                  uint64_t* __restrict__ total) {
-  __shared__ uint64_t sm[1024];
-  const uint32_t t = threadIdx.x;
-  const uint64_t per = (nwg + 1023) / 1024;
-  const uint64_t lo = t * per;
-  const uint64_t hi = lo + per < nwg ? lo + per : nwg;
-  uint64_t s = 0;
-  for (uint64_t i = lo; i < hi; ++i) s += wgsum[i];
-  sm[t] = s;
+  if (tid < 64) {  // wave 0: publish, then look back 64 workgroups per step
+    const uint32_t lane = tid;
+    const uint64_t tag = epoch << 40;
+    if (lane == 0)
+      __hip_atomic_store(&lb[wg], tag | ((wg == 0 ? kLbInc : kLbAgg) << 38) | tot, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    for (uint64_t top = wg; top > 0;) {  // predecessors [top - 64, top)
+      const uint64_t q = top - 1 - lane;  // lane 0: the nearest
+      uint64_t v = 0;
+      if (top > lane) {
+        while (((v = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      const uint64_t inc = __ballot(top > lane && ((v >> 38) & 3u) == kLbInc);
+      const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive prefix
+      uint64_t c = (lane <= stop && top > lane) ? (v & kLbMask) : 0ull;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) c += (uint64_t)__shfl_xor((long long)c, d, 64);
+      excl += c;
+      if (inc) break;
+      top = top > 64 ? top - 64 : 0;
+    }
+    if (lane == 0) {
+      if (wg != 0)
+        __hip_atomic_store(&lb[wg], tag | (kLbInc << 38) | ((excl + tot) & kLbMask), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      s_excl = excl;
+    }
+  }
   __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    const uint64_t v = t >= d ? sm[t - d] : 0;
-    __syncthreads();
-    sm[t] += v;
-    __syncthreads();
+  const uint64_t g0 = s_excl + ex;
+  if (b < nblocks) {
+    fbase[b] = (uint32_t)(g0 < 0xffffffffull ? g0 : 0xffffffffull);
+#pragma unroll
+    for (int k = 0; k < kChaseHold; ++k)
+      if ((uint32_t)k < n)
+        put_frag(frags, g0 + k, frag_cap, (uint32_t)b, hs[k] & 0xffffu, hs[k] >> 16, hc[k], (ht[k >> 2] >> (8 * (k & 3))) & 0xffu);
+    uint64_t g = g0 + kChaseHold;
+    h = h_hold;
+    while (h + kHdr <= bufsize) {  // the tail of a block with more than kChaseHold fragments
+      uint32_t crc, len, type;
+      read_header(seg, seg_len, boff + h, crc, len, type);
+      const uint32_t start = h + kHdr;
+      if (len > bufsize - start) len = bufsize - start;
+      put_frag(frags, g++, frag_cap, (uint32_t)b, start, len, crc, type);
+      h = start + len;
+    }
   }
-  uint64_t run = sm[t] - s;
-  for (uint64_t i = lo; i < hi; ++i) {
-    const uint32_t x = wgsum[i];
-    wgsum[i] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
-    run += x;
+  const uint64_t nwg = (nblocks + 255) / 256;
+  if (wg == nwg - 1 && tid == 255) {
+    const uint64_t total = s_excl + tot;
+    fbase[nblocks] = (uint32_t)(total < 0xffffffffull ? total : 0xffffffffull);
+    misc[M_NFRAGS] = total;
+    misc[M_DONE_CRC] = 0;  // k_crc's workgroup completion counter
   }
-  if (t == 1023) {
-    const uint64_t tot = sm[1023];
-    fbase[nblocks] = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
-    total[0] = tot;                        // misc[M_NFRAGS]
-    total[M_DONE_CRC - M_NFRAGS] = 0;      // k_crc's workgroup completion counter
-  }
-}
-
-// pass 2: fbase[b] = workgroup base + local prefix; chase again (headers cache-resident), write
-__global__ __launch_bounds__(256) void k_chase_write(const uint8_t* __restrict__ seg, uint64_t seg_len,
-                                                     uint32_t start_off, uint64_t nblocks,
-                                                     uint32_t* __restrict__ fbase, const uint32_t* __restrict__ wgbase,
-                                                     Frag* __restrict__ frags, uint64_t frag_cap) {
-  const uint64_t b = blockIdx.x * 256ull + threadIdx.x;
-  if (b >= nblocks) return;
-  const uint32_t g0 = fbase[b] + wgbase[blockIdx.x];
-  fbase[b] = g0;
-  chase_block<true>(seg, seg_len, start_off, b, frags, g0, frag_cap);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1217,17 +1259,15 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   Prof& pr = prof ? *prof : dummy;
   hipEvent_t ev = nullptr;
   const uint32_t nb_grid = (uint32_t)((nblocks + 255) / 256);
-  const uint64_t nwg = (nblocks + 255) / 256;
-  pr.begin(K_CHASE_COUNT, stream, ev);
-  k_chase_count<<<nb_grid, 256, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.wgsum);
-  pr.end(K_CHASE_COUNT, stream, ev);
-  pr.begin(K_SCAN, stream, ev);
-  k_scan_wg<<<1, 1024, 0, stream>>>(s.wgsum, nwg, s.fbase, nblocks, &s.misc[M_NFRAGS]);
-  pr.end(K_SCAN, stream, ev);
-  pr.begin(K_CHASE_WRITE, stream, ev);
-  k_chase_write<<<nb_grid, 256, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.wgsum, s.frags,
-                                             s.frag_cap);
-  pr.end(K_CHASE_WRITE, stream, ev);
+  pr.begin(K_CHASE, stream, ev);
+  k_chase<<<nb_grid, 256, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags, s.frag_cap, s.lb,
+                                       s.misc, s.tickets, s.epoch);
+  pr.end(K_CHASE, stream, ev);
+  s.tickets += nb_grid;
+  if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse
+    (void)hipMemsetAsync(s.lb, 0, s.nlb * sizeof(uint64_t), stream);
+    s.epoch = 1;
+  }
   pr.begin(K_CRC, stream, ev);
   const uint64_t nw = (uint64_t)num_cus * kCrcWaves;
   k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,

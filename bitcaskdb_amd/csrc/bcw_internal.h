@@ -62,7 +62,10 @@ struct Scratch {
   uint64_t nblocks_cap = 0;
   uint64_t frag_cap = 0;
   uint32_t* fbase = nullptr;   // [nblocks+1] global index of each block's first fragment
-  uint32_t* wgsum = nullptr;   // [nblocks/256+1] per-workgroup fragment counts -> bases
+  uint64_t* lb = nullptr;      // [nblocks/256+1] k_chase look-back words (zeroed at allocation)
+  uint64_t nlb = 0;
+  uint64_t tickets = 0;        // k_chase tickets issued so far (misc[M_TICKET] mirrors it)
+  uint64_t epoch = 1;          // look-back epoch of the next launch
   Frag* frags = nullptr;       // [frag_cap]
   Xf* pre = nullptr;           // [nblocks] record-state prefix of each block within its k_crc wave
   Xf* wgagg = nullptr;         // [k_crc waves] wave-exclusive prefix within the k_crc workgroup
@@ -73,7 +76,7 @@ struct Scratch {
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
 // stream around every kernel of the pipeline.
-enum KernelId { K_CHASE_COUNT = 0, K_SCAN, K_CHASE_WRITE, K_CRC, K_RECORDS, K_NUM };
+enum KernelId { K_CHASE = 0, K_CRC, K_RECORDS, K_NUM };
 struct Prof {
   uint32_t mask = 0;  // bit k: time kernel id k
   struct Mark { int kid; hipEvent_t a, b; };
