@@ -61,9 +61,10 @@ def main():
 
     from bitcaskdb_amd import _lib as L
     from bitcaskdb_amd import Context
+    from bitcaskdb_amd import shard
 
     # ---- build this rank's segment on the host with the product writer, then copy to HBM ----
-    seed = 42 + rank
+    seed = shard.segment_seed(42, rank)
     vmode = 0 if args.config == "B" else 1
     n, r = C.c_uint64(), C.c_uint64()
     rc = L.lib.bcw_synth_segment(args.seg_bytes, 0, seed, 20, 100, 4096, vmode, BASE_TIME, None, 0, C.byref(n),
@@ -125,20 +126,14 @@ def main():
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks ----
     # HIP events bracket only the roofline kernel (k_crc) on the codec's stream
     L.lib.bcw_ctx_set_profiling(ctx.handle, 1 << roof_k)
-    kernel_times()  # reset
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
+
+    kernel_times()  # reset (synchronises the codec's stream)
     ev0.record(stream)
-    for _ in range(args.steps):
-        step()
+    # warmup already ran above (with the correctness gate)
+    wall = shard.timed_steps(step, args.steps, 0, torch.cuda.synchronize, dist.barrier if world > 1 else None)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
     crc_ms = kernel_times()["k_crc"]
     # every kernel's average (untimed repeat, events around each kernel)
@@ -148,13 +143,9 @@ def main():
     kern = kernel_times()
     L.lib.bcw_ctx_set_profiling(ctx.handle, 0)
 
-    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    wall_max = float(elapsed.item())
+    wall_max = shard.max_over_ranks(wall, dist, dev)
     ms_per_step = wall_max / args.steps * 1e3
-    total_bytes = seg_len * world
-    value = total_bytes / 2 ** 30 / (wall_max / args.steps)
+    value = shard.aggregate_gib_s([seg_len] * world, wall_max, args.steps)  # same-size segment per rank
 
     # end-to-end PCIe-inclusive rate (pinned H2D of the segment + decode), rank 0 only, not `value`
     pcie = None
