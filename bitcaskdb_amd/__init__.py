@@ -6,9 +6,11 @@ is the Python host mirror of the reference interface (wal.py) and its ctypes bin
 from . import _lib
 from .wal import (Context, Decoded, ErrCorruptedHintRecord, ErrInvalidData, ErrShortFile, ErrWalMismatchBlockSize,
                   ErrWalMismatchCRC, ErrWalMismatchMagic, ErrWalUnknownRecordType, HintRecord, Meta, Record,
-                  RefPanic, Wal, WalError, compute_crc32, default_context, iterate_hint, iterate_record, load_wal)
+                  RefPanic, Wal, WalError, WalFile, compact_one_wal, compute_crc32, default_context, iterate_hint,
+                  iterate_record, load_wal, new_hint_by_wal)
 
 __all__ = ["Context", "Decoded", "ErrCorruptedHintRecord", "ErrInvalidData", "ErrShortFile",
            "ErrWalMismatchBlockSize", "ErrWalMismatchCRC", "ErrWalMismatchMagic", "ErrWalUnknownRecordType",
            "HintRecord", "Meta", "Record", "RefPanic", "Wal", "WalError", "compute_crc32", "default_context",
-           "iterate_hint", "iterate_record", "load_wal", "_lib"]
+           "iterate_hint", "iterate_record", "load_wal", "_lib", "WalFile", "compact_one_wal",
+           "new_hint_by_wal"]

@@ -43,6 +43,23 @@ class FragTable(C.Structure):
                 ("type", u8p), ("crc_ok", u8p)]
 
 
+class EncodeParams(C.Structure):
+    _fields_ = [("src_len", C.c_uint64), ("dst_base_time", C.c_uint64), ("fid", C.c_uint64), ("wal_pos", C.c_uint64),
+                ("hint_pos", C.c_uint64), ("src_start_off", C.c_uint32), ("mode", C.c_uint32), ("ns_size", C.c_uint32),
+                ("etag_size", C.c_uint32)]
+
+
+class EncodeOut(C.Structure):
+    _fields_ = [("wal", u8p), ("wal_cap", C.c_uint64), ("hint", u8p), ("hint_cap", C.c_uint64), ("rec_off", u64p)]
+
+
+class EncodeResult(C.Structure):
+    _fields_ = [("n_in", C.c_uint64), ("n_written", C.c_uint64), ("wal_end", C.c_uint64), ("hint_end", C.c_uint64),
+                ("wal_need", C.c_uint64), ("hint_need", C.c_uint64), ("err_record", C.c_int64),
+                ("err_class", C.c_int32), ("src_err_class", C.c_int32), ("wal_events", C.c_uint32),
+                ("hint_events", C.c_uint32), ("fits", C.c_uint32), ("_pad", C.c_uint32)]
+
+
 # the table's column names, C types and numpy dtypes (one place, used by wal.py and bench.py)
 TABLE_COLUMNS = [("foff", "u8"), ("size", "u8"), ("expire", "u8"), ("aux0", "u8"), ("aux1", "u8"),
                  ("key_len", "u4"), ("val_len", "u4"), ("meta_len", "u4"), ("first_frag", "u4"),
@@ -58,6 +75,8 @@ ST_OK, ST_INVALID, ST_PANIC, ST_UNSUPPORTED = 0, 1, 2, 3
 ERR_NONE, ERR_CRC, ERR_TYPE, ERR_PANIC = 0, 1, 2, 3
 SB_OK, SB_SHORT, SB_CRC, SB_MAGIC, SB_BLOCKSIZE = 0, 1, 2, 3, 4
 E_CAPACITY = -4
+ENC_COMPACT, ENC_HINT = 0, 1
+ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC = 0, 1, 2, 3
 
 
 def _load():
@@ -87,6 +106,10 @@ def _load():
                                          C.POINTER(DecodeResult)]),
         "bcw_decode_fragments_async": (C.c_int, [vp, C.POINTER(FragTable)]),
         "bcw_decode_fragments": (C.c_int, [vp, C.POINTER(FragTable), u64p]),
+        "bcw_encode_segment_async": (C.c_int, [vp, vp, C.POINTER(EncodeParams), C.POINTER(RecordTable), vp, vp,
+                                               C.POINTER(EncodeOut), vp]),
+        "bcw_encode_segment": (C.c_int, [vp, vp, C.POINTER(EncodeParams), vp, C.c_uint64, C.POINTER(EncodeOut),
+                                         C.POINTER(EncodeResult)]),
         "bcw_synth_segment": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_int, C.c_uint64, vp, C.c_uint64, u64p, u64p]),
     }

@@ -69,6 +69,19 @@ void build_lane_tables(uint32_t* fwd, uint32_t* carry, uint32_t* half) {
     for (uint32_t n = 0; n < 16; ++n) half[i * 16 + n] = apply_basis(h64, n << (4 * i));
 }
 
+// k_pack shift operators: ops[m] = A_{8*128*m}, ops[16 + m] = A_{8*2048*m} (m < 16), nibble images
+static void build_enc_ops(uint32_t* ops) {
+  uint32_t t0[256];
+  byte_table(t0);
+  for (int h = 0; h < 2; ++h)
+    for (int m = 0; m < 16; ++m) {
+      uint32_t img[32];
+      shift_basis(t0, (uint64_t)(h ? 2048 : 128) * m, img);
+      for (int i = 0; i < 8; ++i)
+        for (uint32_t n = 0; n < 16; ++n) ops[((h * 16 + m) * 8 + i) * 16 + n] = apply_basis(img, n << (4 * i));
+    }
+}
+
 // initc[L] = A_{8L}(0xFFFFFFFF): the contribution of the CRC init value after L data bytes
 void build_initc(uint32_t* initc) {
   uint32_t t0[256];
@@ -107,6 +120,13 @@ struct bcw_ctx {
   hipStream_t cur = nullptr;
   Tables tabs{};
   Scratch s{};
+  EncScratch es{};
+  // sync encode staging
+  uint8_t* d_keep = nullptr;
+  uint64_t d_keep_cap = 0;
+  void* d_eout = nullptr;
+  uint64_t d_eout_cap = 0;
+  bcw_encode_result* d_eres = nullptr;
   uint64_t frag_hint = 0;  // capacity requested by a retry
   // sync-API staging
   uint8_t* d_seg = nullptr;
@@ -206,6 +226,8 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
   build_slice_tables(slice.data());
   build_lane_tables(fwd.data(), carry.data(), half.data());
   build_initc(initc.data());
+  std::vector<uint32_t> enc_ops(2 * 16 * 128);
+  build_enc_ops(enc_ops.data());
   std::vector<uint32_t> image(kLdsImage);
   for (int e = 0; e < 256; ++e)
     for (int r = 0; r < 32; ++r) {
@@ -223,13 +245,16 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
             hipMalloc(&c->tabs.half, half.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.initc, initc.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.lds_image, image.size() * 4) == hipSuccess &&
+            hipMalloc(&c->tabs.enc_ops, enc_ops.size() * 4) == hipSuccess &&
+            hipMalloc(&c->d_eres, sizeof(bcw_encode_result)) == hipSuccess &&
             hipMalloc(&c->d_result, sizeof(bcw_decode_result)) == hipSuccess;
   ok = ok && hipMemcpy(c->tabs.slice, slice.data(), slice.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.fwd, fwd.data(), fwd.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.carry, carry.data(), carry.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.half, half.data(), half.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.initc, initc.data(), initc.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemcpy(c->tabs.lds_image, image.data(), image.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+       hipMemcpy(c->tabs.lds_image, image.data(), image.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(c->tabs.enc_ops, enc_ops.data(), enc_ops.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
   if (!ok) { bcw_ctx_destroy(c); return BCW_E_NOMEM; }
   *out = c;
   return BCW_OK;
@@ -246,11 +271,22 @@ static void free_scratch(Scratch& s) {
   s = Scratch{};
 }
 
+static void free_enc_scratch(EncScratch& e) {
+  void* ptrs[] = {e.sz, e.mflag, e.dsrc, e.da, e.hda, e.hsz, e.dpos, e.tiles, e.ev, e.evb, e.desc_w, e.desc_h, e.emisc};
+  for (void* q : ptrs) (void)hipFree(q);
+  e = EncScratch{};
+}
+
 int bcw_ctx_destroy(bcw_ctx* c) {
   if (!c) return BCW_E_INVAL;
   (void)hipSetDevice(c->device);
   if (c->cur) (void)hipStreamSynchronize(c->cur);
   free_scratch(c->s);
+  free_enc_scratch(c->es);
+  (void)hipFree(c->tabs.enc_ops);
+  (void)hipFree(c->d_keep);
+  (void)hipFree(c->d_eout);
+  (void)hipFree(c->d_eres);
   (void)hipFree(c->tabs.slice);
   (void)hipFree(c->tabs.fwd);
   (void)hipFree(c->tabs.carry);
@@ -352,7 +388,8 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
   return launch_export_frags(c->s, *d_frags, c->last_start_off, c->cur, n) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_records"};
+static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_records", "k_enc_prep", "k_enc_scan", "k_events",
+                                          "k_pack", "k_pack_hint"};
 
 int bcw_ctx_set_profiling(bcw_ctx* c, int mask) {
   if (!c) return BCW_E_INVAL;
@@ -481,6 +518,162 @@ int bcw_decode_segment(bcw_ctx* c, const uint8_t* h_seg, const bcw_decode_params
   if (!ok) return BCW_E_HIP;
   HIPCHK(hipStreamSynchronize(c->cur));
   return h_result->n_records > h->capacity ? BCW_E_CAPACITY : BCW_OK;
+}
+
+
+// ---- encode (bcw_encode.hip) ----
+static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows, uint64_t blk_w, uint64_t blk_h) {
+  EncScratch& e = c->es;
+  if (rows <= e.rows_cap && blk_w <= e.blk_cap_w && blk_h <= e.blk_cap_h && e.emisc) return BCW_OK;
+  (void)hipStreamSynchronize(c->cur);
+  const uint64_t r = std::max(std::max(rows, e.rows_cap), (uint64_t)1);
+  const uint64_t bw = std::max(std::max(blk_w, e.blk_cap_w), (uint64_t)4);
+  const uint64_t bh = std::max(std::max(blk_h, e.blk_cap_h), (uint64_t)4);
+  free_enc_scratch(e);
+  const uint64_t ntiles = r / enc_tile_items() + 2;
+  const uint64_t nwin = r / enc_ev_win() + 2;
+  bool ok = hipMalloc(&e.sz, r * 4) == hipSuccess && hipMalloc(&e.mflag, r) == hipSuccess &&
+            hipMalloc(&e.dsrc, r * 4) == hipSuccess && hipMalloc(&e.da, (r + 1) * 8) == hipSuccess &&
+            hipMalloc(&e.hda, (r + 1) * 8) == hipSuccess && hipMalloc(&e.hsz, r * 4) == hipSuccess &&
+            hipMalloc(&e.dpos, r * 8) == hipSuccess && hipMalloc(&e.tiles, ntiles * enc_sizeof_tile()) == hipSuccess &&
+            hipMalloc(&e.ev, (r + 2) * enc_sizeof_ev()) == hipSuccess && hipMalloc(&e.evb, nwin * 4) == hipSuccess &&
+            hipMalloc(&e.desc_w, bw * enc_sizeof_desc()) == hipSuccess &&
+            hipMalloc(&e.desc_h, bh * enc_sizeof_desc()) == hipSuccess &&
+            hipMalloc(&e.emisc, 64 * sizeof(uint64_t)) == hipSuccess;
+  if (!ok) { free_enc_scratch(e); return BCW_E_NOMEM; }
+  (void)hipMemset(e.mflag, 0, r);
+  e.rows_cap = r;
+  e.blk_cap_w = bw;
+  e.blk_cap_h = bh;
+  return BCW_OK;
+}
+
+// blocks an append of at most `cap` bytes at file offset `pos` can touch
+static uint64_t blocks_for(uint64_t pos, uint64_t cap) {
+  if (pos < BCW_SUPER_BLOCK_SIZE) return 0;
+  const uint64_t q0 = pos - BCW_SUPER_BLOCK_SIZE;
+  return (q0 + cap) / BCW_BLOCK_SIZE - q0 / BCW_BLOCK_SIZE + 2;
+}
+
+int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_params* p,
+                             const bcw_record_table* t, const bcw_decode_result* d_src_result, const uint8_t* d_keep,
+                             const bcw_encode_out* o, bcw_encode_result* d_result) {
+  if (!c || !p || !t || !d_src_result || !o || !d_result) return BCW_E_INVAL;
+  if (p->mode != BCW_ENC_COMPACT && p->mode != BCW_ENC_HINT) return BCW_E_INVAL;
+  if (p->hint_pos < BCW_SUPER_BLOCK_SIZE || !o->hint) return BCW_E_INVAL;
+  if (p->mode == BCW_ENC_COMPACT && (p->wal_pos < BCW_SUPER_BLOCK_SIZE || !o->wal || !d_keep)) return BCW_E_INVAL;
+  if (!t->foff || !t->size || !t->expire || !t->key_len || !t->val_len || !t->meta_len || !t->first_frag ||
+      !t->emit_frag || !t->hdr_size || !t->flags || !t->etag_off || !t->status)
+    return BCW_E_INVAL;
+  if (!c->s.frags) return BCW_E_INVAL;  // no decode on this context yet
+  if (t->capacity >= 0xffffff00ull) return BCW_E_INVAL;  // u32 dense record ids
+  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  const uint64_t bw = p->mode == BCW_ENC_COMPACT ? blocks_for(p->wal_pos, o->wal_cap) : 0;
+  const uint64_t bh = blocks_for(p->hint_pos, o->hint_cap);
+  int rc = ensure_enc_scratch(c, t->capacity, bw, bh);
+  if (rc != BCW_OK) return rc;
+  EncLaunch L{};
+  L.d_src = d_src;
+  L.p = *p;
+  L.table = *t;
+  L.rows = t->capacity;
+  L.d_src_result = d_src_result;
+  L.d_keep = d_keep;
+  L.out = *o;
+  L.d_result = d_result;
+  L.frags = c->s.frags;
+  L.crc_ops = c->tabs.enc_ops;
+  L.initc = c->tabs.initc;
+  return launch_encode(L, c->es, c->cur, &c->prof) == hipSuccess ? BCW_OK : BCW_E_HIP;
+}
+
+int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params* p, const uint8_t* h_keep,
+                       uint64_t n_keep, const bcw_encode_out* h, bcw_encode_result* h_result) {
+  if (!c || !p || !h || !h_result) return BCW_E_INVAL;
+  if (p->src_len && !h_src) return BCW_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  // decode the source (record mode) into the context's table
+  bcw_super_block sb{};
+  bcw_decode_params dp{};
+  dp.seg_len = p->src_len;
+  dp.start_off = p->src_start_off;
+  dp.ns_size = p->ns_size;
+  dp.etag_size = p->etag_size;
+  dp.mode = BCW_MODE_RECORD;
+  dp.base_time = (bcw_load_super_block(h_src, p->src_len, &sb) == BCW_SB_OK) ? sb.base_time : 0;
+  uint64_t cap = std::max<uint64_t>(16, p->src_len / 64 + 16);
+  int rc;
+  bcw_decode_result dres{};
+  for (;;) {
+    std::vector<uint8_t> dummy;  // host table not needed: decode into the device table only
+    rc = ensure_dev_table(c, cap, false);
+    if (rc != BCW_OK) return rc;
+    if (p->src_len > c->d_seg_cap) {
+      (void)hipStreamSynchronize(c->cur);
+      (void)hipFree(c->d_seg);
+      c->d_seg = nullptr;
+      c->d_seg_cap = 0;
+      if (hipMalloc(&c->d_seg, p->src_len) != hipSuccess) return BCW_E_NOMEM;
+      c->d_seg_cap = p->src_len;
+    }
+    if (p->src_len) HIPCHK(hipMemcpyAsync(c->d_seg, h_src, p->src_len, hipMemcpyHostToDevice, c->cur));
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      rc = bcw_decode_segment_async(c, c->d_seg, &dp, &c->d_tab, c->d_result);
+      if (rc != BCW_OK) return rc;
+      HIPCHK(hipMemcpyAsync(&dres, c->d_result, sizeof dres, hipMemcpyDeviceToHost, c->cur));
+      HIPCHK(hipStreamSynchronize(c->cur));
+      if (!dres.retry_frag_capacity) break;
+      c->frag_hint = dres.retry_frag_capacity + 64;
+    }
+    if (dres.retry_frag_capacity) return BCW_E_NOMEM;
+    if (dres.n_records <= c->d_tab.capacity) break;
+    cap = dres.n_records + 16;
+  }
+  const uint64_t rows = c->d_tab.capacity;
+  // keep mask (missing entries: dropped)
+  if (rows > c->d_keep_cap) {
+    (void)hipFree(c->d_keep);
+    c->d_keep = nullptr;
+    c->d_keep_cap = 0;
+    if (hipMalloc(&c->d_keep, rows) != hipSuccess) return BCW_E_NOMEM;
+    c->d_keep_cap = rows;
+  }
+  HIPCHK(hipMemsetAsync(c->d_keep, 0, rows, c->cur));
+  const uint64_t nk = std::min(n_keep, rows);
+  if (h_keep && nk) HIPCHK(hipMemcpyAsync(c->d_keep, h_keep, nk, hipMemcpyHostToDevice, c->cur));
+  // device outputs
+  const uint64_t need = h->wal_cap + h->hint_cap + rows * 8;
+  if (need > c->d_eout_cap) {
+    (void)hipStreamSynchronize(c->cur);
+    (void)hipFree(c->d_eout);
+    c->d_eout = nullptr;
+    c->d_eout_cap = 0;
+    if (hipMalloc(&c->d_eout, need + 64) != hipSuccess) return BCW_E_NOMEM;
+    c->d_eout_cap = need;
+  }
+  uint8_t* m = (uint8_t*)c->d_eout;
+  bcw_encode_out d{};
+  d.rec_off = (uint64_t*)m;
+  m += rows * 8;
+  d.wal = m;
+  d.wal_cap = h->wal_cap;
+  m += (h->wal_cap + 15) & ~15ull;
+  d.hint = (uint8_t*)(((uintptr_t)m + 15) & ~(uintptr_t)15);
+  d.hint_cap = h->hint_cap;
+  if (p->mode == BCW_ENC_HINT && !d.wal) d.wal = d.hint;
+  rc = bcw_encode_segment_async(c, c->d_seg, p, &c->d_tab, c->d_result, c->d_keep, &d, c->d_eres);
+  if (rc != BCW_OK) return rc;
+  HIPCHK(hipMemcpyAsync(h_result, c->d_eres, sizeof *h_result, hipMemcpyDeviceToHost, c->cur));
+  HIPCHK(hipStreamSynchronize(c->cur));
+  if (!h_result->fits) return BCW_E_CAPACITY;
+  if (h->wal && h_result->wal_need && p->mode == BCW_ENC_COMPACT)
+    HIPCHK(hipMemcpyAsync(h->wal, d.wal, h_result->wal_need, hipMemcpyDeviceToHost, c->cur));
+  if (h->hint && h_result->hint_need)
+    HIPCHK(hipMemcpyAsync(h->hint, d.hint, h_result->hint_need, hipMemcpyDeviceToHost, c->cur));
+  const uint64_t nr = std::min(dres.n_records, rows);
+  if (h->rec_off && nr) HIPCHK(hipMemcpyAsync(h->rec_off, d.rec_off, nr * 8, hipMemcpyDeviceToHost, c->cur));
+  HIPCHK(hipStreamSynchronize(c->cur));
+  return BCW_OK;
 }
 
 // ---- host WAL writer: Record.Encode (record.go:57-138) at synthetic shapes + WriteRecord ----

@@ -46,6 +46,7 @@ struct Tables {
   uint32_t* half;    // [8][16] A_{8*64} (nibble images)
   uint32_t* initc;   // [kBlock+1] A_{8L}(0xFFFFFFFF)
   uint32_t* lds_image;  // k_crc's LDS table image, laid out exactly as in LDS (see kLdsImage)
+  uint32_t* enc_ops;    // [2][16][8][16] A_{8*128*m}, A_{8*2048*m} (m < 16) nibble images (k_pack)
 };
 
 // k_crc LDS table image (dwords): slice-by-2 tables as 256-B rows {T1[e] x32, T0[e] x32} (lane l
@@ -76,7 +77,8 @@ struct Scratch {
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
 // stream around every kernel of the pipeline.
-enum KernelId { K_CHASE = 0, K_CRC, K_RECORDS, K_NUM };
+enum KernelId { K_CHASE = 0, K_CRC, K_RECORDS, K_ENC_PREP, K_ENC_SCAN, K_ENC_EVENTS, K_ENC_PACK, K_ENC_PACK_HINT,
+                K_NUM };
 struct Prof {
   uint32_t mask = 0;  // bit k: time kernel id k
   struct Mark { int kid; hipEvent_t a, b; };
@@ -104,6 +106,45 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
                          hipStream_t stream, int num_cus, Prof* prof);
 hipError_t launch_export_frags(const Scratch& s, const bcw_frag_table& out, uint32_t start_off, hipStream_t stream,
                                uint64_t n);
+
+// Encode scratch (grow-only, per context). rows: source table rows; blk_cap_*: output blocks.
+struct EncScratch {
+  uint64_t rows_cap = 0, blk_cap_w = 0, blk_cap_h = 0;
+  uint32_t* sz = nullptr;     // [rows] payload size per source row (0: not written)
+  uint8_t* mflag = nullptr;   // [rows] meta dropped by Record.Encode
+  uint32_t* dsrc = nullptr;   // [rows] dense record -> source row
+  uint64_t* da = nullptr;     // [rows+1] dst WAL y-coordinates
+  uint64_t* hda = nullptr;    // [rows+1] hint WAL y-coordinates
+  uint32_t* hsz = nullptr;    // [rows] hint payload sizes (compaction)
+  uint64_t* dpos = nullptr;   // [rows] dst record offsets
+  void* tiles = nullptr;      // scan tile sums
+  void* ev = nullptr;         // [rows+2] layout events
+  uint32_t* evb = nullptr;    // [rows/win+2] governing event per k_events window
+  void* desc_w = nullptr;     // [blk_cap_w] block descriptors (dst WAL)
+  void* desc_h = nullptr;     // [blk_cap_h] (hint WAL)
+  uint64_t* emisc = nullptr;  // [64] counters
+};
+
+struct EncLaunch {
+  const uint8_t* d_src;
+  bcw_encode_params p;
+  bcw_record_table table;
+  uint64_t rows;
+  const bcw_decode_result* d_src_result;
+  const uint8_t* d_keep;
+  bcw_encode_out out;
+  bcw_encode_result* d_result;
+  const Frag* frags;
+  const uint32_t* crc_ops;
+  const uint32_t* initc;
+};
+
+hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t stream, Prof* prof);
+size_t enc_sizeof_ev();
+size_t enc_sizeof_desc();
+size_t enc_sizeof_tile();
+int enc_tile_items();
+int enc_ev_win();
 
 // Host-side table builders (bcw_api.cpp).
 void build_slice_tables(uint32_t* t2x256);

@@ -5,6 +5,8 @@ Names, argument meaning and error behaviour follow wenzhang-dev/bitcaskDB:
   iterate_record      IterateRecord                       record.go:242-266
   iterate_hint        IterateHint                         hint.go:163-188
   compute_crc32       ComputeCRC32                        utils.go:24-29
+  compact_one_wal     compactOneWal                       compaction.go:294-327
+  new_hint_by_wal     NewHintByWal                        hint.go:123-161
 Every record comes out of the GPU decode (libbcw.so); the callback replay below reproduces the
 reference's sequential error semantics (records before the first failure are delivered, then
 the first error is returned/raised).
@@ -133,6 +135,37 @@ class Context:
         if with_frags:
             out.frags = self.fragments(max(int(res.n_frags), 1))
         return out
+
+    # synchronous host-in/host-out encode (decode of src + re-encode / hint rebuild on the device)
+    def encode(self, src, mode: int, src_start_off: int, dst_base_time: int, fid: int, wal_pos: int, hint_pos: int,
+               ns_size: int, etag_size: int, keep=None, wal_cap: int | None = None, hint_cap: int | None = None):
+        """Returns (EncodeResult, appended dst WAL bytes, appended hint WAL bytes, rec_off per source row)."""
+        src = np.frombuffer(src, dtype=np.uint8) if not isinstance(src, np.ndarray) else src
+        src = np.ascontiguousarray(src, dtype=np.uint8)
+        n = int(src.size)
+        p = L.EncodeParams(n, dst_base_time, fid, wal_pos, hint_pos, src_start_off, mode, ns_size, etag_size)
+        keep = np.ascontiguousarray(keep if keep is not None else np.zeros(0), dtype=np.uint8)
+        wcap = wal_cap if wal_cap is not None else (n + n // 8 + 4096 if mode == L.ENC_COMPACT else 0)
+        hcap = hint_cap if hint_cap is not None else n // 16 + 4096
+        nrows = max(16, n // 12 + 16)
+        while True:
+            wal = np.zeros(max(wcap, 1), dtype=np.uint8)
+            hint = np.zeros(max(hcap, 1), dtype=np.uint8)
+            offs = np.full(nrows, np.iinfo(np.uint64).max, dtype=np.uint64)
+            out = L.EncodeOut(wal.ctypes.data_as(L.u8p), wcap, hint.ctypes.data_as(L.u8p), hcap,
+                              offs.ctypes.data_as(L.u64p))
+            res = L.EncodeResult()
+            rc = L.lib.bcw_encode_segment(self._h, src.ctypes.data_as(C.c_void_p) if n else None, C.byref(p),
+                                          keep.ctypes.data_as(C.c_void_p) if keep.size else None, keep.size,
+                                          C.byref(out), C.byref(res))
+            if rc == L.E_CAPACITY:
+                wcap = max(wcap, int(res.wal_need))
+                hcap = max(hcap, int(res.hint_need))
+                continue
+            if rc != 0:
+                raise RuntimeError(f"bcw_encode_segment: {L.lib.bcw_strerror(rc).decode()}")
+            break
+        return res, bytes(wal[:int(res.wal_need)]), bytes(hint[:int(res.hint_need)]), offs[:int(res.n_in)].copy()
 
     def fragments(self, capacity: int):
         cols = {name: np.zeros(max(capacity, 1), dtype=dt) for name, dt in L.FRAG_COLUMNS}
@@ -323,3 +356,91 @@ def iterate_hint(hint: Wal, cb, ns_size: int = 20, ctx: Context | None = None):
     err = _frag_error(dec.result)
     if err is not None:
         raise err
+
+
+# ---- write side: compaction re-encode and hint rebuild ----
+class WalFile:
+    """In-memory WAL file being written (NewWal + WriteRecord appends, wal.go:262-360, 490-553)."""
+
+    def __init__(self, fid: int, base_time: int, create_time: int | None = None):
+        sb = (C.c_uint8 * 40)()
+        L.lib.bcw_write_super_block(sb, create_time if create_time is not None else base_time, base_time)
+        self.data = bytearray(bytes(sb))
+        self.fid = fid
+        self.base_time = base_time
+
+    def size(self) -> int:
+        return len(self.data)
+
+    def BaseTime(self) -> int:  # noqa: N802
+        return self.base_time
+
+    def Fid(self) -> int:  # noqa: N802
+        return self.fid
+
+    def as_wal(self) -> Wal:
+        return load_wal(bytes(self.data), self.fid)
+
+
+_ENC_ERRORS = {L.ENC_ERR_EXPIRE: lambda: WalError("invalid expire"),
+               L.ENC_ERR_PANIC: lambda: RefPanic("index out of range (PutUvarint into [MaxVarintLen32]byte)")}
+
+
+def _src_error(res, dec_class, status):
+    if status == L.ST_INVALID:
+        return ErrInvalidData()
+    if status == L.ST_PANIC:
+        return RefPanic("slice bounds out of range")
+    if status == L.ST_UNSUPPORTED:
+        return WalError("record length >= 2^32 is not supported by the device table")
+    return _frag_error(type("R", (), {"err_class": dec_class})())
+
+
+def compact_one_wal(dst: WalFile, hint: WalFile, src: Wal, keep, ns_size: int = 20, etag_size: int = 20,
+                    ctx: Context | None = None):
+    """compactOneWal (compaction.go:294-327): every delivered source record with keep[i] (the doFilter
+    verdict, compaction.go:303) is re-encoded against dst's baseTime and appended to dst, its hint to
+    `hint`. Returns the dst offsets per source row (2**64-1: not written). Raises the reference's error
+    after appending what the reference appends before it."""
+    ctx = ctx or default_context()
+    if callable(keep):  # doFilter(record, fid, off) -> True drops the record (compaction.go:329-348)
+        rows = []
+        try:
+            iterate_record(src, lambda r, foff, size: rows.append(not keep(r, src.fid, foff - HEADER)),
+                           ns_size, etag_size, ctx)
+        except WalError:
+            pass  # raised again below, after the records before it are appended
+        keep = np.array(rows, dtype=np.uint8)
+    res, wal, hb, offs = ctx.encode(src.data, L.ENC_COMPACT, src.start_off, dst.base_time, dst.fid, dst.size(),
+                                    hint.size(), ns_size, etag_size, keep)
+    dst.data += wal
+    hint.data += hb
+    if res.err_class == L.ENC_ERR_SRC:
+        st = L.ST_OK
+        if res.err_record >= 0:
+            dec = ctx.decode(src.data, src.start_off, src.base_time, ns_size, etag_size)
+            st = int(dec.table["status"][res.err_record])
+        raise _src_error(res, res.src_err_class, st)
+    if res.err_class in _ENC_ERRORS:
+        raise _ENC_ERRORS[res.err_class]()
+    return offs
+
+
+def new_hint_by_wal(wal: Wal, ns_size: int = 20, etag_size: int = 20, ctx: Context | None = None,
+                    create_time: int | None = None) -> WalFile:
+    """NewHintByWal (hint.go:123-161): the hint WAL (same fid and baseTime) of a data WAL."""
+    ctx = ctx or default_context()
+    h = WalFile(wal.fid, wal.base_time, create_time)
+    res, _, hb, _ = ctx.encode(wal.data, L.ENC_HINT, wal.start_off, wal.base_time, wal.fid, 40, h.size(), ns_size,
+                               etag_size)
+    h.data += hb
+    if res.err_class == L.ENC_ERR_SRC:
+        st = L.ST_OK
+        if res.err_record >= 0:
+            dec = ctx.decode(wal.data, wal.start_off, wal.base_time, ns_size, etag_size)
+            st = int(dec.table["status"][res.err_record])
+        raise _src_error(res, res.src_err_class, st)
+    return h
+
+
+HEADER = L.HEADER_SIZE

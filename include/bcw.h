@@ -12,6 +12,12 @@
  *   bcw_crc32c_masked    replaces  ComputeCRC32                utils.go:24-29
  *   bcw_load_super_block replaces  Wal.loadSuperBlock          wal.go:362-398
  *   bcw_write_super_block          Wal.writeSuperBlock         wal.go:332-360
+ *   bcw_encode_segment*  replaces  the compactOneWal loop      compaction.go:294-327
+ *     (BCW_ENC_COMPACT)            = Record.Encode              record.go:57-138
+ *                                  + WalRewriter.AppendRecord   wal_rewriter.go:39-51 -> Wal.WriteRecord wal.go:490-553
+ *                                  + HintWriter.AppendRecord    hint.go:109-117 -> HintRecord.Encode hint.go:32-48
+ *     (BCW_ENC_HINT)     replaces  NewHintByWal                 hint.go:123-161
+ *                        callers   compaction.go:203-211 (via compactOneWal), db_impl.go:545
  *   bcw_synth_segment    host WAL writer: Wal.WriteRecord wal.go:490-553 over Record.Encode
  *                                  record.go:57-138 (synthetic segments of the benchmark configs)
  *
@@ -205,6 +211,70 @@ int bcw_decode_fragments(bcw_ctx* ctx, const bcw_frag_table* h_frags, uint64_t* 
 int bcw_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_t seed, uint32_t ns_size,
                       uint32_t key_len, uint32_t value_len, int value_mode, uint64_t base_time,
                       uint8_t* h_out, uint64_t out_cap, uint64_t* out_len, uint64_t* out_records);
+
+/* ---- encode: compaction re-encode (compactOneWal) and hint rebuild (NewHintByWal) ---- */
+#define BCW_ENC_COMPACT 0 /* kept records re-encoded into the dst WAL + one hint each (compaction.go:294-327) */
+#define BCW_ENC_HINT 1    /* a hint per delivered record of a data WAL (hint.go:123-161) */
+
+#define BCW_ENC_ERR_NONE 0
+#define BCW_ENC_ERR_SRC 1    /* IterateRecord failed: a bad row (err_record) or a fragment error (err_record -1,
+                                src_err_class); everything before it was written, as in the reference */
+#define BCW_ENC_ERR_EXPIRE 2 /* Record.Encode: errors.New("invalid expire") (record.go:74) at err_record */
+#define BCW_ENC_ERR_PANIC 3  /* Record.Encode panics at err_record: expire delta >= 2^35 overflows
+                                `var expireBytes [binary.MaxVarintLen32]byte` (record.go:67,78) */
+
+typedef struct bcw_encode_params {
+  uint64_t src_len;       /* source WAL file size */
+  uint64_t dst_base_time; /* Record.Encode baseTime: dst.Wal().BaseTime() (compaction.go:308) */
+  uint64_t fid;           /* hint fid: the dst fid (compaction.go:318) or the data WAL's fid (hint.go:142) */
+  uint64_t wal_pos;       /* dst WAL file size before the append (Wal.writeOffset(false), wal.go:482-487), >= 40 */
+  uint64_t hint_pos;      /* hint WAL file size before the append, >= 40 */
+  uint32_t src_start_off; /* source super block startOff */
+  uint32_t mode;          /* BCW_ENC_COMPACT or BCW_ENC_HINT */
+  uint32_t ns_size;       /* gOpts.NsSize */
+  uint32_t etag_size;     /* gOpts.EtagSize */
+} bcw_encode_params;
+
+/* Outputs. wal / hint receive the bytes appended to each file: out[0] is file offset wal_pos /
+ * hint_pos (the super block of a new file is bcw_write_super_block's job). rec_off (one per
+ * source table row, may be NULL): the offset WriteRecord returned for the row's record in the
+ * dst WAL, UINT64_MAX when not written. Device pointers for the async API, host for the sync one. */
+typedef struct bcw_encode_out {
+  uint8_t* wal;
+  uint64_t wal_cap;
+  uint8_t* hint;
+  uint64_t hint_cap;
+  uint64_t* rec_off;
+} bcw_encode_out;
+
+typedef struct bcw_encode_result {
+  uint64_t n_in;         /* source records delivered by the iteration (before any error) */
+  uint64_t n_written;    /* records appended (dst WAL and hint WAL) */
+  uint64_t wal_end;      /* dst WAL file size after the append */
+  uint64_t hint_end;     /* hint WAL file size after the append */
+  uint64_t wal_need;     /* bytes appended = wal_end - wal_pos */
+  uint64_t hint_need;
+  int64_t err_record;    /* source row of the error, -1 if none / a fragment error */
+  int32_t err_class;     /* BCW_ENC_ERR_* */
+  int32_t src_err_class; /* the decode's BCW_ERR_* */
+  uint32_t wal_events;   /* layout events (blocks starting exactly at a record header) */
+  uint32_t hint_events;
+  uint32_t fits;         /* 0: an output capacity was too small, nothing was written */
+  uint32_t _pad;
+} bcw_encode_result;
+
+/* Async, device-resident. d_src / d_table / d_src_result must be the inputs and outputs of the most
+ * recent bcw_decode_segment_async (BCW_MODE_RECORD) on this context: the encode reads the context's
+ * fragment table. d_keep[i] != 0 keeps source row i (the doFilter verdict, compaction.go:303;
+ * ignored for BCW_ENC_HINT). Launches on the context stream; d_result (device) receives the outcome. */
+int bcw_encode_segment_async(bcw_ctx* ctx, const uint8_t* d_src, const bcw_encode_params* p,
+                             const bcw_record_table* d_table, const bcw_decode_result* d_src_result,
+                             const uint8_t* d_keep, const bcw_encode_out* d_out, bcw_encode_result* d_result);
+/* Synchronous, host in / host out: decodes h_src, then encodes (n_keep entries of h_keep, missing
+ * ones count as dropped). Returns BCW_E_CAPACITY (result filled, nothing copied) when an output is
+ * too small: h_result->wal_need / hint_need tell the sizes. */
+int bcw_encode_segment(bcw_ctx* ctx, const uint8_t* h_src, const bcw_encode_params* p, const uint8_t* h_keep,
+                       uint64_t n_keep, const bcw_encode_out* h_out, bcw_encode_result* h_result);
 
 #ifdef __cplusplus
 }

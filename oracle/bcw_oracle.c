@@ -257,6 +257,9 @@ int64_t oc_record_encode(uint8_t* out, const uint8_t* ns, size_t ns_len, const u
   int expire_size = 0;
   if (expire == 0) flag |= 1u << 1;
   else if (expire < base_time) return -1; /* "invalid expire" */
+  /* binary.PutUvarint into `var expireBytes [binary.MaxVarintLen32]byte` (record.go:67,78): a delta that
+   * needs more than 5 varint bytes (>= 2^35) indexes past the array and panics */
+  else if (expire - base_time >= (1ull << 35)) return -2;
   else expire_size = oc_put_uvarint(expb, expire - base_time);
   uint8_t tmp[30];
   int t = 0;
@@ -568,18 +571,39 @@ uint64_t oc_decode_fast(const uint8_t* seg, uint64_t len, uint32_t start_off, ui
 /* ------------------------------------------------------------------------------------------ */
 /* compaction (compaction.go:294-327) and hint rebuild (hint.go:123-161)                        */
 /* ------------------------------------------------------------------------------------------ */
-int64_t oc_compact_append(oc_writer* dst, oc_writer* hint, uint64_t dst_fid, const uint8_t* seg,
-                          uint64_t len, uint32_t start_off, uint64_t src_base, uint64_t dst_base,
-                          uint32_t ns_size, uint32_t etag_size, const uint8_t* keep, uint64_t n_keep,
-                          uint64_t* offs) {
+/* Record.Meta.AppMetaSize == 0 after msgpack.Unmarshal(meta, &map[string]string) (record.go:213-220,
+ * meta.go:38-49): Record.Encode then writes no meta (record.go:82). Recognised for the canonical msgpack
+ * forms of an empty map: nil (0xc0), {} (0x80) and fixmaps whose keys and values are all empty
+ * strings (0xa0) or nil. Any other meta is copied verbatim (msgpack re-encoding parity unpinned). */
+int oc_meta_app_size_zero(const uint8_t* m, size_t n) {
+  if (n == 1) return m[0] == 0xc0 || m[0] == 0x80;
+  if (n < 3 || (m[0] & 0xf0) != 0x80) return 0;
+  size_t e = m[0] & 0x0f;
+  if (n != 1 + 2 * e) return 0;
+  for (size_t i = 1; i < n; ++i)
+    if (m[i] != 0xa0 && m[i] != 0xc0) return 0;
+  return 1;
+}
+
+/* compactOneWal (compaction.go:294-327) over one source WAL: IterateRecord delivers records until the
+ * first bad row or fragment error; every kept record is re-encoded (Record.Encode against the dst
+ * baseTime) and appended to dst (WriteRecord), then its hint (ns, key, dst fid, dst offset, payload
+ * size) is appended to `hint`. The callback's first error stops the iteration. */
+void oc_compact_append(oc_writer* dst, oc_writer* hint, uint64_t dst_fid, const uint8_t* seg, uint64_t len,
+                       uint32_t start_off, uint64_t src_base, uint64_t dst_base, uint32_t ns_size,
+                       uint32_t etag_size, const uint8_t* keep, uint64_t n_keep, uint64_t* offs,
+                       int32_t* err_class, int64_t* err_rec, uint64_t* n_in) {
   oc_decode* d = oc_decode_segment(seg, len, start_off, src_base, ns_size, etag_size, 0);
   uint8_t* buf = NULL;
   size_t buf_cap = 0;
-  int64_t rc = 0;
-  for (uint64_t i = 0; i < d->n_recs; ++i) {
+  *err_class = OC_ENC_OK;
+  *err_rec = -1;
+  uint64_t i = 0;
+  for (; i < d->n_recs; ++i) {
     const oc_rec* r = &d->recs[i];
-    if (r->status != OC_ST_OK) { rc = -2 - (int64_t)i; break; } /* IterateRecord returns the error */
-    if (i >= n_keep || !keep[i]) { if (offs) offs[i] = UINT64_MAX; continue; } /* doFilter dropped it */
+    if (r->status != OC_ST_OK) { *err_class = OC_ENC_SRC; *err_rec = (int64_t)i; break; } /* RecordFromBytes error */
+    if (offs) offs[i] = UINT64_MAX;
+    if (i >= n_keep || !keep[i]) continue; /* doFilter dropped it */
     const uint8_t* p = d->bytes + d->byte_offs[i];
     const uint8_t* ns = p + 1;
     size_t etag_len = (r->flags & 1u) ? 0 : etag_size;
@@ -587,35 +611,38 @@ int64_t oc_compact_append(oc_writer* dst, oc_writer* hint, uint64_t dst_fid, con
     const uint8_t* key = p + r->hdr_size;
     const uint8_t* val = key + r->key_len;
     const uint8_t* meta = val + r->val_len;
-    size_t need = 64 + ns_size + etag_len + r->key_len + r->val_len + r->meta_len;
+    size_t meta_len = oc_meta_app_size_zero(meta, r->meta_len) ? 0 : r->meta_len;
+    size_t need = 64 + ns_size + etag_len + r->key_len + r->val_len + meta_len;
     if (need > buf_cap) { buf_cap = need * 2; buf = (uint8_t*)realloc(buf, buf_cap); }
     int64_t n = oc_record_encode(buf, ns, ns_size, key, r->key_len, val, r->val_len, etag, etag_len, r->expire,
-                                 (r->flags >> 2) & 1u, meta, r->meta_len, dst_base);
-    if (n < 0) { rc = -1 - (int64_t)i; break; }
+                                 (r->flags >> 2) & 1u, meta, meta_len, dst_base);
+    if (n < 0) { *err_class = n == -1 ? OC_ENC_EXPIRE : OC_ENC_PANIC; *err_rec = (int64_t)i; break; }
     uint64_t o = oc_writer_write(dst, buf, (size_t)n);
     if (offs) offs[i] = o;
-    uint8_t hb[64 + 255 + 30];
-    uint8_t* hp = hb;
     size_t hneed = ns_size + r->key_len + 40;
-    uint8_t* heap = NULL;
-    if (hneed > sizeof hb) { heap = (uint8_t*)malloc(hneed); hp = heap; }
+    uint8_t* hp = (uint8_t*)malloc(hneed);
     size_t hn = oc_hint_encode(hp, ns, ns_size, key, r->key_len, dst_fid, o, (uint64_t)n);
     oc_writer_write(hint, hp, hn);
-    free(heap);
+    free(hp);
   }
-  if (d->err_class != OC_ERR_NONE && rc == 0) rc = -(int64_t)(1ull << 62); /* iterator error */
+  if (*err_class == OC_ENC_OK && d->err_class != OC_ERR_NONE) *err_class = OC_ENC_SRC; /* iterator error */
+  *n_in = i;
   free(buf);
   oc_decode_free(d);
-  return rc;
 }
 
-int64_t oc_hint_by_wal(oc_writer* hint, uint64_t fid, const uint8_t* seg, uint64_t len, uint32_t start_off,
-                       uint64_t base_time, uint32_t ns_size, uint32_t etag_size) {
+/* NewHintByWal (hint.go:123-161): one hint per delivered record, off = foff - 7 (the iterator offset,
+ * so a zero-length First shifts it), size = len(payload). */
+void oc_hint_by_wal(oc_writer* hint, uint64_t fid, const uint8_t* seg, uint64_t len, uint32_t start_off,
+                    uint64_t base_time, uint32_t ns_size, uint32_t etag_size, int32_t* err_class, int64_t* err_rec,
+                    uint64_t* n_in) {
   oc_decode* d = oc_decode_segment(seg, len, start_off, base_time, ns_size, etag_size, 0);
-  int64_t rc = 0;
-  for (uint64_t i = 0; i < d->n_recs; ++i) {
+  *err_class = OC_ENC_OK;
+  *err_rec = -1;
+  uint64_t i = 0;
+  for (; i < d->n_recs; ++i) {
     const oc_rec* r = &d->recs[i];
-    if (r->status != OC_ST_OK) { rc = -1 - (int64_t)i; break; }
+    if (r->status != OC_ST_OK) { *err_class = OC_ENC_SRC; *err_rec = (int64_t)i; break; }
     const uint8_t* p = d->bytes + d->byte_offs[i];
     size_t hneed = ns_size + r->key_len + 40;
     uint8_t* hb = (uint8_t*)malloc(hneed);
@@ -623,9 +650,9 @@ int64_t oc_hint_by_wal(oc_writer* hint, uint64_t fid, const uint8_t* seg, uint64
     oc_writer_write(hint, hb, hn);
     free(hb);
   }
-  if (d->err_class != OC_ERR_NONE && rc == 0) rc = -(int64_t)(1ull << 62);
+  if (*err_class == OC_ENC_OK && d->err_class != OC_ERR_NONE) *err_class = OC_ENC_SRC;
+  *n_in = i;
   oc_decode_free(d);
-  return rc;
 }
 
 /* ------------------------------------------------------------------------------------------ */

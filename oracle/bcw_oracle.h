@@ -103,7 +103,8 @@ const uint8_t* oc_writer_data(const oc_writer* w);
 void oc_writer_free(oc_writer* w);
 
 /* ---- record / hint payload codecs ---- */
-/* Record.Encode (record.go:57-138); returns payload length, or -1 on "invalid expire". */
+/* Record.Encode (record.go:57-138); returns payload length, -1 on "invalid expire", -2 where the reference
+ * panics (expire delta needs > 5 varint bytes). */
 int64_t oc_record_encode(uint8_t* out, const uint8_t* ns, size_t ns_len, const uint8_t* key, size_t key_len,
                          const uint8_t* val, size_t val_len, const uint8_t* etag, size_t etag_len,
                          uint64_t expire, int tombstone, const uint8_t* meta, size_t meta_len,
@@ -136,14 +137,19 @@ uint64_t oc_decode_fast(const uint8_t* seg, uint64_t len, uint32_t start_off, ui
                         uint32_t ns_size, uint32_t etag_size, int32_t* err_class, uint64_t* checksum);
 
 /* ---- compaction re-encode (compactOneWal) and hint rebuild (NewHintByWal) ----
- * Appends every delivered source record with keep[i] != 0 to dst/hint writers.
- * Returns 0, or -1 - i if record i fails Record.Encode ("invalid expire"). offs[i] = dst offset. */
-int64_t oc_compact_append(oc_writer* dst, oc_writer* hint, uint64_t dst_fid, const uint8_t* seg,
-                          uint64_t len, uint32_t start_off, uint64_t src_base, uint64_t dst_base,
-                          uint32_t ns_size, uint32_t etag_size, const uint8_t* keep, uint64_t n_keep,
-                          uint64_t* offs);
-int64_t oc_hint_by_wal(oc_writer* hint, uint64_t fid, const uint8_t* seg, uint64_t len, uint32_t start_off,
-                       uint64_t base_time, uint32_t ns_size, uint32_t etag_size);
+ * err_class: OC_ENC_OK, OC_ENC_SRC (the source iteration failed at row *err_rec, or a fragment error when
+ * *err_rec == -1), OC_ENC_EXPIRE (Record.Encode "invalid expire" at row *err_rec), OC_ENC_PANIC (Record.Encode
+ * panics: expire delta >= 2^35). Records before the error are written. offs[i] = dst offset of row i or
+ * UINT64_MAX (dropped / not reached); *n_in = rows visited. */
+enum { OC_ENC_OK = 0, OC_ENC_SRC = 1, OC_ENC_EXPIRE = 2, OC_ENC_PANIC = 3 };
+int oc_meta_app_size_zero(const uint8_t* meta, size_t n);
+void oc_compact_append(oc_writer* dst, oc_writer* hint, uint64_t dst_fid, const uint8_t* seg, uint64_t len,
+                       uint32_t start_off, uint64_t src_base, uint64_t dst_base, uint32_t ns_size,
+                       uint32_t etag_size, const uint8_t* keep, uint64_t n_keep, uint64_t* offs,
+                       int32_t* err_class, int64_t* err_rec, uint64_t* n_in);
+void oc_hint_by_wal(oc_writer* hint, uint64_t fid, const uint8_t* seg, uint64_t len, uint32_t start_off,
+                    uint64_t base_time, uint32_t ns_size, uint32_t etag_size, int32_t* err_class, int64_t* err_rec,
+                    uint64_t* n_in);
 
 /* ---- synthetic segments for configs A-E (deterministic, seeded) ---- */
 /* value_mode 0: fixed value_len; 1: 128*k, k ~ Zipf(s=1.1) on [1,512] */

@@ -64,11 +64,15 @@ lib.oc_decode_free.argtypes = [vp]
 lib.oc_decode_fast.restype = C.c_uint64
 lib.oc_decode_fast.argtypes = [vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
                                C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
-lib.oc_compact_append.restype = C.c_int64
+_i32p, _i64p, _u64p = C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_uint64)
+lib.oc_compact_append.restype = None
 lib.oc_compact_append.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32,
-                                  C.c_uint32, vp, C.c_uint64, vp]
-lib.oc_hint_by_wal.restype = C.c_int64
-lib.oc_hint_by_wal.argtypes = [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
+                                  C.c_uint32, vp, C.c_uint64, vp, _i32p, _i64p, _u64p]
+lib.oc_hint_by_wal.restype = None
+lib.oc_hint_by_wal.argtypes = [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                               _i32p, _i64p, _u64p]
+lib.oc_meta_app_size_zero.restype = C.c_int
+lib.oc_meta_app_size_zero.argtypes = [vp, C.c_size_t]
 lib.oc_synth_segment.restype = vp
 lib.oc_synth_segment.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
                                  C.c_uint64]
@@ -185,8 +189,29 @@ def synth(target_bytes: int, max_records: int, seed: int, ns_size: int = 20, key
     return out
 
 
-def hint_by_wal(seg, fid, start_off, base_time, ns_size, etag_size, create_time=None):
-    w = Writer(create_time if create_time is not None else base_time, base_time)
+def hint_by_wal(seg, fid, start_off, base_time, ns_size, etag_size, create_time=None, writer=None):
+    """NewHintByWal (hint.go:123-161). Returns (err_class, err_rec, n_in, hint file image)."""
+    w = writer or Writer(create_time if create_time is not None else base_time, base_time)
     seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
-    rc = lib.oc_hint_by_wal(w.h, fid, _ptr(seg), seg.size, start_off, base_time, ns_size, etag_size)
-    return rc, w.data()
+    ec, er, ni = C.c_int32(), C.c_int64(), C.c_uint64()
+    lib.oc_hint_by_wal(w.h, fid, _ptr(seg), seg.size, start_off, base_time, ns_size, etag_size, C.byref(ec),
+                       C.byref(er), C.byref(ni))
+    return int(ec.value), int(er.value), int(ni.value), w.data()
+
+
+def compact_append(dst: "Writer", hint: "Writer", dst_fid: int, seg, start_off: int, src_base: int, dst_base: int,
+                   ns_size: int, etag_size: int, keep):
+    """compactOneWal (compaction.go:294-327) appending to the dst / hint writers.
+    Returns (err_class, err_rec, n_in, offs) with offs[i] = dst offset of row i or 2**64-1."""
+    seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+    keep = np.ascontiguousarray(keep, dtype=np.uint8)
+    offs = np.full(max(keep.size, 1), np.iinfo(np.uint64).max, dtype=np.uint64)
+    ec, er, ni = C.c_int32(), C.c_int64(), C.c_uint64()
+    lib.oc_compact_append(dst.h, hint.h, dst_fid, _ptr(seg), seg.size, start_off, src_base, dst_base, ns_size,
+                          etag_size, _ptr(keep), keep.size, offs.ctypes.data_as(vp), C.byref(ec), C.byref(er),
+                          C.byref(ni))
+    return int(ec.value), int(er.value), int(ni.value), offs[:keep.size]
+
+
+def meta_app_size_zero(meta: bytes) -> bool:
+    return bool(lib.oc_meta_app_size_zero(_ptr(meta), len(meta)))

@@ -193,8 +193,8 @@ def case_panic_records():
 def case_hint(n=500):
     """a hint WAL rebuilt from a data WAL (hint.go:123-161)."""
     data, p = case_config_shape(n, 300)
-    rc, hint = O.hint_by_wal(data, 7, 40, BASE, 20, 20)
-    assert rc == 0
+    ec, _, _, hint = O.hint_by_wal(data, 7, 40, BASE, 20, 20)
+    assert ec == 0
     return hint, params(mode=1)
 
 

@@ -91,6 +91,8 @@ def record_encode(ns, key, value, etag=b"", expire=0, tombstone=False, meta=b"",
         flag |= 2
     elif expire < base_time:
         return None
+    elif expire - base_time >= 1 << 35:  # PutUvarint into a [MaxVarintLen32]byte array panics
+        return None
     else:
         exp = put_uvarint(expire - base_time)
     v = put_uvarint(len(key)) + put_uvarint(len(value)) + put_uvarint(len(meta))

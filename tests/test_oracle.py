@@ -51,7 +51,7 @@ def _rand_record(rng, base):
     key = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 200)))
     val = bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 5, 100, 4096, 33000, 70000])))
     etag = bytes(rng.getrandbits(8) for _ in range(20)) if rng.random() < 0.5 else b""
-    expire = 0 if rng.random() < 0.5 else base + rng.randrange(0, 1 << 40)
+    expire = 0 if rng.random() < 0.5 else base + rng.randrange(0, 1 << 34)
     meta = b"\x81\xa1k\xa1v" if rng.random() < 0.3 else b""
     return ns, key, val, etag, expire, rng.random() < 0.3, meta
 
@@ -65,6 +65,8 @@ def test_record_encode_parity(seed):
         a = O.record_encode(ns, key, val, etag, expire, tomb, meta, base)
         b = P.record_encode(ns, key, val, etag, expire, tomb, meta, base)
         assert a == b
+        if a is None:  # expire delta >= 2^35: the reference panics (both restatements agree)
+            continue
         st, f = P.record_from_bytes(a, base, 20, 20)
         assert st == 0 and f["key_len"] == len(key) and f["val_len"] == len(val)
     assert O.record_encode(b"", b"k", b"v", b"", base - 1, False, b"", base) is None  # "invalid expire"
@@ -169,3 +171,80 @@ def test_synth_counts():
     assert (d.recs["size"] == 4222).all()  # 26 B header + 100 B key + 4096 B value
     n, ec, _ = O.decode_fast(data, 40, 1_700_000_000, 20, 20)
     assert n == len(d.recs) and ec == 0
+
+
+def _py_meta_zero(m: bytes) -> bool:
+    """canonical msgpack empty maps (AppMetaSize 0): nil, {}, fixmap of empty strings / nils"""
+    if len(m) == 1:
+        return m[0] in (0xc0, 0x80)
+    return len(m) >= 3 and (m[0] & 0xf0) == 0x80 and len(m) == 1 + 2 * (m[0] & 15) and all(b in (0xa0, 0xc0) for b in m[1:])
+
+
+def _py_compact(data, keep, dst, hint, fid, src_base, dst_base, ns_size, etag_size):
+    """compactOneWal (compaction.go:294-327) restated over pyref: (err_class, err_rec, offs)."""
+    it = P.iterate(data, 40, src_base, ns_size, etag_size)
+    offs = []
+    for i, r in enumerate(it["recs"]):
+        if r["status"] != 0:
+            return 1, i, offs
+        if not keep[i]:
+            offs.append(None)
+            continue
+        p = r["payload"]
+        ns = p[1:1 + ns_size]
+        el = 0 if r["flags"] & 1 else etag_size
+        etag = p[r["etag_off"]:r["etag_off"] + el]
+        h, kl, vl, ml = r["hdr_size"], r["key_len"], r["val_len"], r["meta_len"]
+        key, val, meta = p[h:h + kl], p[h + kl:h + kl + vl], p[h + kl + vl:h + kl + vl + ml]
+        if _py_meta_zero(meta):
+            meta = b""
+        exp = r["expire"]
+        if exp != 0 and exp < dst_base:
+            return 2, i, offs
+        if exp != 0 and exp - dst_base >= 1 << 35:
+            return 3, i, offs
+        enc = P.record_encode(ns, key, val, etag, exp, bool(r["flags"] & 4), meta, dst_base)
+        o = dst.write_record(enc)
+        offs.append(o)
+        hint.write_record(P.hint_encode(ns, key, fid, o, len(enc)))
+    return (1 if it["err_class"] else 0), -1, offs
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_compact_oracle_vs_pyref(seed):
+    rng = random.Random(300 + seed)
+    base = 1_700_000_000
+    w = P.PyWal(base, base)
+    recs = []
+    for i in range(30):
+        ns, key, val, etag, expire, tomb, meta = _rand_record(rng, base)
+        if rng.random() < 0.1:
+            meta = rng.choice([b"\x80", b"\xc0", b"\x81\xa0\xa0"])
+        enc = P.record_encode(ns, key, val[:3000], etag, expire, tomb, meta, base)
+        if enc is not None:
+            recs.append(enc)
+            w.write_record(enc)
+    data = bytearray(w.buf)
+    if seed % 3 == 2:
+        data[rng.randrange(40, len(data))] ^= 4
+    data = bytes(data)
+    keep = [rng.random() < 0.7 for _ in recs]
+    dst_base = base - rng.choice([0, 10, 1 << 36]) if seed % 2 else base + rng.choice([0, 3])
+    pd, ph = P.PyWal(1, dst_base), P.PyWal(1, dst_base)
+    ec, er, offs = _py_compact(data, keep, pd, ph, 9, base, dst_base, 20, 20)
+    od, oh = O.Writer(1, dst_base), O.Writer(1, dst_base)
+    oec, oer, nin, ooffs = O.compact_append(od, oh, 9, data, 40, base, dst_base, 20, 20,
+                                            np.array(keep, dtype=np.uint8))
+    assert (oec, oer) == (ec, er)
+    assert od.data() == bytes(pd.buf) and oh.data() == bytes(ph.buf)
+    for i, o in enumerate(offs):
+        assert (o is None and ooffs[i] == np.iinfo(np.uint64).max) or o == ooffs[i]
+
+
+def test_meta_app_size_zero_and_expire_panic():
+    for m, z in [(b"\x80", 1), (b"\xc0", 1), (b"\x81\xa0\xa0", 1), (b"\x82\xa0\xc0\xc0\xa0", 1), (b"\x81\xa1k\xa0", 0),
+                 (b"", 0), (b"\x81\xa0", 0), (b"\x90", 0)]:
+        assert O.meta_app_size_zero(m) == bool(z) == _py_meta_zero(m) or (m == b"" and not O.meta_app_size_zero(m))
+    base = 1_700_000_000
+    assert O.record_encode(b"", b"k", b"v", b"", base + (1 << 35) - 1, False, b"", base) is not None
+    assert O.record_encode(b"", b"k", b"v", b"", base + (1 << 35), False, b"", base) is None  # reference panics
