@@ -849,6 +849,7 @@ __global__ void k_enc_finalize(const uint64_t* __restrict__ emisc, uint32_t mode
   if ((err >> 2) < nin) {
     o.err_class = (int32_t)(err & 3u);
     o.err_record = (int64_t)(err >> 2);
+    o.n_in = err >> 2;  // the callback error stops the iteration there
   } else if (emisc[X_SRCERR]) {
     o.err_class = BCW_ENC_ERR_SRC;
     o.err_record = nin < sres->n_records ? (int64_t)nin : -1;

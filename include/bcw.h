@@ -248,7 +248,7 @@ typedef struct bcw_encode_out {
 } bcw_encode_out;
 
 typedef struct bcw_encode_result {
-  uint64_t n_in;         /* source records delivered by the iteration (before any error) */
+  uint64_t n_in;         /* source rows fully processed before the iteration stopped (error row excluded) */
   uint64_t n_written;    /* records appended (dst WAL and hint WAL) */
   uint64_t wal_end;      /* dst WAL file size after the append */
   uint64_t hint_end;     /* hint WAL file size after the append */

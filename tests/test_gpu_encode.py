@@ -123,7 +123,7 @@ def test_compact_large_records(ctx):
 
 def test_compact_config_shape(ctx):
     """config E shape (ns 20, key 100, value 4096, everything kept) at 20k records."""
-    src = O.synth(0, 20000, 42)
+    src = O.synth(1 << 40, 20000, 42)
     keep = np.ones(20000, dtype=np.uint8)
     res = run_compact(ctx, src, keep)
     assert res.n_written == 20000
@@ -144,9 +144,9 @@ def test_compact_errors(ctx):
     r = run_compact(ctx, src, keep2, dst_base=BASE + 11)
     assert r.err_class == L.ENC_ERR_NONE
     # Record.Encode panic: expire delta >= 2^35 against the dst baseTime
-    payloads[60] = O.record_encode(b"A" * 20, b"k", b"v", b"", BASE + (1 << 35), False, b"", BASE)
+    payloads[60] = O.record_encode(b"A" * 20, b"k", b"v", b"", BASE + (1 << 35) - 1, False, b"", BASE)
     src = make_src(payloads)
-    r = run_compact(ctx, src, keep2, dst_base=BASE)
+    r = run_compact(ctx, src, keep2, dst_base=BASE - 1)
     assert r.err_class == L.ENC_ERR_PANIC and r.err_record == 60
     # source corruption: the iteration stops at the CRC error, earlier records are written
     bad = bytearray(make_src([rec_of(rng, i, kinds=False) for i in range(200)]))
@@ -171,7 +171,7 @@ def run_hint(ctx, src, ns=20, etag=20, fid=5):
 def test_hint_by_wal(ctx):
     rng = random.Random(11)
     run_hint(ctx, make_src([rec_of(rng, i) for i in range(500)]))
-    run_hint(ctx, O.synth(0, 3000, 1, value_mode=1))
+    run_hint(ctx, O.synth(1 << 40, 3000, 1, value_mode=1))
 
 
 def test_hint_by_wal_zero_length_first(ctx):
