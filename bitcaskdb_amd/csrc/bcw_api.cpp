@@ -337,7 +337,10 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   s.nlb = nwg;
   s.tickets = 0;
   s.epoch = 1;
-  if (hipMemset(s.lb, 0, nwg * 8) != hipSuccess || hipMemset(s.misc, 0, 16 * sizeof(uint64_t)) != hipSuccess) {
+  // on the codec's stream: a null-stream hipMemset is not ordered before kernels on a non-blocking
+  // stream, and a look-back word zeroed after k_chase published it would never be seen again
+  if (hipMemsetAsync(s.lb, 0, nwg * 8, c->cur) != hipSuccess ||
+      hipMemsetAsync(s.misc, 0, 16 * sizeof(uint64_t), c->cur) != hipSuccess) {
     free_scratch(s);
     return BCW_E_HIP;
   }
@@ -369,10 +372,16 @@ int bcw_decode_segment_async(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_
     HIPCHK(hipMemcpyAsync(d_result, &r, sizeof r, hipMemcpyHostToDevice, c->cur));
     return BCW_OK;
   }
-  if (bcw_max_fragments(p->seg_len, p->start_off) >= 0xfffffff0ull) return BCW_E_INVAL;  // u32 fragment ids
-  uint64_t want = std::max<uint64_t>(65536, (p->seg_len - p->start_off) / 256 + nblocks * 2);
+  // fragment ids are u32: segments may be any size as long as they hold < 2^32 - 16 fragments (a retry
+  // that asks for more is refused)
+  if (c->frag_hint >= 0xfffffff0ull) return BCW_E_INVAL;
+  // first guess of the fragment count (a retry sizes it exactly): 4 KiB-class records average ~4 KiB
+  // per fragment; hint WALs hold ~130 B records
+  const uint64_t per = p->mode == BCW_MODE_HINT ? 96 : 256;
+  uint64_t want = std::max<uint64_t>(65536, (p->seg_len - p->start_off) / per + nblocks * 2);
   want = std::max(want, c->frag_hint);
   want = std::min(want, bcw_max_fragments(p->seg_len, p->start_off) + 64);
+  want = std::min<uint64_t>(want, 0xfffffff0ull);
   int rc = ensure_scratch(c, nblocks, want);
   if (rc != BCW_OK) return rc;
   if (launch_decode(d_seg, *p, *t, d_result, c->tabs, c->s, nblocks, c->cur, c->num_cus, &c->prof) != hipSuccess)
@@ -541,7 +550,7 @@ static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows, uint64_t blk_w, uint64_
             hipMalloc(&e.desc_h, bh * enc_sizeof_desc()) == hipSuccess &&
             hipMalloc(&e.emisc, 64 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_enc_scratch(e); return BCW_E_NOMEM; }
-  (void)hipMemset(e.mflag, 0, r);
+  (void)hipMemsetAsync(e.mflag, 0, r, c->cur);
   e.rows_cap = r;
   e.blk_cap_w = bw;
   e.blk_cap_h = bh;

@@ -94,3 +94,19 @@ def test_truncations(ctx, cut):
 def test_empty_and_small(ctx):
     for data in (b"", bytes(40), bytes(46), bytes(47)):
         assert_parity(ctx, data, cases.params(), f"small{len(data)}")
+
+
+@pytest.mark.parametrize("vlen,mib,mode", [(10, 24, 0), (0, 24, 0), (300, 16, 0)])
+def test_dense_fragments_at_scale(ctx, vlen, mib, mode):
+    """~230 fragments per block (hint-WAL density) over many workgroups: exercises the fragment-table
+    retry (first capacity guess too small) and the multi-window ring of k_crc at full occupancy."""
+    seg = O.synth(mib << 20, 0, 11 + vlen, 20, 100, vlen, 0)
+    assert_parity(ctx, seg, cases.params(), f"dense vlen={vlen}")
+
+
+def test_hint_wal_at_scale(ctx):
+    """a hint WAL rebuilt from a 20 MiB data WAL, decoded in hint mode (IterateHint)."""
+    data = O.synth(20 << 20, 0, 5, 20, 100, 4096, 1)
+    ec, _, _, hint = O.hint_by_wal(data, 3, 40, 1_700_000_000, 20, 20)
+    assert ec == 0
+    assert_parity(ctx, hint, cases.params(mode=1), "hint at scale")

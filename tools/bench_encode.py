@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""Config E measurement: compaction re-encode (compactOneWal: Record.Encode + WriteRecord + hint) of
+N records (default 10 M, NsSize 20, 100 B keys, 4 KiB values, every record kept, dst baseTime = src
+baseTime) on one MI355X, device-resident, through the C-ABI (bcw_decode_segment_async then
+bcw_encode_segment_async on the same context).
+
+Full-size parity: with everything kept and equal baseTimes the re-encoded records equal the source
+records and a fresh dst WAL repeats the source layout, so the appended dst bytes must equal the source
+file from byte 40 (checked with torch.equal on the device); the hint WAL is decoded back on the device
+and its (off, size) fields must equal the returned offsets / source sizes. Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+BASE_TIME = 1_700_000_000
+HBM_PEAK_GBS = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=10_000_000)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    import torch
+    from bitcaskdb_amd import _lib as L
+    from bitcaskdb_amd import Context
+
+    dev = torch.device("cuda", 0)
+    t0 = time.time()
+    n, r = C.c_uint64(), C.c_uint64()
+    assert L.lib.bcw_synth_segment(1 << 62, args.records, 42, 20, 100, 4096, 0, BASE_TIME, None, 0, C.byref(n),
+                                   C.byref(r)) == 0
+    host = torch.empty(n.value, dtype=torch.uint8).pin_memory()
+    assert L.lib.bcw_synth_segment(1 << 62, args.records, 42, 20, 100, 4096, 0, BASE_TIME,
+                                   C.c_void_p(host.data_ptr()), n.value, C.byref(n), C.byref(r)) == 0
+    seg_len, n_rec = int(n.value), int(r.value)
+    print(f"synth {seg_len} B, {n_rec} records in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
+    d_src = host.to(dev, non_blocking=True)
+    torch.cuda.synchronize()
+    del host
+
+    cap = n_rec + 64
+    cols = {}
+    for name, dt in L.TABLE_COLUMNS:
+        tdt = {"u8": torch.int64, "u4": torch.int32, "u1": torch.uint8}[dt]
+        cols[name] = torch.empty(cap, dtype=tdt, device=dev)
+    ptr_t = {"u8": L.u64p, "u4": L.u32p, "u1": L.u8p}
+    table = L.RecordTable(cap, *[C.cast(C.c_void_p(cols[nm].data_ptr()), ptr_t[dt]) for nm, dt in L.TABLE_COLUMNS])
+    d_res = torch.zeros(C.sizeof(L.DecodeResult), dtype=torch.uint8, device=dev)
+    d_eres = torch.zeros(C.sizeof(L.EncodeResult), dtype=torch.uint8, device=dev)
+    keep = torch.ones(cap, dtype=torch.uint8, device=dev)
+    wal_cap = seg_len + (seg_len >> 6)
+    hint_cap = n_rec * 160 + (1 << 20)
+    d_wal = torch.empty(wal_cap, dtype=torch.uint8, device=dev)
+    d_hint = torch.empty(hint_cap, dtype=torch.uint8, device=dev)
+    d_off = torch.empty(cap, dtype=torch.int64, device=dev)
+    dparams = L.DecodeParams(seg_len, BASE_TIME, 40, 20, 20, L.MODE_RECORD)
+    eparams = L.EncodeParams(seg_len, BASE_TIME, 1, 40, 40, 40, L.ENC_COMPACT, 20, 20)
+    out = L.EncodeOut(C.cast(C.c_void_p(d_wal.data_ptr()), L.u8p), wal_cap,
+                      C.cast(C.c_void_p(d_hint.data_ptr()), L.u8p), hint_cap,
+                      C.cast(C.c_void_p(d_off.data_ptr()), L.u64p))
+    ctx = Context(0)
+    stream = torch.cuda.Stream()
+    ctx.set_stream(stream.cuda_stream)
+
+    def decode():
+        assert L.lib.bcw_decode_segment_async(ctx.handle, C.c_void_p(d_src.data_ptr()), C.byref(dparams),
+                                              C.byref(table), C.c_void_p(d_res.data_ptr())) == 0
+
+    def decode_checked(seg_ptr, prm):
+        # async API contract: a result with retry_frag_capacity != 0 is invalid; the next call on the
+        # context is sized for it
+        for _ in range(2):
+            assert L.lib.bcw_decode_segment_async(ctx.handle, C.c_void_p(seg_ptr), C.byref(prm), C.byref(table),
+                                                  C.c_void_p(d_res.data_ptr())) == 0
+            torch.cuda.synchronize()
+            rr = L.DecodeResult.from_buffer_copy(bytes(d_res.cpu().numpy()))
+            if not rr.retry_frag_capacity:
+                return rr
+        raise SystemExit("decode retry failed")
+
+    def encode():
+        assert L.lib.bcw_encode_segment_async(ctx.handle, C.c_void_p(d_src.data_ptr()), C.byref(eparams),
+                                              C.byref(table), C.c_void_p(d_res.data_ptr()),
+                                              C.c_void_p(keep.data_ptr()), C.byref(out),
+                                              C.c_void_p(d_eres.data_ptr())) == 0
+
+    decode_checked(d_src.data_ptr(), dparams)
+    for _ in range(args.warmup):
+        encode()
+    torch.cuda.synchronize()
+    res = L.EncodeResult.from_buffer_copy(bytes(d_eres.cpu().numpy()))
+    assert res.fits and res.err_class == 0 and res.n_written == n_rec, (res.fits, res.err_class, res.n_written)
+    wal_bytes, hint_bytes = int(res.wal_need), int(res.hint_need)
+    # full-size parity: dst WAL == source WAL from byte 40
+    same = wal_bytes == seg_len - 40 and bool(torch.equal(d_wal[:wal_bytes], d_src[40:]))
+    # the hint WAL decodes to (off, size) = (returned offsets, source sizes)
+    sb = (C.c_uint8 * 40)()
+    L.lib.bcw_write_super_block(sb, BASE_TIME, BASE_TIME)
+    himg = torch.empty(40 + hint_bytes, dtype=torch.uint8, device=dev)
+    himg[:40] = torch.frombuffer(bytearray(bytes(sb)), dtype=torch.uint8).to(dev)
+    himg[40:] = d_hint[:hint_bytes]
+    hp = L.DecodeParams(40 + hint_bytes, BASE_TIME, 40, 20, 0, L.MODE_HINT)
+    torch.cuda.synchronize()  # the image was assembled on torch's stream, the codec runs on its own
+    hres = decode_checked(himg.data_ptr(), hp)
+    hint_ok = (hres.err_class == 0 and hres.n_records == n_rec and int(hres.first_bad_record) == -1
+               and bool(torch.equal(cols["aux0"][:n_rec], d_off[:n_rec])))
+    if not hint_ok:
+        a, b = cols["aux0"][:n_rec], d_off[:n_rec]
+        bad = torch.nonzero(a != b)
+        print("hint check:", hres.err_class, hres.n_records, n_rec, hres.first_bad_record, hres.err_frag,
+              "mismatches", bad.numel(), bad[:5].flatten().tolist(),
+              [(int(a[i]), int(b[i])) for i in bad[:5].flatten().tolist()], file=sys.stderr)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O  # noqa: E402  (diagnostics only)
+        hcpu = himg.cpu().numpy()
+        od = O.decode(hcpu, 40, BASE_TIME, 20, 0, 1, want_bytes=False)
+        print("oracle hint decode:", od.err_class, len(od.recs), od.err_frag, file=sys.stderr)
+        if od.err_class:
+            f = od.frags[od.err_frag]
+            print("bad frag", f, "block", (int(f["data_off"]) - 40) // 32768, file=sys.stderr)
+    del himg
+    # the timed loop re-decodes the source first (the encode reads the context's fragment table)
+    decode_checked(d_src.data_ptr(), dparams)
+    torch.cuda.synchronize()
+    nk = int(L.lib.bcw_ctx_kernel_times(ctx.handle, None, None, 0))
+    names = [L.lib.bcw_kernel_name(k).decode() for k in range(nk)]
+    L.lib.bcw_ctx_set_profiling(ctx.handle, -1)
+    L.lib.bcw_ctx_kernel_times(ctx.handle, None, None, nk)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        encode()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    enc_ms = e0.elapsed_time(e1) / args.steps
+    tot = (C.c_double * nk)()
+    cnt = (C.c_uint64 * nk)()
+    L.lib.bcw_ctx_kernel_times(ctx.handle, tot, cnt, nk)
+    kern = {names[k]: round(tot[k] / cnt[k], 4) for k in range(nk) if cnt[k]}
+    # decode + encode (a whole compactOneWal of the segment)
+    L.lib.bcw_ctx_set_profiling(ctx.handle, 0)
+    e0.record(stream)
+    for _ in range(args.steps):
+        decode()
+        encode()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    both_ms = e0.elapsed_time(e1) / args.steps
+    alg = seg_len + wal_bytes + hint_bytes  # source read once + both outputs written
+    pack_ms = kern.get("k_pack", 0) + kern.get("k_pack_hint", 0)
+    line = {
+        "metric": "compaction re-encode GB/s (device-resident, config E)", "value": round(alg / (enc_ms * 1e-3) / 1e9, 1),
+        "unit": "GB/s (src read + WAL + hint written)", "records": n_rec, "src_bytes": seg_len, "wal_bytes": wal_bytes,
+        "hint_bytes": hint_bytes, "encode_ms": round(enc_ms, 3), "decode_plus_encode_ms": round(both_ms, 3),
+        "records_per_s": round(n_rec / (enc_ms * 1e-3)), "kernel_ms": kern,
+        "roofline": {"bound": "hbm", "kernel": "k_pack+k_pack_hint",
+                     "achieved": round(alg / (pack_ms * 1e-3) / 1e9, 1) if pack_ms else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(alg / (pack_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pack_ms else None},
+        "layout_events": {"wal": int(res.wal_events), "hint": int(res.hint_events)},
+        "parity": {"wal_equals_source": same, "hint_decodes_to_offsets": hint_ok},
+    }
+    s = json.dumps(line)
+    print(s, flush=True)
+    if args.out:
+        with open(args.out, "w") as fh:
+            fh.write(s + "\n")
+    if not (same and hint_ok):
+        raise SystemExit("config E parity check failed")
+
+
+if __name__ == "__main__":
+    main()
