@@ -272,7 +272,8 @@ static void free_scratch(Scratch& s) {
 }
 
 static void free_enc_scratch(EncScratch& e) {
-  void* ptrs[] = {e.sz, e.mflag, e.dsrc, e.da, e.hda, e.hsz, e.dpos, e.tiles, e.ev, e.evb, e.desc_w, e.desc_h, e.emisc};
+  void* ptrs[] = {e.sz,     e.mflag,  e.dsrc,   e.da,      e.hda,   e.hsz, e.dpos,
+                  e.tiles,  e.ev,     e.evb,    e.desc_w,  e.desc_h, e.recdesc, e.emisc};
   for (void* q : ptrs) (void)hipFree(q);
   e = EncScratch{};
 }
@@ -548,6 +549,7 @@ static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows, uint64_t blk_w, uint64_
             hipMalloc(&e.ev, (r + 2) * enc_sizeof_ev()) == hipSuccess && hipMalloc(&e.evb, nwin * 4) == hipSuccess &&
             hipMalloc(&e.desc_w, bw * enc_sizeof_desc()) == hipSuccess &&
             hipMalloc(&e.desc_h, bh * enc_sizeof_desc()) == hipSuccess &&
+            hipMalloc(&e.recdesc, r * enc_sizeof_recdesc()) == hipSuccess &&
             hipMalloc(&e.emisc, 64 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_enc_scratch(e); return BCW_E_NOMEM; }
   (void)hipMemsetAsync(e.mflag, 0, r, c->cur);
@@ -593,6 +595,7 @@ int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_
   L.frags = c->s.frags;
   L.crc_ops = c->tabs.enc_ops;
   L.initc = c->tabs.initc;
+  L.num_cus = c->num_cus;
   return launch_encode(L, c->es, c->cur, &c->prof) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 

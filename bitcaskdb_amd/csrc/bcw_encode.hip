@@ -28,6 +28,9 @@
 // all but rare records (~7/M of them): k_events runs it over 4096 records per step with a
 // workgroup-wide ballot, and every other quantity (block starts, record offsets, fragment types
 // and lengths) follows in parallel from the event list.
+#include <algorithm>
+#include <cstdlib>
+
 #include "bcw_internal.h"
 
 namespace bcw {
@@ -39,7 +42,6 @@ constexpr int kTileItems = 4096;          // scan tile: 256 threads x 16 items
 constexpr int kEvThreads = 1024;
 constexpr int kEvPer = 4;
 constexpr int kEvWin = kEvThreads * kEvPer;  // records per k_events step
-constexpr int kPackThreads = 512;
 constexpr int kJobCap = 1024;
 constexpr int kJobsPerRec = 8;
 
@@ -544,10 +546,7 @@ __device__ __forceinline__ uint32_t op_apply(const uint32_t* __restrict__ op, ui
 struct PackArgs {
   EncDev e;
   const uint64_t* da;       // this layout's y-coordinates (dense, N+1)
-  const uint64_t* dst_da;   // dst layout's (hint of a compaction: payload size of the dst record)
-  const uint64_t* dpos;     // dst record offsets (hint of a compaction)
-  const uint32_t* dsrc;     // dense -> source row (nullptr: identity)
-  const uint8_t* mflag;
+  const void* rd;           // RecDesc per dense record (k_recdesc)
   const BlkDesc* desc;
   const uint64_t* emisc;
   int lay;
@@ -555,7 +554,64 @@ struct PackArgs {
   uint64_t pos, cap;        // file offset of out[0]; out capacity
   const uint32_t* crc_ops;  // [2][16][8][16]: A_{8*128*m}, A_{8*2048*m}, m < 16
   const uint32_t* initc;    // A_{8L}(0xFFFFFFFF)
+  uint32_t abl;             // ablation bits for measurements only (0 in the product): 1 no CRC, 2 no copy, 8 no store
 };
+
+// Per written record: its payload as up to 6 pieces (literal bytes or ranges of the source payload)
+// and the source payload's placement in the source file. Built once per record by k_recdesc, read
+// by the one or two k_pack workgroups whose blocks hold the record.
+struct RecDesc {
+  uint64_t d0;       // file offset of the data of the source payload's first fragment
+  uint32_t l0;       // its length
+  uint32_t f0, f1;   // source fragments (irregular records are walked)
+  uint16_t regular;  // fragments after the first are whole blocks' data: closed-form placement
+  uint8_t npieces, psrc;  // psrc bit q: piece q is a source range
+  uint32_t plen[6];
+  uint32_t poff[6];  // source payload offset (source piece) or offset into lit
+  uint8_t lit[48];
+  uint64_t _pad;
+};
+static_assert(sizeof(RecDesc) == 128, "RecDesc layout");
+
+template <int PM>
+__global__ __launch_bounds__(256) void k_recdesc(EncDev e, const uint64_t* __restrict__ emisc,
+                                                  const uint32_t* __restrict__ dsrc, const uint64_t* __restrict__ dst_da,
+                                                  const uint64_t* __restrict__ dpos, const uint8_t* __restrict__ mflag,
+                                                  RecDesc* __restrict__ rd) {
+  const uint64_t j = blockIdx.x * 256ull + threadIdx.x;
+  if (j >= emisc[X_NDENSE]) return;
+  const uint64_t row = dsrc[j];
+  Prog p;
+  if (PM == PM_DST) prog_record(e, row, mflag[row] != 0, p);
+  else if (PM == PM_HINT_DST) prog_hint(e, row, dpos[j], dst_da[j + 1] - dst_da[j] - kHdr, p);
+  else prog_hint(e, row, e.t.foff[row] - kHdr, e.t.size[row], p);
+  const SrcRec sr = src_rec(e.t, e.frags, row);
+  const Frag F0 = e.frags[sr.f0];
+  RecDesc d;
+  d.d0 = frag_file(F0, e.start_off);
+  d.l0 = F0.len;
+  d.f0 = sr.f0;
+  d.f1 = sr.f1;
+  bool reg = true;
+  for (uint32_t f = sr.f0 + 1; f <= sr.f1 && reg; ++f) {
+    const Frag F = e.frags[f];
+    reg = F.blk == F0.blk + (f - sr.f0) && F.start == kHdr && (f == sr.f1 || F.len == kM);
+  }
+  d.regular = reg ? 1 : 0;
+  d.npieces = (uint8_t)p.n;
+  d.psrc = 0;
+  for (uint32_t q = 0; q < 6; ++q) {
+    d.plen[q] = q < p.n ? p.len[q] : 0;
+    d.poff[q] = q < p.n ? (uint32_t)p.off[q] : 0;
+    if (q < p.n && p.src[q]) d.psrc |= (uint8_t)(1u << q);
+  }
+#pragma unroll
+  for (int b = 0; b < 48; ++b) d.lit[b] = p.lit[b];
+  uint4* dst = reinterpret_cast<uint4*>(rd + j);
+  const uint4* s = reinterpret_cast<const uint4*>(&d);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) dst[k] = s[k];
+}
 
 __device__ __forceinline__ uint8_t img_get(const uint32_t* img, uint32_t b) {
   return (uint8_t)(img[b >> 2] >> ((b & 3u) * 8));
@@ -565,18 +621,13 @@ __device__ __forceinline__ void img_put(uint32_t* img, uint32_t b, uint8_t v) {
 }
 
 // 16 source bytes at an arbitrary address from two aligned 16 B loads (caller checks bounds)
-__device__ __forceinline__ uint4 load16_shift(const uint8_t* __restrict__ seg, uint64_t s) {
-  const uint64_t a = s & ~15ull;
-  const uint32_t sh = (uint32_t)(s & 15u);
-  const uint4 v0 = *reinterpret_cast<const uint4*>(seg + a);
+__device__ __forceinline__ uint4 shift16(uint4 v0, uint4 v1, uint32_t sh) {
   if (sh == 0) return v0;
-  const uint4 v1 = *reinterpret_cast<const uint4*>(seg + a + 16);
   const uint32_t W[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
   const uint32_t w = sh >> 2, b = sh & 3u;
   uint32_t o[5];
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    // o[k] = W[w + k] (w + k <= 7)
     uint32_t x = W[k];
     if (w == 1) x = W[k + 1];
     if (w == 2) x = W[k + 2];
@@ -591,235 +642,331 @@ __device__ __forceinline__ uint4 load16_shift(const uint8_t* __restrict__ seg, u
   return r;
 }
 
+// source payload offset z -> file offset (regular records: closed form)
+__device__ __forceinline__ uint64_t src_at(const RecDesc& d, uint32_t start_off, uint64_t z, uint64_t& run) {
+  if (z < d.l0) { run = d.l0 - z; return d.d0 + z; }
+  const uint64_t zz = z - d.l0;
+  const uint64_t q = zz / kM, r = zz - q * kM;
+  const uint64_t blk0 = (d.d0 - start_off) / kL;
+  run = kM - r;
+  return (uint64_t)start_off + (blk0 + 1 + q) * kL + kHdr + r;
+}
+
+constexpr int kPT = 512;   // k_pack threads
+constexpr int kPWaves = kPT / 64;
+constexpr int kRecBatch = kPT;
+
+// k_pack: persistent workgroups, one output block at a time: (1) each record with a fragment in the
+// block writes its literal bytes into the LDS image and queues source copy jobs; (2) the waves copy
+// the jobs (lanes over 16 B image chunks, loads issued ahead of the LDS writes); (3) CRC-32C of every
+// fragment: 128 B windows aligned to the fragment end, two slice-by-4 chains per window, shifted to
+// the fragment end with A_{8*128*m} and XOR-ed into the fragment's accumulator; headers written;
+// (4) the image streams out with aligned 16 B stores.
 template <int PM>
-__global__ __launch_bounds__(kPackThreads) void k_pack(PackArgs A) {
+__global__ __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4))) void k_pack(PackArgs A) {
   const uint64_t* X = A.emisc + X_LAY + A.lay * kLayStride;
   const uint64_t b0 = X[4], ke = X[2];
-  const uint64_t k = b0 + blockIdx.x;
-  if (ke == b0 - 1 || k > ke) return;
-  if (X[3] - A.pos > A.cap) return;  // output does not fit: nothing is written (result says so)
+  if (ke == b0 - 1 || X[3] - A.pos > A.cap) return;  // nothing to write / does not fit (result says so)
+  const uint64_t K = ke - b0 + 1;
   const EncDev& e = A.e;
-  const BlkDesc D = A.desc[blockIdx.x];
   const uint64_t N = A.emisc[X_NDENSE];
-  const int64_t Y = D.Y;
-  const int64_t E = Y + (int64_t)kL - (int64_t)kHdr * D.c;
+  const RecDesc* __restrict__ RD = static_cast<const RecDesc*>(A.rd);
 
   __shared__ __attribute__((aligned(16))) uint32_t img[kL / 4 + 8];
-  __shared__ uint32_t tab[256];
+  __shared__ uint32_t tab[4 * 256];
   __shared__ uint32_t ops[2 * 16 * 128];
-  __shared__ uint16_t f_hdr[kPackThreads], f_dat[kPackThreads], f_len[kPackThreads];
-  __shared__ uint8_t f_type[kPackThreads];
-  __shared__ uint32_t f_acc[kPackThreads], f_win[kPackThreads + 1];
+  __shared__ uint32_t half[128];
+  __shared__ uint16_t f_hdr[kRecBatch], f_dat[kRecBatch], f_len[kRecBatch];
+  __shared__ uint8_t f_type[kRecBatch];
+  __shared__ uint32_t f_acc[kRecBatch], f_win[kRecBatch + 1];
   __shared__ uint16_t j_img[kJobCap], j_len[kJobCap];
   __shared__ uint64_t j_src[kJobCap];
   __shared__ uint32_t j_pre[kJobCap + 1];
-  __shared__ uint32_t s_njobs, s_nrec, s_scan[kPackThreads / 64];
+  __shared__ uint32_t s_njobs, s_nrec, s_scan[kPWaves];
 
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (uint32_t i = tid; i < 256; i += kPackThreads) {
+  // slice-by-4 tables (tab[256*k + b] = CRC of byte b followed by k zero bytes) and operators
+  for (uint32_t i = tid; i < 256; i += kPT) {
     uint32_t c = i;
     for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
     tab[i] = c;
   }
-  for (uint32_t i = tid; i < 2 * 16 * 128; i += kPackThreads) ops[i] = A.crc_ops[i];
-  // pad bytes at the block end are zero (wal.go:505-511)
-  if (D.pad) for (uint32_t b = kL - D.pad + tid; b < kL; b += kPackThreads) img_put(img, b, 0);
+  for (uint32_t i = tid; i < 2 * 16 * 128; i += kPT) ops[i] = A.crc_ops[i];
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t c = tab[tid];
+    for (int k = 1; k < 4; ++k) { c = (c >> 8) ^ tab[c & 0xffu]; tab[256 * k + tid] = c; }
+  }
+  // A_{8*64}: 64 zero bytes (half-window join)
+  if (tid < 128) {
+    const uint32_t i = tid >> 4, n = tid & 15u;
+    uint32_t x = n << (4 * i);
+    for (int b = 0; b < 64; ++b) x = (x >> 8) ^ tab[x & 0xffu];
+    half[tid] = x;
+  }
+  __syncthreads();
 
-  for (uint64_t rb = D.first;; rb += kPackThreads) {
-    // ---- one batch of up to 512 records: fragment of each in this block, literals, copy jobs ----
-    if (tid == 0) { s_njobs = 0; s_nrec = 0; }
-    __syncthreads();
-    const uint64_t j = rb + tid;
-    bool act = false;
-    uint64_t aj = 0, aj1 = 0;
-    if (j < N) {
-      aj = A.da[j];
-      aj1 = A.da[j + 1];
-      act = ((int64_t)aj < Y) || ((int64_t)aj + (int64_t)kHdr <= E);
-    }
-    if (act) atomicAdd(&s_nrec, 1u);
-    f_acc[tid] = 0;
-    if (act) {
-      const bool cont = (int64_t)aj < Y;
-      const int64_t y0 = cont ? Y : (int64_t)aj + kHdr;
-      const int64_t y1 = (int64_t)aj1 < E ? (int64_t)aj1 : E;
-      const uint32_t hdr = cont ? 0u : (uint32_t)(kHdr * D.c + ((int64_t)aj - Y));
-      const uint32_t d0 = hdr + kHdr;
-      const uint32_t len = (uint32_t)(y1 - y0);
-      const bool ends = (int64_t)aj1 <= E;
-      f_hdr[tid] = (uint16_t)hdr;
-      f_dat[tid] = (uint16_t)d0;
-      f_len[tid] = (uint16_t)len;
-      f_type[tid] = cont ? (ends ? BCW_RECORD_LAST : BCW_RECORD_MIDDLE) : (ends ? BCW_RECORD_FULL : BCW_RECORD_FIRST);
-      // payload range of this fragment
-      const uint64_t x0 = (uint64_t)(y0 - (int64_t)aj - kHdr), x1 = x0 + len;
-      const uint64_t row = A.dsrc ? A.dsrc[j] : j;
-      Prog p;
-      if (PM == PM_DST) {
-        prog_record(e, row, A.mflag[row] != 0, p);
-      } else if (PM == PM_HINT_DST) {
-        prog_hint(e, row, A.dpos[j], A.dst_da[j + 1] - A.dst_da[j] - kHdr, p);
-      } else {
-        prog_hint(e, row, e.t.foff[row] - kHdr, e.t.size[row], p);
+  for (uint64_t kb = blockIdx.x; kb < K; kb += gridDim.x) {
+    const uint64_t k = b0 + kb;
+    const BlkDesc D = A.desc[kb];
+    const int64_t Y = D.Y;
+    const int64_t E = Y + (int64_t)kL - (int64_t)kHdr * D.c;
+    if (D.pad) for (uint32_t b = kL - D.pad + tid; b < kL; b += kPT) img_put(img, b, 0);
+
+    for (uint64_t rb = D.first;; rb += kRecBatch) {
+      if (tid == 0) { s_njobs = 0; s_nrec = 0; }
+      __syncthreads();
+      // ---- (1) one record per thread: fragment geometry, literals, copy jobs ----
+      const uint64_t j = rb + tid;
+      bool act = false;
+      uint64_t aj = 0, aj1 = 0;
+      if (j < N) {
+        aj = A.da[j];
+        aj1 = A.da[j + 1];
+        act = ((int64_t)aj < Y) || ((int64_t)aj + (int64_t)kHdr <= E);
       }
-      const SrcRec sr = src_rec(e.t, e.frags, row);
-      uint64_t pb = 0;  // payload offset of piece q
-      bool slow = false;
-      for (uint32_t q = 0; q < p.n; ++q) {
-        const uint64_t pe = pb + p.len[q];
-        const uint64_t s0 = pb > x0 ? pb : x0, s1 = pe < x1 ? pe : x1;
-        if (s0 < s1) {
-          uint32_t io = d0 + (uint32_t)(s0 - x0);
-          if (!p.src[q]) {
-            for (uint64_t s = s0; s < s1; ++s) img_put(img, io++, p.lit[p.off[q] + (s - pb)]);
-          } else {
-            // source payload [z, z + l) -> fragment data ranges -> copy jobs
-            uint64_t z = p.off[q] + (s0 - pb), l = s1 - s0;
-            uint32_t f = sr.f0;
-            Frag F = e.frags[f];
-            uint64_t cum = 0;
-            while (z >= cum + F.len && f < sr.f1) { cum += F.len; ++f; F = e.frags[f]; }
-            while (l > 0) {
-              const uint64_t in = z - cum;
-              uint64_t take = F.len - in;
-              if (take > l || f >= sr.f1) take = l;
-              const uint64_t src = frag_file(F, e.start_off) + in;
-              uint32_t slot = kJobCap;
-              if (!slow) {
-                slot = atomicAdd(&s_njobs, 1u);
-                if (slot >= kJobCap) slow = true;
+      if (act) atomicAdd(&s_nrec, 1u);
+      f_acc[tid] = 0;
+      if (act) {
+        const bool cont = (int64_t)aj < Y;
+        const int64_t y0 = cont ? Y : (int64_t)aj + kHdr;
+        const int64_t y1 = (int64_t)aj1 < E ? (int64_t)aj1 : E;
+        const uint32_t hdr = cont ? 0u : (uint32_t)(kHdr * D.c + ((int64_t)aj - Y));
+        const uint32_t d0 = hdr + kHdr;
+        const uint32_t len = (uint32_t)(y1 - y0);
+        const bool ends = (int64_t)aj1 <= E;
+        f_hdr[tid] = (uint16_t)hdr;
+        f_dat[tid] = (uint16_t)d0;
+        f_len[tid] = (uint16_t)len;
+        f_type[tid] = cont ? (ends ? BCW_RECORD_LAST : BCW_RECORD_MIDDLE) : (ends ? BCW_RECORD_FULL : BCW_RECORD_FIRST);
+        const uint64_t x0 = (uint64_t)(y0 - (int64_t)aj - kHdr), x1 = x0 + len;
+        RecDesc d;
+        {
+          const uint4* s = reinterpret_cast<const uint4*>(RD + j);
+          uint4* t = reinterpret_cast<uint4*>(&d);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) t[q] = s[q];
+        }
+        uint64_t pb = 0;
+        bool slow = false;
+        for (uint32_t q = 0; q < d.npieces; ++q) {
+          const uint64_t pe = pb + d.plen[q];
+          const uint64_t s0 = pb > x0 ? pb : x0, s1 = pe < x1 ? pe : x1;
+          if (s0 < s1) {
+            uint32_t io = d0 + (uint32_t)(s0 - x0);
+            if (!((d.psrc >> q) & 1u)) {
+              for (uint64_t s = s0; s < s1; ++s) img_put(img, io++, d.lit[d.poff[q] + (s - pb)]);
+            } else {
+              uint64_t z = d.poff[q] + (s0 - pb), l = s1 - s0;
+              // irregular source records: walk their fragments
+              uint32_t f = d.f0;
+              Frag F{};
+              uint64_t cum = 0;
+              if (!d.regular) {
+                F = e.frags[f];
+                while (z >= cum + F.len && f < d.f1) { cum += F.len; ++f; F = e.frags[f]; }
               }
-              if (slow) {
-                for (uint64_t b = 0; b < take; ++b) img_put(img, io + (uint32_t)b, e.seg[src + b]);
-              } else {
-                j_img[slot] = (uint16_t)io;
-                j_len[slot] = (uint16_t)take;
-                j_src[slot] = src;
+              while (l > 0) {
+                uint64_t src, take;
+                if (d.regular) {
+                  src = src_at(d, e.start_off, z, take);
+                } else {
+                  const uint64_t in = z - cum;
+                  take = F.len - in;
+                  if (f >= d.f1) take = l;
+                  src = frag_file(F, e.start_off) + in;
+                }
+                if (take > l) take = l;
+                uint32_t slot = kJobCap;
+                if (!slow) {
+                  slot = atomicAdd(&s_njobs, 1u);
+                  if (slot >= kJobCap) slow = true;
+                }
+                if (slow) {
+                  for (uint64_t b = 0; b < take; ++b) img_put(img, io + (uint32_t)b, e.seg[src + b]);
+                } else {
+                  j_img[slot] = (uint16_t)io;
+                  j_len[slot] = (uint16_t)take;
+                  j_src[slot] = src;
+                }
+                io += (uint32_t)take;
+                z += take;
+                l -= take;
+                if (!d.regular && l > 0) { cum += F.len; ++f; F = e.frags[f]; }
               }
-              io += (uint32_t)take;
-              z += take;
-              l -= take;
-              cum += F.len;
-              if (l > 0) { ++f; F = e.frags[f]; }
+            }
+          }
+          pb = pe;
+        }
+      }
+      __syncthreads();
+      const uint32_t nrec = s_nrec;
+      const uint32_t njobs = min(s_njobs, (uint32_t)kJobCap);
+      if (nrec == 0) break;
+      // ---- (2) copy jobs: prefix of the jobs' 16 B image chunks, then every thread takes 4 chunks
+      //      per round (job lookup, both loads of all 4 issued before any LDS write) ----
+      for (uint32_t base = 0; base < njobs; base += kPT) {
+        const uint32_t q = base + tid;
+        uint32_t cnt = 0;
+        if (q < njobs) {
+          const uint32_t o = j_img[q], l = j_len[q];
+          cnt = l ? ((o + l + 15) >> 4) - (o >> 4) : 0;
+        }
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) { const uint32_t t = __shfl_up(incl, d, 64); if (lane >= (uint32_t)d) incl += t; }
+        if (lane == 63) s_scan[wave] = incl;
+        __syncthreads();
+        uint32_t pre = base ? j_pre[base] : 0;
+        for (uint32_t w = 0; w < wave; ++w) pre += s_scan[w];
+        if (q < njobs) j_pre[q + 1] = pre + incl;
+        if (q == 0) j_pre[0] = 0;
+        __syncthreads();
+      }
+      const uint32_t nunits = (njobs && !(A.abl & 2)) ? j_pre[njobs] : 0;
+      for (uint32_t u0 = tid; u0 < nunits; u0 += 4 * kPT) {
+        uint4 v0[4], v1[4];
+        uint32_t c0s[4], c1s[4];
+        uint64_t ss[4];
+        bool full[4];
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) {
+          const uint32_t u = u0 + (uint32_t)k2 * kPT;
+          full[k2] = false;
+          c0s[k2] = c1s[k2] = 0;
+          ss[k2] = 0;
+          if (u < nunits) {
+            uint32_t lo = 0, hi = njobs;  // largest q with j_pre[q] <= u
+            while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (j_pre[mid] <= u) lo = mid; else hi = mid; }
+            const uint32_t o = j_img[lo], l = j_len[lo];
+            const uint32_t c = (o >> 4) + (u - j_pre[lo]);
+            const uint32_t c0 = c * 16 > o ? c * 16 : o;
+            const uint32_t c1 = c * 16 + 16 < o + l ? c * 16 + 16 : o + l;
+            const uint64_t sv = j_src[lo] + (c0 - o);
+            c0s[k2] = c0;
+            c1s[k2] = c1;
+            ss[k2] = sv;
+            if (c1 - c0 == 16 && (sv & ~15ull) + 32 <= e.src_len) {
+              full[k2] = true;
+              v0[k2] = *reinterpret_cast<const uint4*>(e.seg + (sv & ~15ull));
+              v1[k2] = *reinterpret_cast<const uint4*>(e.seg + (sv & ~15ull) + 16);
             }
           }
         }
-        pb = pe;
-      }
-    }
-    __syncthreads();
-    const uint32_t nrec = s_nrec;
-    const uint32_t njobs = min(s_njobs, (uint32_t)kJobCap);
-    if (nrec == 0) break;
-    // ---- copy jobs: 16 B image chunks of every job, spread over the workgroup ----
-    for (uint32_t base = 0; base < njobs; base += kPackThreads) {
-      const uint32_t q = base + tid;
-      uint32_t cnt = 0;
-      if (q < njobs) {
-        const uint32_t o = j_img[q], l = j_len[q];
-        cnt = l ? ((o + l + 15) >> 4) - (o >> 4) : 0;
-      }
-      uint32_t incl = cnt;
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) { const uint32_t t = __shfl_up(incl, d, 64); if (lane >= (uint32_t)d) incl += t; }
-      if (lane == 63) s_scan[wave] = incl;
-      __syncthreads();
-      uint32_t pre = base ? j_pre[base] : 0;
-      for (uint32_t w = 0; w < wave; ++w) pre += s_scan[w];
-      if (q < njobs) j_pre[q + 1] = pre + incl;
-      if (q == 0) j_pre[0] = 0;
-      __syncthreads();
-    }
-    const uint32_t nunits = njobs ? j_pre[njobs] : 0;
-    for (uint32_t u = tid; u < nunits; u += kPackThreads) {
-      uint32_t lo = 0, hi = njobs;  // largest q with j_pre[q] <= u
-      while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (j_pre[mid] <= u) lo = mid; else hi = mid; }
-      const uint32_t o = j_img[lo], l = j_len[lo];
-      const uint64_t src = j_src[lo];
-      const uint32_t c = (o >> 4) + (u - j_pre[lo]);
-      const uint32_t c0 = c * 16 > o ? c * 16 : o;
-      const uint32_t c1 = c * 16 + 16 < o + l ? c * 16 + 16 : o + l;
-      const uint64_t s = src + (c0 - o);
-      if (c1 - c0 == 16 && (s & ~15ull) + 32 <= e.src_len) {
-        const uint4 v = load16_shift(e.seg, s);
-        *reinterpret_cast<uint4*>(&img[c0 >> 2]) = v;
-      } else {
-        for (uint32_t b = c0; b < c1; ++b) img_put(img, b, e.seg[s + (b - c0)]);
+        for (int k2 = 0; k2 < 4; ++k2) {
+          if (full[k2]) {
+            *reinterpret_cast<uint4*>(&img[c0s[k2] >> 2]) = shift16(v0[k2], v1[k2], (uint32_t)(ss[k2] & 15u));
+          } else {
+            for (uint32_t b = c0s[k2]; b < c1s[k2]; ++b) img_put(img, b, e.seg[ss[k2] + (b - c0s[k2])]);
+          }
+        }
       }
-    }
-    __syncthreads();
-    // ---- CRC-32C of every fragment: 128 B windows aligned to the fragment end, one per lane ----
-    {
-      const uint32_t f = tid;
-      const uint32_t cw = (f < nrec) ? ((uint32_t)f_len[f] + 127u) >> 7 : 0u;
-      uint32_t incl = cw;
+      // window counts of the fragments (128 B windows, end-aligned)
+      {
+        const uint32_t cw = (tid < nrec) ? ((uint32_t)f_len[tid] + 127u) >> 7 : 0u;
+        uint32_t incl = cw;
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) { const uint32_t t = __shfl_up(incl, d, 64); if (lane >= (uint32_t)d) incl += t; }
-      if (lane == 63) s_scan[wave] = incl;
-      __syncthreads();
-      uint32_t pre = 0;
-      for (uint32_t w = 0; w < wave; ++w) pre += s_scan[w];
-      f_win[f + 1] = pre + incl;
-      if (f == 0) f_win[0] = 0;
-      __syncthreads();
-    }
-    const uint32_t nwin = f_win[nrec];
-    for (uint32_t w = tid; w < nwin; w += kPackThreads) {
-      uint32_t lo = 0, hi = nrec;  // largest f with f_win[f] <= w
-      while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (f_win[mid] <= w) lo = mid; else hi = mid; }
-      const uint32_t f = lo;
-      const uint32_t cwin = f_win[f + 1] - f_win[f];
-      const uint32_t m = cwin - 1 - (w - f_win[f]);  // windows between this one and the fragment end
-      const uint32_t dend = (uint32_t)f_dat[f] + f_len[f];
-      const uint32_t we = dend - 128u * m;
-      const uint32_t ws = (we - f_dat[f] > 128u) ? we - 128u : f_dat[f];
-      uint32_t c = 0;
-      for (uint32_t b = ws; b < we; ++b) c = tab[(c ^ img_get(img, b)) & 0xffu] ^ (c >> 8);
-      if (m & 15u) c = op_apply(&ops[(m & 15u) * 128], c);
-      if (m >> 4) c = op_apply(&ops[2048 + (m >> 4) * 128], c);
-      atomicXor(&f_acc[f], c);
-    }
-    __syncthreads();
-    if (tid < nrec) {
-      const uint32_t len = f_len[tid];
-      const uint32_t crc = ~(f_acc[tid] ^ A.initc[len]);
-      const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
-      const uint32_t h = f_hdr[tid];
-      img_put(img, h + 0, (uint8_t)masked);
-      img_put(img, h + 1, (uint8_t)(masked >> 8));
-      img_put(img, h + 2, (uint8_t)(masked >> 16));
-      img_put(img, h + 3, (uint8_t)(masked >> 24));
-      img_put(img, h + 4, (uint8_t)len);
-      img_put(img, h + 5, (uint8_t)(len >> 8));
-      img_put(img, h + 6, f_type[tid]);
-    }
-    __syncthreads();
-    if (nrec < kPackThreads) break;
-  }
-  __syncthreads();
-  // ---- store image [lo, hi) at out[file - pos]: aligned 16 B stores, bytes at the edges ----
-  const int64_t base = (int64_t)(40 + k * kL) - (int64_t)A.pos;  // out offset of image byte 0
-  const int64_t o0 = base + D.lo, o1 = base + D.hi;
-  const int64_t a0 = (o0 + 15) & ~15ll, a1 = o1 & ~15ll;
-  if (a0 >= a1) {
-    for (int64_t o = o0 + tid; o < o1; o += kPackThreads) A.out[o] = img_get(img, (uint32_t)(o - base));
-  } else {
-    for (int64_t o = o0 + tid; o < a0; o += kPackThreads) A.out[o] = img_get(img, (uint32_t)(o - base));
-    for (int64_t o = a1 + tid; o < o1; o += kPackThreads) A.out[o] = img_get(img, (uint32_t)(o - base));
-    const uint32_t sh = (uint32_t)((a0 - base) & 3);
-    for (int64_t o = a0 + 16 * (int64_t)tid; o < a1; o += 16 * kPackThreads) {
-      const uint32_t ib = (uint32_t)(o - base);
-      const uint32_t w0 = ib >> 2;
-      uint4 v;
-      if (sh == 0) {
-        v = make_uint4(img[w0], img[w0 + 1], img[w0 + 2], img[w0 + 3]);
-      } else {
-        const uint32_t x0 = img[w0], x1 = img[w0 + 1], x2 = img[w0 + 2], x3 = img[w0 + 3], x4 = img[w0 + 4];
-        v = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+        for (int d = 1; d < 64; d <<= 1) { const uint32_t t = __shfl_up(incl, d, 64); if (lane >= (uint32_t)d) incl += t; }
+        if (lane == 63) s_scan[wave] = incl;
+        __syncthreads();  // also: the copies are complete
+        uint32_t pre = 0;
+        for (uint32_t w = 0; w < wave; ++w) pre += s_scan[w];
+        f_win[tid + 1] = pre + incl;
+        if (tid == 0) f_win[0] = 0;
+        __syncthreads();
       }
-      *reinterpret_cast<uint4*>(A.out + o) = v;
+      // ---- (3) CRC windows ----
+      const uint32_t nwin = (A.abl & 1) ? 0 : f_win[nrec];
+      for (uint32_t w = tid; w < nwin; w += kPT) {
+        uint32_t lo = 0, hi = nrec;
+        while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (f_win[mid] <= w) lo = mid; else hi = mid; }
+        const uint32_t f = lo;
+        const uint32_t m = f_win[f + 1] - 1 - w;  // windows between this one and the fragment end
+        const int32_t fs = f_dat[f];
+        const int32_t we = fs + (int32_t)f_len[f] - 128 * (int32_t)m;
+        const int32_t base = we - 128;
+        const int32_t dw = base >> 2;  // arithmetic: negative bases read clamped (masked) words
+        const uint32_t sh = (uint32_t)(base & 3);
+        uint32_t wv[32];
+        uint32_t prev = dw >= 0 ? img[dw] : 0u;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          const int32_t idx = dw + 1 + i;
+          const uint32_t nx = idx >= 0 ? img[idx] : 0u;
+          wv[i] = __builtin_amdgcn_alignbyte(nx, prev, sh);
+          prev = nx;
+        }
+        // zero the bytes before the fragment start (first window only)
+        const int32_t zb = fs - base;  // bytes to clear
+        if (zb > 0) {
+#pragma unroll
+          for (int i = 0; i < 32; ++i) {
+            int32_t t = zb - 4 * i;
+            t = t < 0 ? 0 : (t > 4 ? 4 : t);
+            wv[i] &= (uint32_t)(0xffffffffull << (8 * t));
+          }
+        }
+        uint32_t ca = 0, cb2 = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          ca ^= wv[i];
+          ca = tab[768 + (ca & 0xffu)] ^ tab[512 + ((ca >> 8) & 0xffu)] ^ tab[256 + ((ca >> 16) & 0xffu)] ^ tab[ca >> 24];
+          cb2 ^= wv[16 + i];
+          cb2 = tab[768 + (cb2 & 0xffu)] ^ tab[512 + ((cb2 >> 8) & 0xffu)] ^ tab[256 + ((cb2 >> 16) & 0xffu)] ^ tab[cb2 >> 24];
+        }
+        uint32_t c = op_apply(half, ca) ^ cb2;
+        if (m & 15u) c = op_apply(&ops[(m & 15u) * 128], c);
+        if (m >> 4) c = op_apply(&ops[2048 + (m >> 4) * 128], c);
+        atomicXor(&f_acc[f], c);
+      }
+      __syncthreads();
+      if (tid < nrec) {
+        const uint32_t len = f_len[tid];
+        const uint32_t crc = ~(f_acc[tid] ^ A.initc[len]);
+        const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
+        const uint32_t h = f_hdr[tid];
+        img_put(img, h + 0, (uint8_t)masked);
+        img_put(img, h + 1, (uint8_t)(masked >> 8));
+        img_put(img, h + 2, (uint8_t)(masked >> 16));
+        img_put(img, h + 3, (uint8_t)(masked >> 24));
+        img_put(img, h + 4, (uint8_t)len);
+        img_put(img, h + 5, (uint8_t)(len >> 8));
+        img_put(img, h + 6, f_type[tid]);
+      }
+      __syncthreads();
+      if (nrec < kRecBatch) break;
     }
+    // ---- (4) store image [lo, hi) at out[file - pos]: aligned 16 B stores, bytes at the edges ----
+    if (!(A.abl & 8)) {
+      const int64_t base = (int64_t)(40 + k * kL) - (int64_t)A.pos;  // out offset of image byte 0
+      const int64_t o0 = base + D.lo, o1 = base + D.hi;
+      const int64_t a0 = (o0 + 15) & ~15ll, a1 = o1 & ~15ll;
+      if (a0 >= a1) {
+        for (int64_t o = o0 + tid; o < o1; o += kPT) A.out[o] = img_get(img, (uint32_t)(o - base));
+      } else {
+        for (int64_t o = o0 + tid; o < a0; o += kPT) A.out[o] = img_get(img, (uint32_t)(o - base));
+        for (int64_t o = a1 + tid; o < o1; o += kPT) A.out[o] = img_get(img, (uint32_t)(o - base));
+        const uint32_t sh = (uint32_t)((a0 - base) & 3);
+        for (int64_t o = a0 + 16 * (int64_t)tid; o < a1; o += 16 * kPT) {
+          const uint32_t ib = (uint32_t)(o - base);
+          const uint32_t w0 = ib >> 2;
+          uint4 v;
+          if (sh == 0) {
+            v = make_uint4(img[w0], img[w0 + 1], img[w0 + 2], img[w0 + 3]);
+          } else {
+            const uint32_t x0 = img[w0], x1 = img[w0 + 1], x2 = img[w0 + 2], x3 = img[w0 + 3], x4 = img[w0 + 4];
+            v = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                           __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+          }
+          __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(A.out + o));
+          __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(A.out + o) + 1);
+          __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(A.out + o) + 2);
+          __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(A.out + o) + 3);
+        }
+      }
+    }
+    __syncthreads();  // the image is reused by the next block
   }
 }
 
@@ -915,12 +1062,18 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
   };
   PackArgs A{};
   A.e = e;
-  A.dsrc = s.dsrc;
-  A.mflag = s.mflag;
+  A.rd = s.recdesc;
   A.emisc = s.emisc;
   A.crc_ops = L.crc_ops;
   A.initc = L.initc;
+  {
+    static const char* ev = getenv("BCW_PACK_ABL");
+    A.abl = ev ? (uint32_t)atoi(ev) : 0u;
+  }
   const uint32_t rgrid = (uint32_t)((rows + 255) / 256) + 1;
+  RecDesc* rdp = static_cast<RecDesc*>(s.recdesc);
+  // persistent pack grid: two 512-thread workgroups per CU (LDS ~75 KiB each)
+  auto pgrid = [&](uint64_t blocks) { return (uint32_t)std::min<uint64_t>(blocks, (uint64_t)L.num_cus * 2); };
   if (compact) {
     pr.begin(K_ENC_SCAN, st, ev0);
     scan(s.sz, 1, 0, s.da);
@@ -934,21 +1087,21 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     A.pos = L.p.wal_pos;
     A.cap = L.out.wal_cap;
     pr.begin(K_ENC_PACK, st, ev0);
-    k_pack<PM_DST><<<(uint32_t)s.blk_cap_w, kPackThreads, 0, st>>>(A);
+    k_recdesc<PM_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, rdp);
+    k_pack<PM_DST><<<pgrid(s.blk_cap_w), kPT, 0, st>>>(A);
     pr.end(K_ENC_PACK, st, ev0);
     k_hint_sizes<<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.hsz);
     scan(s.hsz, 0, 1, s.hda);
     layout(1, s.hda, L.p.hint_pos, desc_h, s.blk_cap_h);
     A.da = s.hda;
-    A.dst_da = s.da;
-    A.dpos = s.dpos;
     A.desc = desc_h;
     A.lay = 1;
     A.out = L.out.hint;
     A.pos = L.p.hint_pos;
     A.cap = L.out.hint_cap;
     pr.begin(K_ENC_PACK_HINT, st, ev0);
-    k_pack<PM_HINT_DST><<<(uint32_t)s.blk_cap_h, kPackThreads, 0, st>>>(A);
+    k_recdesc<PM_HINT_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag, rdp);
+    k_pack<PM_HINT_DST><<<pgrid(s.blk_cap_h), kPT, 0, st>>>(A);
     pr.end(K_ENC_PACK_HINT, st, ev0);
   } else {
     pr.begin(K_ENC_SCAN, st, ev0);
@@ -962,7 +1115,8 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     A.pos = L.p.hint_pos;
     A.cap = L.out.hint_cap;
     pr.begin(K_ENC_PACK_HINT, st, ev0);
-    k_pack<PM_HINT_SRC><<<(uint32_t)s.blk_cap_h, kPackThreads, 0, st>>>(A);
+    k_recdesc<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, rdp);
+    k_pack<PM_HINT_SRC><<<pgrid(s.blk_cap_h), kPT, 0, st>>>(A);
     pr.end(K_ENC_PACK_HINT, st, ev0);
   }
   k_enc_finalize<<<1, 1, 0, st>>>(s.emisc, L.p.mode, L.p.wal_pos, L.out.wal_cap, L.p.hint_pos, L.out.hint_cap,
@@ -971,6 +1125,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
 }
 
 size_t enc_sizeof_ev() { return sizeof(enc::Ev); }
+size_t enc_sizeof_recdesc() { return sizeof(enc::RecDesc); }
 size_t enc_sizeof_desc() { return sizeof(enc::BlkDesc); }
 size_t enc_sizeof_tile() { return sizeof(enc::TileSum); }
 int enc_tile_items() { return enc::kTileItems; }

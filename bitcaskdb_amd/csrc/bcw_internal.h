@@ -122,6 +122,7 @@ struct EncScratch {
   uint32_t* evb = nullptr;    // [rows/win+2] governing event per k_events window
   void* desc_w = nullptr;     // [blk_cap_w] block descriptors (dst WAL)
   void* desc_h = nullptr;     // [blk_cap_h] (hint WAL)
+  void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc -> k_pack)
   uint64_t* emisc = nullptr;  // [64] counters
 };
 
@@ -137,10 +138,12 @@ struct EncLaunch {
   const Frag* frags;
   const uint32_t* crc_ops;
   const uint32_t* initc;
+  int num_cus;
 };
 
 hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t stream, Prof* prof);
 size_t enc_sizeof_ev();
+size_t enc_sizeof_recdesc();
 size_t enc_sizeof_desc();
 size_t enc_sizeof_tile();
 int enc_tile_items();
