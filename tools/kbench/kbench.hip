@@ -2,6 +2,7 @@
 // pipeline and k_crc variants on a synthetic 1 GiB config-B segment.
 #include "../../bitcaskdb_amd/csrc/bcw_api.cpp"
 #include "../../bitcaskdb_amd/csrc/bcw_decode.hip"
+#include "../../bitcaskdb_amd/csrc/bcw_encode.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -193,6 +194,22 @@ int main(int argc, char** argv) {
   bcw_ctx_set_profiling(ctx, 0);
   for (int k = 0; k < nk; ++k) printf("  %-14s %.4f ms\n", bcw_kernel_name(k), tot[k] / (cnt[k] ? cnt[k] : 1));
   Scratch& s = ctx->s;
+  {  // k_crc timeline: wall_clock64 (100 MHz) stamps of WG 0's start and the last workgroup's final scan
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipEventRecord(a, st));
+      CK(bcw_decode_segment_async(ctx, d, &p, &t, dres));
+      CK(hipEventRecord(b, st));
+      CK(hipStreamSynchronize(st));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      uint64_t mc[16];
+      CK(hipMemcpy(mc, s.misc, sizeof mc, hipMemcpyDeviceToHost));
+      printf("timeline: pipeline %.1f us; k_crc WG0 start -> final scan start %.1f us, final scan %.1f us\n", ms * 1e3,
+             (mc[M_T_SCAN0] - mc[M_T_CRC0]) / 100.0, (mc[M_T_SCAN1] - mc[M_T_SCAN0]) / 100.0);
+    }
+  }
   const uint64_t nblocks = (n - 40 + kBlock - 1) / kBlock;
   auto run = [&](auto kern, int grid) {
     return timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, s.pre, s.wgagg, s.wgx, s.misc); },
