@@ -118,6 +118,8 @@ struct bcw_ctx {
   int num_cus = 256;
   hipStream_t own = nullptr;
   hipStream_t cur = nullptr;
+  hipStream_t aux = nullptr;  // encode: the hint WAL's layout + pack beside the dst pack
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   Tables tabs{};
   Scratch s{};
   EncScratch es{};
@@ -221,6 +223,12 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return BCW_E_HIP; }
+  if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+    bcw_ctx_destroy(c);
+    return BCW_E_HIP;
+  }
   c->cur = c->own;
   std::vector<uint32_t> slice(512), fwd(64 * 128), carry(128), half(128), initc(kBlock + 1);
   build_slice_tables(slice.data());
@@ -272,8 +280,8 @@ static void free_scratch(Scratch& s) {
 }
 
 static void free_enc_scratch(EncScratch& e) {
-  void* ptrs[] = {e.sz,     e.mflag,  e.dsrc,   e.da,      e.hda,   e.hsz, e.dpos,
-                  e.tiles,  e.ev,     e.evb,    e.desc_w,  e.desc_h, e.recdesc, e.emisc};
+  void* ptrs[] = {e.sz,    e.mflag,  e.dsrc,   e.da,      e.hda,    e.hsz,       e.dpos,
+                  e.tiles, e.ev,     e.evb,    e.desc_w,  e.desc_h, e.recdesc,   e.recdesc_h, e.emisc};
   for (void* q : ptrs) (void)hipFree(q);
   e = EncScratch{};
 }
@@ -299,6 +307,9 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   (void)hipFree(c->d_result);
   for (auto& m : c->prof.marks) { (void)hipEventDestroy(m.a); (void)hipEventDestroy(m.b); }
   for (auto e : c->prof.pool) (void)hipEventDestroy(e);
+  if (c->aux) { (void)hipStreamSynchronize(c->aux); (void)hipStreamDestroy(c->aux); }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
   return BCW_OK;
@@ -550,6 +561,7 @@ static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows, uint64_t blk_w, uint64_
             hipMalloc(&e.desc_w, bw * enc_sizeof_desc()) == hipSuccess &&
             hipMalloc(&e.desc_h, bh * enc_sizeof_desc()) == hipSuccess &&
             hipMalloc(&e.recdesc, r * enc_sizeof_recdesc()) == hipSuccess &&
+            hipMalloc(&e.recdesc_h, r * enc_sizeof_recdesc()) == hipSuccess &&
             hipMalloc(&e.emisc, 64 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_enc_scratch(e); return BCW_E_NOMEM; }
   (void)hipMemsetAsync(e.mflag, 0, r, c->cur);
@@ -596,6 +608,9 @@ int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_
   L.crc_ops = c->tabs.enc_ops;
   L.initc = c->tabs.initc;
   L.num_cus = c->num_cus;
+  L.aux = c->aux;
+  L.ev_fork = c->ev_fork;
+  L.ev_join = c->ev_join;
   return launch_encode(L, c->es, c->cur, &c->prof) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 

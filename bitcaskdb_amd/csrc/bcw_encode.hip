@@ -40,8 +40,7 @@ constexpr uint32_t kL = kBlock;           // 32768
 constexpr uint32_t kM = kBlock - kHdr;    // 32761
 constexpr int kTileItems = 4096;          // scan tile: 256 threads x 16 items
 constexpr int kEvThreads = 1024;
-constexpr int kEvPer = 4;
-constexpr int kEvWin = kEvThreads * kEvPer;  // records per k_events step
+constexpr int kEvWin = 4096;  // records per k_events step (LDS double buffer: 2 x 40 KiB)
 constexpr int kJobCap = 1024;
 constexpr int kJobsPerRec = 8;
 
@@ -291,6 +290,9 @@ struct Ev {
   uint32_t pad;
 };
 
+// One workgroup: wave 0 scans a window of kEvWin records per step out of LDS (8 residues per lane
+// per ballot, events resolved in the wave without barriers), while waves 1..15 load the next
+// window's y-coordinates into the other LDS buffer. One barrier per window.
 __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restrict__ da, uint64_t* __restrict__ emisc,
                                                         int lay, uint64_t q0, Ev* __restrict__ ev,
                                                         uint32_t* __restrict__ evb) {
@@ -299,87 +301,102 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
   const uint64_t AN = X[0];
   const int64_t U = (int64_t)(q0 % kL);
   const uint64_t b0 = q0 / kL;
+  __shared__ __attribute__((aligned(16))) uint64_t s_a[2][kEvWin];
+  __shared__ __attribute__((aligned(16))) uint16_t s_r[2][kEvWin];
   __shared__ int64_t s_ya;
   __shared__ uint64_t s_kb;
-  __shared__ uint32_t s_rho, s_nev, s_best;
-  __shared__ uint32_t s_wmin[kEvThreads / 64];
-  if (threadIdx.x == 0) {
+  __shared__ uint32_t s_nev;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // scanner state (wave 0, wave-uniform)
+  int64_t ya = -U;
+  uint64_t kb = b0;
+  uint32_t nev = 1;
+  uint32_t rho = (uint32_t)((kL - U) % kM);  // the virtual block ends at y = L - U
+  if (tid == 0) {
     ev[0] = {b0, -U, 0xffffffffu, 0};
-    int64_t ya = -U;
-    uint64_t kb = b0;
-    uint32_t nev = 1;
-    uint32_t rho = (uint32_t)((kL - U) % kM);  // the virtual block ends at y = L - U
-    if (N > 0 && kL - U < (int64_t)kHdr) {    // record 0's header does not fit: pad, event at record 0
-      ev[1] = {b0 + 1, 0, 0u, (uint32_t)(kL - U)};
-      ya = 0;
-      kb = b0 + 1;
-      nev = 2;
-      rho = kL % kM;
-    }
-    s_ya = ya; s_kb = kb; s_rho = rho; s_nev = nev;
+    if (N > 0 && kL - U < (int64_t)kHdr) ev[1] = {b0 + 1, 0, 0u, (uint32_t)(kL - U)};
   }
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (uint64_t base = 0; base < N; base += kEvWin) {
-    if (threadIdx.x == 0) evb[base / kEvWin] = s_nev - 1;
-    uint64_t a[kEvPer];
-    uint32_t r[kEvPer];
+  if (N > 0 && kL - U < (int64_t)kHdr) {  // record 0's header does not fit: pad, event at record 0
+    ya = 0;
+    kb = b0 + 1;
+    nev = 2;
+    rho = kL % kM;
+  }
+  auto load_window = [&](uint64_t base, int buf, uint32_t t0, uint32_t nt) {
+    constexpr int kB = 8;  // loads in flight per thread before the LDS writes
+    for (uint32_t i0 = t0; i0 < (uint32_t)kEvWin; i0 += kB * nt) {
+      uint64_t av[kB];
 #pragma unroll
-    for (int k = 0; k < kEvPer; ++k) {
-      const uint64_t idx = base + (uint64_t)k * kEvThreads + threadIdx.x;
-      a[k] = idx < N ? da[idx] : 0;
-      r[k] = (uint32_t)(a[k] % kM);
-    }
-    // record 0 is never tested against the virtual event (its header is in block b0 or it is ev[1])
-    int last = (base == 0) ? 0 : -1;
-    uint32_t rho = s_rho;
-    for (;;) {
-      uint32_t best = 0xffffffffu;
+      for (int k = 0; k < kB; ++k) {
+        const uint32_t i = i0 + (uint32_t)k * nt;
+        const uint64_t idx = base + i;
+        av[k] = (i < (uint32_t)kEvWin && idx < N) ? da[idx] : 0;
+      }
 #pragma unroll
-      for (int k = kEvPer - 1; k >= 0; --k) {
-        const uint32_t q = (uint32_t)k * kEvThreads + threadIdx.x;
-        const uint64_t idx = base + q;
-        if (idx < N && (int)q > last) {
-          int32_t d = (int32_t)rho - (int32_t)r[k];
-          if (d < 0) d += kM;
-          if (d <= 6) best = q;
+      for (int k = 0; k < kB; ++k) {
+        const uint32_t i = i0 + (uint32_t)k * nt;
+        if (i < (uint32_t)kEvWin) {
+          s_a[buf][i] = av[k];
+          s_r[buf][i] = (uint16_t)(av[k] % kM);
         }
       }
-      for (int d = 32; d >= 1; d >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, d, 64));
-      if (lane == 0) s_wmin[wave] = best;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint32_t m = 0xffffffffu;
-        for (int w = 0; w < kEvThreads / 64; ++w) m = min(m, s_wmin[w]);
-        s_best = m;
-      }
-      __syncthreads();
-      const uint32_t b = s_best;
-      if (b == 0xffffffffu) break;
-      if (threadIdx.x == (b & (kEvThreads - 1))) {  // the owner records the event
-        const int k = (int)(b / kEvThreads);
-        uint64_t ai = a[0];
-        uint32_t ri = r[0];
-#pragma unroll
-        for (int kk = 1; kk < kEvPer; ++kk) if (kk == k) { ai = a[kk]; ri = r[kk]; }
-        int32_t d = (int32_t)s_rho - (int32_t)ri;
-        if (d < 0) d += kM;
-        const int64_t E = (int64_t)ai + d;                         // block end that hits the header
-        const uint64_t m = (uint64_t)(E - s_ya - (int64_t)kL) / kM;  // blocks after the event block
-        const uint64_t kb = s_kb + m + 1;
-        ev[s_nev] = {kb, (int64_t)ai, (uint32_t)(base + b), (uint32_t)d};
-        s_nev = s_nev + 1;
-        s_kb = kb;
-        s_ya = (int64_t)ai;
-        s_rho = (ri + kHdr) % kM;
-      }
-      __syncthreads();
-      rho = s_rho;
-      last = (int)b;
     }
+  };
+  if (N > 0) load_window(0, 0, tid, kEvThreads);
+  __syncthreads();
+  const uint64_t nwin = (N + kEvWin - 1) / kEvWin;
+  for (uint64_t w = 0; w < nwin; ++w) {
+    const int buf = (int)(w & 1);
+    const uint64_t base = w * kEvWin;
+    if (wave != 0) {
+      if (w + 1 < nwin) load_window(base + kEvWin, buf ^ 1, tid - 64, kEvThreads - 64);
+    } else {
+      if (lane == 0) evb[w] = nev - 1;
+      const uint32_t nrec = (uint32_t)((N - base) < (uint64_t)kEvWin ? (N - base) : (uint64_t)kEvWin);
+      // records of group g: [512 g, 512 g + 512); lane l tests [512 g + 8 l, +8)
+      for (uint32_t g0 = 0; g0 < nrec; g0 += 512) {
+        const uint32_t i0 = g0 + 8 * lane;
+        uint32_t rr[8];
+        {
+          const uint4 v = *reinterpret_cast<const uint4*>(&s_r[buf][i0]);
+          rr[0] = v.x & 0xffffu; rr[1] = v.x >> 16; rr[2] = v.y & 0xffffu; rr[3] = v.y >> 16;
+          rr[4] = v.z & 0xffffu; rr[5] = v.z >> 16; rr[6] = v.w & 0xffffu; rr[7] = v.w >> 16;
+        }
+        int32_t last = (base == 0) ? 0 : -1;  // record 0 is never an event of the virtual block
+        last -= (int32_t)g0;                  // in group-relative indices
+        for (;;) {
+          uint32_t first = 0xffffffffu;  // this lane's first candidate after `last` (group-relative)
+#pragma unroll
+          for (int k = 7; k >= 0; --k) {
+            const int32_t q = 8 * (int32_t)lane + k;
+            if (g0 + (uint32_t)q < nrec && q > last) {
+              int32_t d = (int32_t)rho - (int32_t)rr[k];
+              if (d < 0) d += kM;
+              if (d <= 6) first = (uint32_t)q;
+            }
+          }
+          const uint64_t m = __ballot(first != 0xffffffffu);
+          if (!m) break;
+          const uint32_t owner = (uint32_t)__builtin_ctzll(m);
+          const uint32_t q = __builtin_amdgcn_readlane(first, owner);  // lowest lane holds the lowest index
+          const uint64_t ai = s_a[buf][g0 + q];
+          const uint32_t ri = (uint32_t)s_r[buf][g0 + q];
+          int32_t d = (int32_t)rho - (int32_t)ri;
+          if (d < 0) d += kM;
+          const int64_t E = (int64_t)ai + d;                      // block end that hits the header
+          const uint64_t mm = (uint64_t)(E - ya - (int64_t)kL) / kM;  // blocks after the event block
+          kb = kb + mm + 1;
+          ya = (int64_t)ai;
+          if (lane == 0) ev[nev] = {kb, ya, (uint32_t)(base + g0 + q), (uint32_t)d};
+          ++nev;
+          rho = (ri + kHdr) % kM;
+          last = (int32_t)q;
+        }
+      }
+    }
+    __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const uint32_t nev = s_nev;
+  if (tid == 0) {
     X[1] = nev;
     X[4] = b0;
     X[5] = (uint64_t)U;
@@ -387,8 +404,6 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
       X[2] = b0 - 1;  // no blocks
       X[3] = 40 + q0;
     } else {
-      const int64_t ya = s_ya;
-      const uint64_t kb = s_kb;
       // the block whose end E_k >= A_N first: E_kb = ya + L, E_{kb+m} = ya + L + m M
       const int64_t over = (int64_t)AN - ya - (int64_t)kL;
       const uint64_t m = over > 0 ? ((uint64_t)over + kM - 1) / kM : 0;
@@ -399,6 +414,7 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
       X[3] = 40 + ke * kL + kHdr * c + (uint64_t)((int64_t)AN - Y);
     }
   }
+  (void)s_ya; (void)s_kb; (void)s_nev;
 }
 
 // per-block descriptor for k_pack
@@ -613,11 +629,15 @@ __global__ __launch_bounds__(256) void k_recdesc(EncDev e, const uint64_t* __res
   for (int k = 0; k < 8; ++k) dst[k] = s[k];
 }
 
+// The LDS block image is skewed by one dword per 128 B (word w lives at w + w/32): lanes reading
+// consecutive 128 B CRC windows would otherwise all hit the same bank. 16 B chunks (the copy and
+// store units) never straddle a pad word.
+__device__ __forceinline__ uint32_t iw(uint32_t w) { return w + (w >> 5); }
 __device__ __forceinline__ uint8_t img_get(const uint32_t* img, uint32_t b) {
-  return (uint8_t)(img[b >> 2] >> ((b & 3u) * 8));
+  return (uint8_t)(img[iw(b >> 2)] >> ((b & 3u) * 8));
 }
 __device__ __forceinline__ void img_put(uint32_t* img, uint32_t b, uint8_t v) {
-  reinterpret_cast<uint8_t*>(img)[b] = v;
+  reinterpret_cast<uint8_t*>(img)[iw(b >> 2) * 4 + (b & 3u)] = v;
 }
 
 // 16 source bytes at an arbitrary address from two aligned 16 B loads (caller checks bounds)
@@ -627,12 +647,10 @@ __device__ __forceinline__ uint4 shift16(uint4 v0, uint4 v1, uint32_t sh) {
   const uint32_t w = sh >> 2, b = sh & 3u;
   uint32_t o[5];
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    uint32_t x = W[k];
-    if (w == 1) x = W[k + 1];
-    if (w == 2) x = W[k + 2];
-    if (w == 3) x = W[(k + 3) & 7];
-    o[k] = x;
+  for (int k = 0; k < 5; ++k) {  // o[k] = W[k + w] by two selects (static indices: no scratch)
+    const uint32_t lo = (w & 1u) ? W[k + 1] : W[k];
+    const uint32_t hi = (w & 1u) ? W[(k + 3) & 7] : W[(k + 2) & 7];
+    o[k] = (w & 2u) ? hi : lo;
   }
   uint4 r;
   r.x = __builtin_amdgcn_alignbyte(o[1], o[0], b);
@@ -643,11 +661,11 @@ __device__ __forceinline__ uint4 shift16(uint4 v0, uint4 v1, uint32_t sh) {
 }
 
 // source payload offset z -> file offset (regular records: closed form)
-__device__ __forceinline__ uint64_t src_at(const RecDesc& d, uint32_t start_off, uint64_t z, uint64_t& run) {
-  if (z < d.l0) { run = d.l0 - z; return d.d0 + z; }
-  const uint64_t zz = z - d.l0;
+__device__ __forceinline__ uint64_t src_at(uint64_t d0, uint32_t l0, uint32_t start_off, uint64_t z, uint64_t& run) {
+  if (z < l0) { run = l0 - z; return d0 + z; }
+  const uint64_t zz = z - l0;
   const uint64_t q = zz / kM, r = zz - q * kM;
-  const uint64_t blk0 = (d.d0 - start_off) / kL;
+  const uint64_t blk0 = (d0 - start_off) / kL;
   run = kM - r;
   return (uint64_t)start_off + (blk0 + 1 + q) * kL + kHdr + r;
 }
@@ -672,7 +690,7 @@ __global__ __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint64_t N = A.emisc[X_NDENSE];
   const RecDesc* __restrict__ RD = static_cast<const RecDesc*>(A.rd);
 
-  __shared__ __attribute__((aligned(16))) uint32_t img[kL / 4 + 8];
+  __shared__ __attribute__((aligned(16))) uint32_t img[kL / 4 + kL / 128 + 8];
   __shared__ uint32_t tab[4 * 256];
   __shared__ uint32_t ops[2 * 16 * 128];
   __shared__ uint32_t half[128];
@@ -720,7 +738,12 @@ __global__ __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4))) void k
       const uint64_t j = rb + tid;
       bool act = false;
       uint64_t aj = 0, aj1 = 0;
+      uint4 rv[5];  // descriptor bytes [0, 80): everything but the literals (static indexing only)
       if (j < N) {
+        // the descriptor load does not depend on the y-coordinates: both in flight together
+        const uint4* sp = reinterpret_cast<const uint4*>(RD + j);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) rv[q] = sp[q];
         aj = A.da[j];
         aj1 = A.da[j + 1];
         act = ((int64_t)aj < Y) || ((int64_t)aj + (int64_t)kHdr <= E);
@@ -740,24 +763,33 @@ __global__ __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4))) void k
         f_len[tid] = (uint16_t)len;
         f_type[tid] = cont ? (ends ? BCW_RECORD_LAST : BCW_RECORD_MIDDLE) : (ends ? BCW_RECORD_FULL : BCW_RECORD_FIRST);
         const uint64_t x0 = (uint64_t)(y0 - (int64_t)aj - kHdr), x1 = x0 + len;
-        RecDesc d;
-        {
-          const uint4* s = reinterpret_cast<const uint4*>(RD + j);
-          uint4* t = reinterpret_cast<uint4*>(&d);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) t[q] = s[q];
-        }
+        const uint8_t* litg = RD[j].lit;  // literal bytes straight from the (cached) descriptor line
+        struct {
+          uint64_t d0;
+          uint32_t l0, f0, f1;
+          bool regular;
+        } d;
+        d.d0 = (uint64_t)rv[0].x | ((uint64_t)rv[0].y << 32);
+        d.l0 = rv[0].z;
+        d.f0 = rv[0].w;
+        d.f1 = rv[1].x;
+        d.regular = (rv[1].y & 0xffffu) != 0;
+        const uint32_t npieces = (rv[1].y >> 16) & 0xffu, psrc = rv[1].y >> 24;
+        const uint32_t plen[6] = {rv[1].z, rv[1].w, rv[2].x, rv[2].y, rv[2].z, rv[2].w};
+        const uint32_t poff[6] = {rv[3].x, rv[3].y, rv[3].z, rv[3].w, rv[4].x, rv[4].y};
         uint64_t pb = 0;
         bool slow = false;
-        for (uint32_t q = 0; q < d.npieces; ++q) {
-          const uint64_t pe = pb + d.plen[q];
+#pragma unroll
+        for (uint32_t q = 0; q < 6; ++q) {
+          if (q >= npieces) break;
+          const uint64_t pe = pb + plen[q];
           const uint64_t s0 = pb > x0 ? pb : x0, s1 = pe < x1 ? pe : x1;
           if (s0 < s1) {
             uint32_t io = d0 + (uint32_t)(s0 - x0);
-            if (!((d.psrc >> q) & 1u)) {
-              for (uint64_t s = s0; s < s1; ++s) img_put(img, io++, d.lit[d.poff[q] + (s - pb)]);
+            if (!((psrc >> q) & 1u)) {
+              for (uint64_t s = s0; s < s1; ++s) img_put(img, io++, litg[poff[q] + (s - pb)]);
             } else {
-              uint64_t z = d.poff[q] + (s0 - pb), l = s1 - s0;
+              uint64_t z = poff[q] + (s0 - pb), l = s1 - s0;
               // irregular source records: walk their fragments
               uint32_t f = d.f0;
               Frag F{};
@@ -769,7 +801,7 @@ __global__ __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4))) void k
               while (l > 0) {
                 uint64_t src, take;
                 if (d.regular) {
-                  src = src_at(d, e.start_off, z, take);
+                  src = src_at(d.d0, d.l0, e.start_off, z, take);
                 } else {
                   const uint64_t in = z - cum;
                   take = F.len - in;
@@ -856,7 +888,7 @@ __global__ __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
         for (int k2 = 0; k2 < 4; ++k2) {
           if (full[k2]) {
-            *reinterpret_cast<uint4*>(&img[c0s[k2] >> 2]) = shift16(v0[k2], v1[k2], (uint32_t)(ss[k2] & 15u));
+            *reinterpret_cast<uint4*>(&img[iw(c0s[k2] >> 2)]) = shift16(v0[k2], v1[k2], (uint32_t)(ss[k2] & 15u));
           } else {
             for (uint32_t b = c0s[k2]; b < c1s[k2]; ++b) img_put(img, b, e.seg[ss[k2] + (b - c0s[k2])]);
           }
@@ -889,11 +921,11 @@ __global__ __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4))) void k
         const int32_t dw = base >> 2;  // arithmetic: negative bases read clamped (masked) words
         const uint32_t sh = (uint32_t)(base & 3);
         uint32_t wv[32];
-        uint32_t prev = dw >= 0 ? img[dw] : 0u;
+        uint32_t prev = dw >= 0 ? img[iw((uint32_t)dw)] : 0u;
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
           const int32_t idx = dw + 1 + i;
-          const uint32_t nx = idx >= 0 ? img[idx] : 0u;
+          const uint32_t nx = idx >= 0 ? img[iw((uint32_t)idx)] : 0u;
           wv[i] = __builtin_amdgcn_alignbyte(nx, prev, sh);
           prev = nx;
         }
@@ -953,9 +985,11 @@ __global__ __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4))) void k
           const uint32_t w0 = ib >> 2;
           uint4 v;
           if (sh == 0) {
-            v = make_uint4(img[w0], img[w0 + 1], img[w0 + 2], img[w0 + 3]);
+            if ((w0 & 3u) == 0) v = *reinterpret_cast<const uint4*>(&img[iw(w0)]);
+            else v = make_uint4(img[iw(w0)], img[iw(w0 + 1)], img[iw(w0 + 2)], img[iw(w0 + 3)]);
           } else {
-            const uint32_t x0 = img[w0], x1 = img[w0 + 1], x2 = img[w0 + 2], x3 = img[w0 + 3], x4 = img[w0 + 4];
+            const uint32_t x0 = img[iw(w0)], x1 = img[iw(w0 + 1)], x2 = img[iw(w0 + 2)], x3 = img[iw(w0 + 3)],
+                           x4 = img[iw(w0 + 4)];
             v = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
                            __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
           }
@@ -1090,19 +1124,38 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     k_recdesc<PM_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, rdp);
     k_pack<PM_DST><<<pgrid(s.blk_cap_w), kPT, 0, st>>>(A);
     pr.end(K_ENC_PACK, st, ev0);
-    k_hint_sizes<<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.hsz);
-    scan(s.hsz, 0, 1, s.hda);
-    layout(1, s.hda, L.p.hint_pos, desc_h, s.blk_cap_h);
-    A.da = s.hda;
-    A.desc = desc_h;
-    A.lay = 1;
-    A.out = L.out.hint;
-    A.pos = L.p.hint_pos;
-    A.cap = L.out.hint_cap;
-    pr.begin(K_ENC_PACK_HINT, st, ev0);
-    k_recdesc<PM_HINT_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag, rdp);
-    k_pack<PM_HINT_DST><<<pgrid(s.blk_cap_h), kPT, 0, st>>>(A);
-    pr.end(K_ENC_PACK_HINT, st, ev0);
+    // the hint WAL only needs the dst offsets: its layout and pack run on the auxiliary stream,
+    // beside the dst pack
+    hipStream_t sh = L.aux ? L.aux : st;
+    if (L.aux) {
+      (void)hipEventRecord(L.ev_fork, st);
+      (void)hipStreamWaitEvent(sh, L.ev_fork, 0);
+    }
+    k_hint_sizes<<<rgrid, 256, 0, sh>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.hsz);
+    {
+      hipStream_t keep = st;
+      st = sh;
+      scan(s.hsz, 0, 1, s.hda);
+      layout(1, s.hda, L.p.hint_pos, desc_h, s.blk_cap_h);
+      st = keep;
+    }
+    PackArgs H = A;
+    H.da = s.hda;
+    H.rd = s.recdesc_h;
+    H.desc = desc_h;
+    H.lay = 1;
+    H.out = L.out.hint;
+    H.pos = L.p.hint_pos;
+    H.cap = L.out.hint_cap;
+    pr.begin(K_ENC_PACK_HINT, sh, ev0);
+    k_recdesc<PM_HINT_DST><<<rgrid, 256, 0, sh>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag,
+                                                  static_cast<RecDesc*>(s.recdesc_h));
+    k_pack<PM_HINT_DST><<<pgrid(s.blk_cap_h), kPT, 0, sh>>>(H);
+    pr.end(K_ENC_PACK_HINT, sh, ev0);
+    if (L.aux) {
+      (void)hipEventRecord(L.ev_join, sh);
+      (void)hipStreamWaitEvent(st, L.ev_join, 0);
+    }
   } else {
     pr.begin(K_ENC_SCAN, st, ev0);
     scan(s.sz, 1, 0, s.hda);

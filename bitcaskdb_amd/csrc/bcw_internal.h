@@ -122,7 +122,8 @@ struct EncScratch {
   uint32_t* evb = nullptr;    // [rows/win+2] governing event per k_events window
   void* desc_w = nullptr;     // [blk_cap_w] block descriptors (dst WAL)
   void* desc_h = nullptr;     // [blk_cap_h] (hint WAL)
-  void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc -> k_pack)
+  void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc -> k_pack), dst WAL
+  void* recdesc_h = nullptr;  // [rows] the same for the hint WAL (packed beside the dst WAL)
   uint64_t* emisc = nullptr;  // [64] counters
 };
 
@@ -139,6 +140,8 @@ struct EncLaunch {
   const uint32_t* crc_ops;
   const uint32_t* initc;
   int num_cus;
+  hipStream_t aux;            // second stream of the context (the hint WAL of a compaction), or null
+  hipEvent_t ev_fork, ev_join;
 };
 
 hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t stream, Prof* prof);
