@@ -322,38 +322,52 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
     nev = 2;
     rho = kL % kM;
   }
-  auto load_window = [&](uint64_t base, int buf, uint32_t t0, uint32_t nt) {
-    constexpr int kB = 8;  // loads in flight per thread before the LDS writes
-    for (uint32_t i0 = t0; i0 < (uint32_t)kEvWin; i0 += kB * nt) {
-      uint64_t av[kB];
+  // loader waves (1..15) hold the window after next in registers: its loads are in flight for a
+  // whole window of scanning before they are written to LDS
+  constexpr int kLd = (kEvWin + kEvThreads - 64 - 1) / (kEvThreads - 64);  // slots per loader thread
+  const uint32_t lt = tid - 64;                                            // loader thread index
+  uint64_t pf[kLd];
+  auto prefetch = [&](uint64_t base) {
 #pragma unroll
-      for (int k = 0; k < kB; ++k) {
-        const uint32_t i = i0 + (uint32_t)k * nt;
-        const uint64_t idx = base + i;
-        av[k] = (i < (uint32_t)kEvWin && idx < N) ? da[idx] : 0;
-      }
+    for (int k = 0; k < kLd; ++k) {
+      const uint32_t i = lt + (uint32_t)k * (kEvThreads - 64);
+      const uint64_t idx = base + i;
+      pf[k] = (i < (uint32_t)kEvWin && idx < N) ? da[idx] : 0;
+    }
+  };
+  auto commit = [&](int buf, uint64_t wb) {
 #pragma unroll
-      for (int k = 0; k < kB; ++k) {
-        const uint32_t i = i0 + (uint32_t)k * nt;
-        if (i < (uint32_t)kEvWin) {
-          s_a[buf][i] = av[k];
-          s_r[buf][i] = (uint16_t)(av[k] % kM);
-        }
+    for (int k = 0; k < kLd; ++k) {
+      const uint32_t i = lt + (uint32_t)k * (kEvThreads - 64);
+      if (i < (uint32_t)kEvWin) {
+        const uint64_t idx = wb + i;
+        s_a[buf][i] = pf[k];
+        s_r[buf][i] = idx < N ? (uint16_t)(pf[k] % kM) : (uint16_t)0xffffu;
       }
     }
   };
-  if (N > 0) load_window(0, 0, tid, kEvThreads);
+  // window 0 straight into LDS (all threads), window 1 into the loaders' registers
+  for (uint32_t i = tid; i < (uint32_t)kEvWin; i += kEvThreads) {
+    const uint64_t av = i < N ? da[i] : 0;
+    s_a[0][i] = av;
+    s_r[0][i] = i < N ? (uint16_t)(av % kM) : (uint16_t)0xffffu;
+  }
+  if (wave != 0) prefetch(kEvWin);
   __syncthreads();
   const uint64_t nwin = (N + kEvWin - 1) / kEvWin;
   for (uint64_t w = 0; w < nwin; ++w) {
     const int buf = (int)(w & 1);
     const uint64_t base = w * kEvWin;
     if (wave != 0) {
-      if (w + 1 < nwin) load_window(base + kEvWin, buf ^ 1, tid - 64, kEvThreads - 64);
+      if (w + 1 < nwin) commit(buf ^ 1, base + kEvWin);
+      if (w + 2 < nwin) prefetch(base + 2 * (uint64_t)kEvWin);
     } else {
       if (lane == 0) evb[w] = nev - 1;
       const uint32_t nrec = (uint32_t)((N - base) < (uint64_t)kEvWin ? (N - base) : (uint64_t)kEvWin);
-      // records of group g: [512 g, 512 g + 512); lane l tests [512 g + 8 l, +8)
+      // records of group g: [512 g, 512 g + 512); lane l tests [512 g + 8 l, +8). Residues past the
+      // window's records are 0xffff and never match. Record i is an event iff a_i mod M lies in
+      // [rho - 6, rho] (mod M): one subtract and one compare per record, the candidate masks of the
+      // 8 slots are ballots combined with scalar ops.
       for (uint32_t g0 = 0; g0 < nrec; g0 += 512) {
         const uint32_t i0 = g0 + 8 * lane;
         uint32_t rr[8];
@@ -362,23 +376,27 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
           rr[0] = v.x & 0xffffu; rr[1] = v.x >> 16; rr[2] = v.y & 0xffffu; rr[3] = v.y >> 16;
           rr[4] = v.z & 0xffffu; rr[5] = v.z >> 16; rr[6] = v.w & 0xffffu; rr[7] = v.w >> 16;
         }
-        int32_t last = (base == 0) ? 0 : -1;  // record 0 is never an event of the virtual block
-        last -= (int32_t)g0;                  // in group-relative indices
-        for (;;) {
-          uint32_t first = 0xffffffffu;  // this lane's first candidate after `last` (group-relative)
+        uint64_t elig[8];  // slot k of lane l still eligible (after the last event of this group)
 #pragma unroll
-          for (int k = 7; k >= 0; --k) {
-            const int32_t q = 8 * (int32_t)lane + k;
-            if (g0 + (uint32_t)q < nrec && q > last) {
-              int32_t d = (int32_t)rho - (int32_t)rr[k];
-              if (d < 0) d += kM;
-              if (d <= 6) first = (uint32_t)q;
-            }
+        for (int k = 0; k < 8; ++k) elig[k] = ~0ull;
+        if (base == 0 && g0 == 0) elig[0] = ~1ull;  // record 0 is never an event of the virtual block
+        for (;;) {
+          const uint32_t lo = rho >= 6 ? rho - 6 : rho + kM - 6;
+          const bool wrap = rho < 6;
+          uint64_t c[8], any = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const bool hit = (rr[k] - lo) <= 6u || (wrap && rr[k] <= rho);
+            c[k] = __ballot(hit) & elig[k];
+            any |= c[k];
           }
-          const uint64_t m = __ballot(first != 0xffffffffu);
-          if (!m) break;
-          const uint32_t owner = (uint32_t)__builtin_ctzll(m);
-          const uint32_t q = __builtin_amdgcn_readlane(first, owner);  // lowest lane holds the lowest index
+          if (!any) break;
+          const uint32_t L = (uint32_t)__builtin_ctzll(any);
+          uint32_t K = 7;
+#pragma unroll
+          for (int k = 6; k >= 0; --k)
+            if ((c[k] >> L) & 1ull) K = (uint32_t)k;
+          const uint32_t q = 8 * L + K;  // group-relative index of the event record
           const uint64_t ai = s_a[buf][g0 + q];
           const uint32_t ri = (uint32_t)s_r[buf][g0 + q];
           int32_t d = (int32_t)rho - (int32_t)ri;
@@ -390,7 +408,10 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
           if (lane == 0) ev[nev] = {kb, ya, (uint32_t)(base + g0 + q), (uint32_t)d};
           ++nev;
           rho = (ri + kHdr) % kM;
-          last = (int32_t)q;
+          // only records after q stay eligible: lanes above L, and slots above K of lane L
+          const uint64_t above = L == 63 ? 0ull : (~0ull << (L + 1));
+#pragma unroll
+          for (int k = 0; k < 8; ++k) elig[k] &= above | ((uint32_t)k > K ? (1ull << L) : 0ull);
         }
       }
     }
