@@ -7,7 +7,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbcw.so")
+# BCW_LIB: an alternative build of the same library (A/B measurements of kernel variants only)
+LIB_PATH = os.environ.get("BCW_LIB") or os.path.join(_HERE, "libbcw.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "bcw.h")
 
 u8p = C.POINTER(C.c_uint8)

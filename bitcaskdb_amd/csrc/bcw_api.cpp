@@ -410,7 +410,7 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
 }
 
 static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_records", "k_enc_prep", "k_enc_scan", "k_events",
-                                          "k_pack", "k_pack_hint"};
+                                          "k_pack", "k_pack_hint", "k_events_hint"};
 
 int bcw_ctx_set_profiling(bcw_ctx* c, int mask) {
   if (!c) return BCW_E_INVAL;

@@ -40,6 +40,7 @@ constexpr uint32_t kL = kBlock;           // 32768
 constexpr uint32_t kM = kBlock - kHdr;    // 32761
 constexpr int kTileItems = 4096;          // scan tile: 256 threads x 16 items
 constexpr int kEvThreads = 1024;
+constexpr int kEvPer = 4;
 constexpr int kEvWin = 4096;  // records per k_events step (LDS double buffer: 2 x 40 KiB)
 constexpr int kJobCap = 1024;
 constexpr int kJobsPerRec = 8;
@@ -290,9 +291,11 @@ struct Ev {
   uint32_t pad;
 };
 
-// One workgroup: wave 0 scans a window of kEvWin records per step out of LDS (8 residues per lane
-// per ballot, events resolved in the wave without barriers), while waves 1..15 load the next
-// window's y-coordinates into the other LDS buffer. One barrier per window.
+// One workgroup of kEvThreads, kEvWin = kEvThreads * kEvPer records per window in registers. A round:
+// every thread tests its records after the last event against rho, the wave minima meet in LDS, and
+// the owner of the first hit records the event and advances the scan state. Rounds per window =
+// events in it + 1. (Measured against a barrier-free scanner wave fed by loader waves and against a
+// one-barrier-per-round replay from LDS: both slower)
 __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restrict__ da, uint64_t* __restrict__ emisc,
                                                         int lay, uint64_t q0, Ev* __restrict__ ev,
                                                         uint32_t* __restrict__ evb) {
@@ -301,123 +304,87 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
   const uint64_t AN = X[0];
   const int64_t U = (int64_t)(q0 % kL);
   const uint64_t b0 = q0 / kL;
-  __shared__ __attribute__((aligned(16))) uint64_t s_a[2][kEvWin];
-  __shared__ __attribute__((aligned(16))) uint16_t s_r[2][kEvWin];
   __shared__ int64_t s_ya;
   __shared__ uint64_t s_kb;
-  __shared__ uint32_t s_nev;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // scanner state (wave 0, wave-uniform)
-  int64_t ya = -U;
-  uint64_t kb = b0;
-  uint32_t nev = 1;
-  uint32_t rho = (uint32_t)((kL - U) % kM);  // the virtual block ends at y = L - U
-  if (tid == 0) {
+  __shared__ uint32_t s_rho, s_nev, s_best;
+  __shared__ uint32_t s_wmin[kEvThreads / 64];
+  if (threadIdx.x == 0) {
     ev[0] = {b0, -U, 0xffffffffu, 0};
-    if (N > 0 && kL - U < (int64_t)kHdr) ev[1] = {b0 + 1, 0, 0u, (uint32_t)(kL - U)};
-  }
-  if (N > 0 && kL - U < (int64_t)kHdr) {  // record 0's header does not fit: pad, event at record 0
-    ya = 0;
-    kb = b0 + 1;
-    nev = 2;
-    rho = kL % kM;
-  }
-  // loader waves (1..15) hold the window after next in registers: its loads are in flight for a
-  // whole window of scanning before they are written to LDS
-  constexpr int kLd = (kEvWin + kEvThreads - 64 - 1) / (kEvThreads - 64);  // slots per loader thread
-  const uint32_t lt = tid - 64;                                            // loader thread index
-  uint64_t pf[kLd];
-  auto prefetch = [&](uint64_t base) {
-#pragma unroll
-    for (int k = 0; k < kLd; ++k) {
-      const uint32_t i = lt + (uint32_t)k * (kEvThreads - 64);
-      const uint64_t idx = base + i;
-      pf[k] = (i < (uint32_t)kEvWin && idx < N) ? da[idx] : 0;
+    int64_t ya = -U;
+    uint64_t kb = b0;
+    uint32_t nev = 1;
+    uint32_t rho = (uint32_t)((kL - U) % kM);  // the virtual block ends at y = L - U
+    if (N > 0 && kL - U < (int64_t)kHdr) {    // record 0's header does not fit: pad, event at record 0
+      ev[1] = {b0 + 1, 0, 0u, (uint32_t)(kL - U)};
+      ya = 0;
+      kb = b0 + 1;
+      nev = 2;
+      rho = kL % kM;
     }
-  };
-  auto commit = [&](int buf, uint64_t wb) {
-#pragma unroll
-    for (int k = 0; k < kLd; ++k) {
-      const uint32_t i = lt + (uint32_t)k * (kEvThreads - 64);
-      if (i < (uint32_t)kEvWin) {
-        const uint64_t idx = wb + i;
-        s_a[buf][i] = pf[k];
-        s_r[buf][i] = idx < N ? (uint16_t)(pf[k] % kM) : (uint16_t)0xffffu;
-      }
-    }
-  };
-  // window 0 straight into LDS (all threads), window 1 into the loaders' registers
-  for (uint32_t i = tid; i < (uint32_t)kEvWin; i += kEvThreads) {
-    const uint64_t av = i < N ? da[i] : 0;
-    s_a[0][i] = av;
-    s_r[0][i] = i < N ? (uint16_t)(av % kM) : (uint16_t)0xffffu;
+    s_ya = ya; s_kb = kb; s_rho = rho; s_nev = nev;
   }
-  if (wave != 0) prefetch(kEvWin);
   __syncthreads();
-  const uint64_t nwin = (N + kEvWin - 1) / kEvWin;
-  for (uint64_t w = 0; w < nwin; ++w) {
-    const int buf = (int)(w & 1);
-    const uint64_t base = w * kEvWin;
-    if (wave != 0) {
-      if (w + 1 < nwin) commit(buf ^ 1, base + kEvWin);
-      if (w + 2 < nwin) prefetch(base + 2 * (uint64_t)kEvWin);
-    } else {
-      if (lane == 0) evb[w] = nev - 1;
-      const uint32_t nrec = (uint32_t)((N - base) < (uint64_t)kEvWin ? (N - base) : (uint64_t)kEvWin);
-      // records of group g: [512 g, 512 g + 512); lane l tests [512 g + 8 l, +8). Residues past the
-      // window's records are 0xffff and never match. Record i is an event iff a_i mod M lies in
-      // [rho - 6, rho] (mod M): one subtract and one compare per record, the candidate masks of the
-      // 8 slots are ballots combined with scalar ops.
-      for (uint32_t g0 = 0; g0 < nrec; g0 += 512) {
-        const uint32_t i0 = g0 + 8 * lane;
-        uint32_t rr[8];
-        {
-          const uint4 v = *reinterpret_cast<const uint4*>(&s_r[buf][i0]);
-          rr[0] = v.x & 0xffffu; rr[1] = v.x >> 16; rr[2] = v.y & 0xffffu; rr[3] = v.y >> 16;
-          rr[4] = v.z & 0xffffu; rr[5] = v.z >> 16; rr[6] = v.w & 0xffffu; rr[7] = v.w >> 16;
-        }
-        uint64_t elig[8];  // slot k of lane l still eligible (after the last event of this group)
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint64_t base = 0; base < N; base += kEvWin) {
+    if (threadIdx.x == 0) evb[base / kEvWin] = s_nev - 1;
+    uint64_t a[kEvPer];
+    uint32_t r[kEvPer];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) elig[k] = ~0ull;
-        if (base == 0 && g0 == 0) elig[0] = ~1ull;  // record 0 is never an event of the virtual block
-        for (;;) {
-          const uint32_t lo = rho >= 6 ? rho - 6 : rho + kM - 6;
-          const bool wrap = rho < 6;
-          uint64_t c[8], any = 0;
+    for (int k = 0; k < kEvPer; ++k) {
+      const uint64_t idx = base + (uint64_t)k * kEvThreads + threadIdx.x;
+      a[k] = idx < N ? da[idx] : 0;
+      r[k] = (uint32_t)(a[k] % kM);
+    }
+    // record 0 is never tested against the virtual event (its header is in block b0 or it is ev[1])
+    int last = (base == 0) ? 0 : -1;
+    uint32_t rho = s_rho;
+    for (;;) {
+      uint32_t best = 0xffffffffu;
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const bool hit = (rr[k] - lo) <= 6u || (wrap && rr[k] <= rho);
-            c[k] = __ballot(hit) & elig[k];
-            any |= c[k];
-          }
-          if (!any) break;
-          const uint32_t L = (uint32_t)__builtin_ctzll(any);
-          uint32_t K = 7;
-#pragma unroll
-          for (int k = 6; k >= 0; --k)
-            if ((c[k] >> L) & 1ull) K = (uint32_t)k;
-          const uint32_t q = 8 * L + K;  // group-relative index of the event record
-          const uint64_t ai = s_a[buf][g0 + q];
-          const uint32_t ri = (uint32_t)s_r[buf][g0 + q];
-          int32_t d = (int32_t)rho - (int32_t)ri;
+      for (int k = kEvPer - 1; k >= 0; --k) {
+        const uint32_t q = (uint32_t)k * kEvThreads + threadIdx.x;
+        const uint64_t idx = base + q;
+        if (idx < N && (int)q > last) {
+          int32_t d = (int32_t)rho - (int32_t)r[k];
           if (d < 0) d += kM;
-          const int64_t E = (int64_t)ai + d;                      // block end that hits the header
-          const uint64_t mm = (uint64_t)(E - ya - (int64_t)kL) / kM;  // blocks after the event block
-          kb = kb + mm + 1;
-          ya = (int64_t)ai;
-          if (lane == 0) ev[nev] = {kb, ya, (uint32_t)(base + g0 + q), (uint32_t)d};
-          ++nev;
-          rho = (ri + kHdr) % kM;
-          // only records after q stay eligible: lanes above L, and slots above K of lane L
-          const uint64_t above = L == 63 ? 0ull : (~0ull << (L + 1));
-#pragma unroll
-          for (int k = 0; k < 8; ++k) elig[k] &= above | ((uint32_t)k > K ? (1ull << L) : 0ull);
+          if (d <= 6) best = q;
         }
       }
+      for (int d = 32; d >= 1; d >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, d, 64));
+      if (lane == 0) s_wmin[wave] = best;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t m = 0xffffffffu;
+        for (int w = 0; w < kEvThreads / 64; ++w) m = min(m, s_wmin[w]);
+        s_best = m;
+      }
+      __syncthreads();
+      const uint32_t b = s_best;
+      if (b == 0xffffffffu) break;
+      if (threadIdx.x == (b & (kEvThreads - 1))) {  // the owner records the event
+        const int k = (int)(b / kEvThreads);
+        uint64_t ai = a[0];
+        uint32_t ri = r[0];
+#pragma unroll
+        for (int kk = 1; kk < kEvPer; ++kk) if (kk == k) { ai = a[kk]; ri = r[kk]; }
+        int32_t d = (int32_t)s_rho - (int32_t)ri;
+        if (d < 0) d += kM;
+        const int64_t E = (int64_t)ai + d;                         // block end that hits the header
+        const uint64_t m = (uint64_t)(E - s_ya - (int64_t)kL) / kM;  // blocks after the event block
+        const uint64_t kb = s_kb + m + 1;
+        ev[s_nev] = {kb, (int64_t)ai, (uint32_t)(base + b), (uint32_t)d};
+        s_nev = s_nev + 1;
+        s_kb = kb;
+        s_ya = (int64_t)ai;
+        s_rho = (ri + kHdr) % kM;
+      }
+      __syncthreads();
+      rho = s_rho;
+      last = (int)b;
     }
-    __syncthreads();
   }
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
+    const uint32_t nev = s_nev;
     X[1] = nev;
     X[4] = b0;
     X[5] = (uint64_t)U;
@@ -425,6 +392,8 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
       X[2] = b0 - 1;  // no blocks
       X[3] = 40 + q0;
     } else {
+      const int64_t ya = s_ya;
+      const uint64_t kb = s_kb;
       // the block whose end E_k >= A_N first: E_kb = ya + L, E_{kb+m} = ya + L + m M
       const int64_t over = (int64_t)AN - ya - (int64_t)kL;
       const uint64_t m = over > 0 ? ((uint64_t)over + kM - 1) / kM : 0;
@@ -435,7 +404,6 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
       X[3] = 40 + ke * kL + kHdr * c + (uint64_t)((int64_t)AN - Y);
     }
   }
-  (void)s_ya; (void)s_kb; (void)s_nev;
 }
 
 // per-block descriptor for k_pack
@@ -1110,9 +1078,10 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     k_tile_scatter<<<ntiles, 256, 0, st>>>(sz, s.emisc, over_rows, tiles, s.dsrc, da);
   };
   auto layout = [&](int lay, const uint64_t* da, uint64_t pos, BlkDesc* desc, uint64_t desc_cap) {
-    pr.begin(K_ENC_EVENTS, st, ev0);
+    const int kid = lay == 1 ? K_ENC_EVENTS_HINT : K_ENC_EVENTS;
+    pr.begin(kid, st, ev0);
     k_events<<<1, kEvThreads, 0, st>>>(da, s.emisc, lay, pos - 40, evs, s.evb);
-    pr.end(K_ENC_EVENTS, st, ev0);
+    pr.end(kid, st, ev0);
     k_blkdesc<<<(uint32_t)((desc_cap + 255) / 256), 256, 0, st>>>(da, s.emisc, lay, evs, desc, desc_cap);
   };
   PackArgs A{};

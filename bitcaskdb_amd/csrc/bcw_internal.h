@@ -78,7 +78,7 @@ struct Scratch {
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
 // stream around every kernel of the pipeline.
 enum KernelId { K_CHASE = 0, K_CRC, K_RECORDS, K_ENC_PREP, K_ENC_SCAN, K_ENC_EVENTS, K_ENC_PACK, K_ENC_PACK_HINT,
-                K_NUM };
+                K_ENC_EVENTS_HINT, K_NUM };
 struct Prof {
   uint32_t mask = 0;  // bit k: time kernel id k
   struct Mark { int kid; hipEvent_t a, b; };
