@@ -631,21 +631,17 @@ __device__ __forceinline__ void img_put(uint32_t* img, uint32_t b, uint8_t v) {
 
 // 16 source bytes at an arbitrary address from two aligned 16 B loads (caller checks bounds)
 __device__ __forceinline__ uint4 shift16(uint4 v0, uint4 v1, uint32_t sh) {
-  if (sh == 0) return v0;
-  const uint32_t W[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-  const uint32_t w = sh >> 2, b = sh & 3u;
-  uint32_t o[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {  // o[k] = W[k + w] by two selects (static indices: no scratch)
-    const uint32_t lo = (w & 1u) ? W[k + 1] : W[k];
-    const uint32_t hi = (w & 1u) ? W[(k + 3) & 7] : W[(k + 2) & 7];
-    o[k] = (w & 2u) ? hi : lo;
-  }
+  // named scalars and two select stages: an array indexed by w would be lowered to a scratch round trip
+  const bool s2 = (sh & 8u) != 0, s1 = (sh & 4u) != 0;
+  const uint32_t b0 = s2 ? v0.z : v0.x, b1 = s2 ? v0.w : v0.y, b2 = s2 ? v1.x : v0.z, b3 = s2 ? v1.y : v0.w,
+                 b4 = s2 ? v1.z : v1.x, b5 = s2 ? v1.w : v1.y;
+  const uint32_t c0 = s1 ? b1 : b0, c1 = s1 ? b2 : b1, c2 = s1 ? b3 : b2, c3 = s1 ? b4 : b3, c4 = s1 ? b5 : b4;
+  const uint32_t b = sh & 3u;
   uint4 r;
-  r.x = __builtin_amdgcn_alignbyte(o[1], o[0], b);
-  r.y = __builtin_amdgcn_alignbyte(o[2], o[1], b);
-  r.z = __builtin_amdgcn_alignbyte(o[3], o[2], b);
-  r.w = __builtin_amdgcn_alignbyte(o[4], o[3], b);
+  r.x = __builtin_amdgcn_alignbyte(c1, c0, b);
+  r.y = __builtin_amdgcn_alignbyte(c2, c1, b);
+  r.z = __builtin_amdgcn_alignbyte(c3, c2, b);
+  r.w = __builtin_amdgcn_alignbyte(c4, c3, b);
   return r;
 }
 
