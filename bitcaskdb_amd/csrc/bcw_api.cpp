@@ -69,17 +69,49 @@ void build_lane_tables(uint32_t* fwd, uint32_t* carry, uint32_t* half) {
     for (uint32_t n = 0; n < 16; ++n) half[i * 16 + n] = apply_basis(h64, n << (4 * i));
 }
 
-// k_pack shift operators: ops[m] = A_{8*128*m}, ops[16 + m] = A_{8*2048*m} (m < 16), nibble images
+// basis images of the inverse of a (bijective) GF(2)-linear map given by its basis images
+static void invert_basis(const uint32_t* img, uint32_t* inv) {
+  uint32_t out[32], in[32];
+  for (int i = 0; i < 32; ++i) { out[i] = img[i]; in[i] = 1u << i; }
+  for (int bit = 0; bit < 32; ++bit) {
+    int p = bit;
+    while (p < 32 && !((out[p] >> bit) & 1u)) ++p;  // x^8n mod P is invertible: a pivot always exists
+    std::swap(out[bit], out[p]);
+    std::swap(in[bit], in[p]);
+    for (int r = 0; r < 32; ++r)
+      if (r != bit && ((out[r] >> bit) & 1u)) { out[r] ^= out[bit]; in[r] ^= in[bit]; }
+  }
+  for (int bit = 0; bit < 32; ++bit) inv[bit] = in[bit];
+}
+
+static void nibble_image(const uint32_t* img, uint32_t* t) {
+  for (int i = 0; i < 8; ++i)
+    for (uint32_t n = 0; n < 16; ++n) t[i * 16 + n] = apply_basis(img, n << (4 * i));
+}
+
+// encode shift operators (nibble images, 128 words each):
+//   k_pack:  [m] = A_{8*128*m}, [16 + m] = A_{8*2048*m} (m < 16)
+//   k_write (from kEncWrOps): [h] = A_{8*16*h}, [8 + g] = A_{8*128*g} (h, g < 8), [16] = A_{8*1024},
+//            [17 + t] = A_{8t}^-1 (t < 16)
 static void build_enc_ops(uint32_t* ops) {
   uint32_t t0[256];
   byte_table(t0);
+  uint32_t img[32], inv[32];
   for (int h = 0; h < 2; ++h)
     for (int m = 0; m < 16; ++m) {
-      uint32_t img[32];
       shift_basis(t0, (uint64_t)(h ? 2048 : 128) * m, img);
-      for (int i = 0; i < 8; ++i)
-        for (uint32_t n = 0; n < 16; ++n) ops[((h * 16 + m) * 8 + i) * 16 + n] = apply_basis(img, n << (4 * i));
+      nibble_image(img, ops + (h * 16 + m) * 128);
     }
+  uint32_t* w = ops + kEncWrOps;
+  for (int h = 0; h < 8; ++h) { shift_basis(t0, 16ull * h, img); nibble_image(img, w + h * 128); }
+  for (int g = 0; g < 8; ++g) { shift_basis(t0, 128ull * g, img); nibble_image(img, w + (8 + g) * 128); }
+  shift_basis(t0, 1024, img);
+  nibble_image(img, w + 16 * 128);
+  for (int t = 0; t < 16; ++t) {
+    shift_basis(t0, (uint64_t)t, img);
+    invert_basis(img, inv);
+    nibble_image(inv, w + (17 + t) * 128);
+  }
 }
 
 // initc[L] = A_{8L}(0xFFFFFFFF): the contribution of the CRC init value after L data bytes
@@ -118,8 +150,6 @@ struct bcw_ctx {
   int num_cus = 256;
   hipStream_t own = nullptr;
   hipStream_t cur = nullptr;
-  hipStream_t aux = nullptr;  // encode: the hint WAL's layout + pack beside the dst pack
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   Tables tabs{};
   Scratch s{};
   EncScratch es{};
@@ -223,18 +253,12 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return BCW_E_HIP; }
-  if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
-    bcw_ctx_destroy(c);
-    return BCW_E_HIP;
-  }
   c->cur = c->own;
   std::vector<uint32_t> slice(512), fwd(64 * 128), carry(128), half(128), initc(kBlock + 1);
   build_slice_tables(slice.data());
   build_lane_tables(fwd.data(), carry.data(), half.data());
   build_initc(initc.data());
-  std::vector<uint32_t> enc_ops(2 * 16 * 128);
+  std::vector<uint32_t> enc_ops(kEncOpsWords);
   build_enc_ops(enc_ops.data());
   std::vector<uint32_t> image(kLdsImage);
   for (int e = 0; e < 256; ++e)
@@ -280,8 +304,8 @@ static void free_scratch(Scratch& s) {
 }
 
 static void free_enc_scratch(EncScratch& e) {
-  void* ptrs[] = {e.sz,    e.mflag,  e.dsrc,   e.da,      e.hda,    e.hsz,       e.dpos,
-                  e.tiles, e.ev,     e.evb,    e.desc_w,  e.desc_h, e.recdesc,   e.recdesc_h, e.emisc};
+  void* ptrs[] = {e.sz,    e.mflag, e.dsrc, e.da,      e.hda,       e.hsz,  e.dpos,
+                  e.hpos,  e.tiles, e.ev,   e.evb,     e.recdesc,   e.recdesc_h, e.emisc};
   for (void* q : ptrs) (void)hipFree(q);
   e = EncScratch{};
 }
@@ -307,9 +331,6 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   (void)hipFree(c->d_result);
   for (auto& m : c->prof.marks) { (void)hipEventDestroy(m.a); (void)hipEventDestroy(m.b); }
   for (auto e : c->prof.pool) (void)hipEventDestroy(e);
-  if (c->aux) { (void)hipStreamSynchronize(c->aux); (void)hipStreamDestroy(c->aux); }
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
   return BCW_OK;
@@ -410,7 +431,7 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
 }
 
 static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_records", "k_enc_prep", "k_enc_scan", "k_events",
-                                          "k_pack", "k_pack_hint", "k_events_hint"};
+                                          "k_write", "k_hint_layout", "k_events_hint"};
 
 int bcw_ctx_set_profiling(bcw_ctx* c, int mask) {
   if (!c) return BCW_E_INVAL;
@@ -543,39 +564,27 @@ int bcw_decode_segment(bcw_ctx* c, const uint8_t* h_seg, const bcw_decode_params
 
 
 // ---- encode (bcw_encode.hip) ----
-static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows, uint64_t blk_w, uint64_t blk_h) {
+static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows) {
   EncScratch& e = c->es;
-  if (rows <= e.rows_cap && blk_w <= e.blk_cap_w && blk_h <= e.blk_cap_h && e.emisc) return BCW_OK;
+  if (rows <= e.rows_cap && e.emisc) return BCW_OK;
   (void)hipStreamSynchronize(c->cur);
   const uint64_t r = std::max(std::max(rows, e.rows_cap), (uint64_t)1);
-  const uint64_t bw = std::max(std::max(blk_w, e.blk_cap_w), (uint64_t)4);
-  const uint64_t bh = std::max(std::max(blk_h, e.blk_cap_h), (uint64_t)4);
   free_enc_scratch(e);
   const uint64_t ntiles = r / enc_tile_items() + 2;
   const uint64_t nwin = r / enc_ev_win() + 2;
   bool ok = hipMalloc(&e.sz, r * 4) == hipSuccess && hipMalloc(&e.mflag, r) == hipSuccess &&
             hipMalloc(&e.dsrc, r * 4) == hipSuccess && hipMalloc(&e.da, (r + 1) * 8) == hipSuccess &&
             hipMalloc(&e.hda, (r + 1) * 8) == hipSuccess && hipMalloc(&e.hsz, r * 4) == hipSuccess &&
-            hipMalloc(&e.dpos, r * 8) == hipSuccess && hipMalloc(&e.tiles, ntiles * enc_sizeof_tile()) == hipSuccess &&
+            hipMalloc(&e.dpos, r * 8) == hipSuccess && hipMalloc(&e.hpos, r * 8) == hipSuccess &&
+            hipMalloc(&e.tiles, ntiles * enc_sizeof_tile()) == hipSuccess &&
             hipMalloc(&e.ev, (r + 2) * enc_sizeof_ev()) == hipSuccess && hipMalloc(&e.evb, nwin * 4) == hipSuccess &&
-            hipMalloc(&e.desc_w, bw * enc_sizeof_desc()) == hipSuccess &&
-            hipMalloc(&e.desc_h, bh * enc_sizeof_desc()) == hipSuccess &&
             hipMalloc(&e.recdesc, r * enc_sizeof_recdesc()) == hipSuccess &&
             hipMalloc(&e.recdesc_h, r * enc_sizeof_recdesc()) == hipSuccess &&
             hipMalloc(&e.emisc, 64 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_enc_scratch(e); return BCW_E_NOMEM; }
   (void)hipMemsetAsync(e.mflag, 0, r, c->cur);
   e.rows_cap = r;
-  e.blk_cap_w = bw;
-  e.blk_cap_h = bh;
   return BCW_OK;
-}
-
-// blocks an append of at most `cap` bytes at file offset `pos` can touch
-static uint64_t blocks_for(uint64_t pos, uint64_t cap) {
-  if (pos < BCW_SUPER_BLOCK_SIZE) return 0;
-  const uint64_t q0 = pos - BCW_SUPER_BLOCK_SIZE;
-  return (q0 + cap) / BCW_BLOCK_SIZE - q0 / BCW_BLOCK_SIZE + 2;
 }
 
 int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_params* p,
@@ -591,9 +600,7 @@ int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_
   if (!c->s.frags) return BCW_E_INVAL;  // no decode on this context yet
   if (t->capacity >= 0xffffff00ull) return BCW_E_INVAL;  // u32 dense record ids
   if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
-  const uint64_t bw = p->mode == BCW_ENC_COMPACT ? blocks_for(p->wal_pos, o->wal_cap) : 0;
-  const uint64_t bh = blocks_for(p->hint_pos, o->hint_cap);
-  int rc = ensure_enc_scratch(c, t->capacity, bw, bh);
+  int rc = ensure_enc_scratch(c, t->capacity);
   if (rc != BCW_OK) return rc;
   EncLaunch L{};
   L.d_src = d_src;
@@ -608,9 +615,6 @@ int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_
   L.crc_ops = c->tabs.enc_ops;
   L.initc = c->tabs.initc;
   L.num_cus = c->num_cus;
-  L.aux = c->aux;
-  L.ev_fork = c->ev_fork;
-  L.ev_join = c->ev_join;
   return launch_encode(L, c->es, c->cur, &c->prof) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 

@@ -9,11 +9,12 @@
 //   k_enc_prep      per source row: keep / Encode errors / re-encoded payload size     record.go:57-138
 //   k_tile_*        3-phase scan: dense list of written records, y-coordinates a_j
 //   k_events        the writer's layout recurrence as an event scan (one workgroup)    wal.go:505-549
-//   k_blkdesc       per output block: start y, continuation flag, pad, first record
 //   k_recoff        per record: the file offset WriteRecord returns                     wal.go:514-516
-//   k_pack<PM>      per output 32 KiB block: LDS image of headers + payload bytes, CRC-32C per
-//                   fragment (utils.go:24-29), streamed out with aligned 16 B stores
-//   (compaction) k_hint_sizes + scan + events + blkdesc + k_pack<hint> for the hint WAL
+//   (compaction) k_hint_sizes + scan + k_events + k_recoff for the hint WAL            hint.go:32-48
+//   k_recdesc_w     per record: payload as literal prefix | source range | literal suffix
+//   k_write         one persistent launch over every record of both WALs: fragments in closed form,
+//                   16 B units copied and folded into each fragment's CRC-32C (utils.go:24-29)
+//   k_write_general the rare records with more literal bytes than the descriptor holds
 //   k_enc_finalize  bcw_encode_result
 //
 // Layout as an event scan. Concatenate the records' (7 B header + payload) units into a y axis:
@@ -26,8 +27,8 @@
 // mod M, so with rho = (next block end) mod M, record i is an event iff (rho - a_i) mod M <= 6,
 // and after it rho = (a_i + 7) mod M. That is a scan with a 15-bit state that is the identity on
 // all but rare records (~7/M of them): k_events runs it over 4096 records per step with a
-// workgroup-wide ballot, and every other quantity (block starts, record offsets, fragment types
-// and lengths) follows in parallel from the event list.
+// workgroup-wide minimum, and every other quantity (record offsets, and from them fragment types,
+// lengths and pads) follows in parallel from the event list.
 #include <algorithm>
 #include <cstdlib>
 
@@ -40,10 +41,8 @@ constexpr uint32_t kL = kBlock;           // 32768
 constexpr uint32_t kM = kBlock - kHdr;    // 32761
 constexpr int kTileItems = 4096;          // scan tile: 256 threads x 16 items
 constexpr int kEvThreads = 1024;
-constexpr int kEvPer = 4;
-constexpr int kEvWin = 4096;  // records per k_events step (LDS double buffer: 2 x 40 KiB)
-constexpr int kJobCap = 1024;
-constexpr int kJobsPerRec = 8;
+constexpr int kEvWin = 4096;  // records per k_events step
+constexpr int kEvPer = kEvWin / kEvThreads;
 
 // emisc slots
 enum {
@@ -406,60 +405,6 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
   }
 }
 
-// per-block descriptor for k_pack
-struct BlkDesc {
-  int64_t Y;       // y of the block start
-  uint32_t first;  // dense record holding Y (or the record whose header is at Y)
-  uint32_t lo;     // first image byte the block writes (U for the first block)
-  uint32_t hi;     // image end (L, or the file end in the last block)
-  uint8_t c;       // continuation header at image 0
-  uint8_t pad;     // zero bytes at the block end
-  uint16_t _r;
-};
-
-__device__ __forceinline__ uint32_t ev_of_block(const Ev* __restrict__ ev, uint32_t nev, uint64_t k) {
-  uint32_t lo = 0, hi = nev;  // largest g with ev[g].blk <= k
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (ev[mid].blk <= k) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-__global__ __launch_bounds__(256) void k_blkdesc(const uint64_t* __restrict__ da, const uint64_t* __restrict__ emisc,
-                                                  int lay, const Ev* __restrict__ ev, BlkDesc* __restrict__ desc,
-                                                  uint64_t desc_cap) {
-  const uint64_t* X = emisc + X_LAY + lay * kLayStride;
-  const uint64_t b0 = X[4], ke = X[2];
-  const uint64_t k = b0 + blockIdx.x * 256ull + threadIdx.x;
-  if (k > ke || ke == b0 - 1 || k - b0 >= desc_cap) return;
-  const uint32_t nev = (uint32_t)X[1];
-  const uint64_t N = emisc[X_NDENSE];
-  const uint32_t g = ev_of_block(ev, nev, k);
-  const Ev e = ev[g];
-  BlkDesc d;
-  if (k == e.blk) {
-    d.Y = e.ya;
-    d.c = 0;
-    d.first = (g == 0) ? 0u : e.rec;
-  } else {
-    d.Y = e.ya + (int64_t)kL + (int64_t)(k - e.blk - 1) * kM;
-    d.c = 1;
-    // the record holding Y: largest j with a_j < Y, between this event's record and the next one's
-    uint64_t lo = (g == 0) ? 0 : e.rec, hi = (g + 1 < nev) ? ev[g + 1].rec : N;
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if ((int64_t)da[mid] < d.Y) lo = mid; else hi = mid;
-    }
-    d.first = (uint32_t)lo;
-  }
-  d.pad = (g + 1 < nev && ev[g + 1].blk == k + 1) ? (uint8_t)ev[g + 1].pad : 0;
-  d.lo = (k == b0) ? (uint32_t)X[5] : 0u;
-  d.hi = (k == ke) ? (uint32_t)(X[3] - 40 - ke * kL) : kL;
-  d._r = 0;
-  desc[k - b0] = d;
-}
-
 // file offset WriteRecord returns for dense record j (wal.go:514-516): its header position
 __device__ __forceinline__ uint64_t rec_phys(const Ev& e, uint32_t g, uint64_t j, uint64_t aj) {
   if (g >= 1 && e.rec == j) return 40 + e.blk * kL;
@@ -540,95 +485,6 @@ __device__ void prog_hint(const EncDev& e, uint64_t i, uint64_t off, uint64_t si
 
 enum { PM_DST = 0, PM_HINT_DST = 1, PM_HINT_SRC = 2 };
 
-// CRC-32C helpers: raw (init 0, no final xor) byte update; shift operators as nibble tables
-__device__ __forceinline__ uint32_t op_apply(const uint32_t* __restrict__ op, uint32_t x) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r ^= op[i * 16 + ((x >> (4 * i)) & 15u)];
-  return r;
-}
-
-struct PackArgs {
-  EncDev e;
-  const uint64_t* da;       // this layout's y-coordinates (dense, N+1)
-  const void* rd;           // RecDesc per dense record (k_recdesc)
-  const BlkDesc* desc;
-  const uint64_t* emisc;
-  int lay;
-  uint8_t* out;
-  uint64_t pos, cap;        // file offset of out[0]; out capacity
-  const uint32_t* crc_ops;  // [2][16][8][16]: A_{8*128*m}, A_{8*2048*m}, m < 16
-  const uint32_t* initc;    // A_{8L}(0xFFFFFFFF)
-  uint32_t abl;             // ablation bits for measurements only (0 in the product): 1 no CRC, 2 no copy, 8 no store
-};
-
-// Per written record: its payload as up to 6 pieces (literal bytes or ranges of the source payload)
-// and the source payload's placement in the source file. Built once per record by k_recdesc, read
-// by the one or two k_pack workgroups whose blocks hold the record.
-struct RecDesc {
-  uint64_t d0;       // file offset of the data of the source payload's first fragment
-  uint32_t l0;       // its length
-  uint32_t f0, f1;   // source fragments (irregular records are walked)
-  uint16_t regular;  // fragments after the first are whole blocks' data: closed-form placement
-  uint8_t npieces, psrc;  // psrc bit q: piece q is a source range
-  uint32_t plen[6];
-  uint32_t poff[6];  // source payload offset (source piece) or offset into lit
-  uint8_t lit[48];
-  uint64_t _pad;
-};
-static_assert(sizeof(RecDesc) == 128, "RecDesc layout");
-
-template <int PM>
-__global__ __launch_bounds__(256) void k_recdesc(EncDev e, const uint64_t* __restrict__ emisc,
-                                                  const uint32_t* __restrict__ dsrc, const uint64_t* __restrict__ dst_da,
-                                                  const uint64_t* __restrict__ dpos, const uint8_t* __restrict__ mflag,
-                                                  RecDesc* __restrict__ rd) {
-  const uint64_t j = blockIdx.x * 256ull + threadIdx.x;
-  if (j >= emisc[X_NDENSE]) return;
-  const uint64_t row = dsrc[j];
-  Prog p;
-  if (PM == PM_DST) prog_record(e, row, mflag[row] != 0, p);
-  else if (PM == PM_HINT_DST) prog_hint(e, row, dpos[j], dst_da[j + 1] - dst_da[j] - kHdr, p);
-  else prog_hint(e, row, e.t.foff[row] - kHdr, e.t.size[row], p);
-  const SrcRec sr = src_rec(e.t, e.frags, row);
-  const Frag F0 = e.frags[sr.f0];
-  RecDesc d;
-  d.d0 = frag_file(F0, e.start_off);
-  d.l0 = F0.len;
-  d.f0 = sr.f0;
-  d.f1 = sr.f1;
-  bool reg = true;
-  for (uint32_t f = sr.f0 + 1; f <= sr.f1 && reg; ++f) {
-    const Frag F = e.frags[f];
-    reg = F.blk == F0.blk + (f - sr.f0) && F.start == kHdr && (f == sr.f1 || F.len == kM);
-  }
-  d.regular = reg ? 1 : 0;
-  d.npieces = (uint8_t)p.n;
-  d.psrc = 0;
-  for (uint32_t q = 0; q < 6; ++q) {
-    d.plen[q] = q < p.n ? p.len[q] : 0;
-    d.poff[q] = q < p.n ? (uint32_t)p.off[q] : 0;
-    if (q < p.n && p.src[q]) d.psrc |= (uint8_t)(1u << q);
-  }
-#pragma unroll
-  for (int b = 0; b < 48; ++b) d.lit[b] = p.lit[b];
-  uint4* dst = reinterpret_cast<uint4*>(rd + j);
-  const uint4* s = reinterpret_cast<const uint4*>(&d);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) dst[k] = s[k];
-}
-
-// The LDS block image is skewed by one dword per 128 B (word w lives at w + w/32): lanes reading
-// consecutive 128 B CRC windows would otherwise all hit the same bank. 16 B chunks (the copy and
-// store units) never straddle a pad word.
-__device__ __forceinline__ uint32_t iw(uint32_t w) { return w + (w >> 5); }
-__device__ __forceinline__ uint8_t img_get(const uint32_t* img, uint32_t b) {
-  return (uint8_t)(img[iw(b >> 2)] >> ((b & 3u) * 8));
-}
-__device__ __forceinline__ void img_put(uint32_t* img, uint32_t b, uint8_t v) {
-  reinterpret_cast<uint8_t*>(img)[iw(b >> 2) * 4 + (b & 3u)] = v;
-}
-
 // 16 source bytes at an arbitrary address from two aligned 16 B loads (caller checks bounds)
 __device__ __forceinline__ uint4 shift16(uint4 v0, uint4 v1, uint32_t sh) {
   // named scalars and two select stages: an array indexed by w would be lowered to a scratch round trip
@@ -655,337 +511,421 @@ __device__ __forceinline__ uint64_t src_at(uint64_t d0, uint32_t l0, uint32_t st
   return (uint64_t)start_off + (blk0 + 1 + q) * kL + kHdr + r;
 }
 
-constexpr int kPT = 512;   // k_pack threads
-constexpr int kPWaves = kPT / 64;
-constexpr int kRecBatch = kPT;
+// ------------------------------------------------------------------------------------------
+// k_write's per-record descriptor: the payload as materialised prefix bytes | one source range (the
+// longest source piece: key+value+meta of a record, the key of a hint) | materialised suffix bytes.
+// Records whose prefix + suffix exceed kWLit bytes (NsSize/EtagSize beyond ~60) are marked
+// `general` and written by k_write_general instead.
+constexpr int kWLit = 96;
+struct RecDescW {
+  uint64_t d0;       // file offset of the data of the source payload's first fragment
+  uint32_t l0;       // its length
+  uint32_t f0, f1;   // source fragments
+  uint32_t mid_off;  // source payload offset of the source range
+  uint32_t mid_len;
+  uint8_t npre, nsuf, regular, general;
+  uint8_t lit[kWLit];  // prefix bytes, then suffix bytes
+};
+static_assert(sizeof(RecDescW) == 128, "RecDescW layout");
 
-// k_pack: persistent workgroups, one output block at a time: (1) each record with a fragment in the
-// block writes its literal bytes into the LDS image and queues source copy jobs; (2) the waves copy
-// the jobs (lanes over 16 B image chunks, loads issued ahead of the LDS writes); (3) CRC-32C of every
-// fragment: 128 B windows aligned to the fragment end, two slice-by-4 chains per window, shifted to
-// the fragment end with A_{8*128*m} and XOR-ed into the fragment's accumulator; headers written;
-// (4) the image streams out with aligned 16 B stores.
 template <int PM>
-__global__ __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4))) void k_pack(PackArgs A) {
-  const uint64_t* X = A.emisc + X_LAY + A.lay * kLayStride;
-  const uint64_t b0 = X[4], ke = X[2];
-  if (ke == b0 - 1 || X[3] - A.pos > A.cap) return;  // nothing to write / does not fit (result says so)
-  const uint64_t K = ke - b0 + 1;
-  const EncDev& e = A.e;
+__device__ __forceinline__ void prog_of(const EncDev& e, uint64_t j, uint64_t row, const uint64_t* __restrict__ dst_da,
+                                        const uint64_t* __restrict__ dpos, const uint8_t* __restrict__ mflag, Prog& p) {
+  if (PM == PM_DST) prog_record(e, row, mflag[row] != 0, p);
+  else if (PM == PM_HINT_DST) prog_hint(e, row, dpos[j], dst_da[j + 1] - dst_da[j] - kHdr, p);
+  else prog_hint(e, row, e.t.foff[row] - kHdr, e.t.size[row], p);
+}
+
+template <int PM>
+__global__ __launch_bounds__(256) void k_recdesc_w(EncDev e, const uint64_t* __restrict__ emisc,
+                                                    const uint32_t* __restrict__ dsrc, const uint64_t* __restrict__ dst_da,
+                                                    const uint64_t* __restrict__ dpos, const uint8_t* __restrict__ mflag,
+                                                    RecDescW* __restrict__ rd) {
+  const uint64_t j = blockIdx.x * 256ull + threadIdx.x;
+  if (j >= emisc[X_NDENSE]) return;
+  const uint64_t row = dsrc[j];
+  Prog p;
+  prog_of<PM>(e, j, row, dst_da, dpos, mflag, p);
+  const SrcRec sr = src_rec(e.t, e.frags, row);
+  const Frag F0 = e.frags[sr.f0];
+  RecDescW d;
+  d.d0 = frag_file(F0, e.start_off);
+  d.l0 = F0.len;
+  d.f0 = sr.f0;
+  d.f1 = sr.f1;
+  bool reg = true;
+  for (uint32_t f = sr.f0 + 1; f <= sr.f1 && reg; ++f) {
+    const Frag F = e.frags[f];
+    reg = F.blk == F0.blk + (f - sr.f0) && F.start == kHdr && (f == sr.f1 || F.len == kM);
+  }
+  d.regular = reg ? 1 : 0;
+  // the source range: the longest source piece (none: everything is prefix)
+  uint32_t m = p.n, ml = 0;
+  for (uint32_t q = 0; q < p.n; ++q)
+    if (p.src[q] && p.len[q] > ml) { m = q; ml = p.len[q]; }
+  uint32_t npre = 0, nsuf = 0;
+  for (uint32_t q = 0; q < p.n; ++q) {
+    if (q < m) npre += p.len[q];
+    else if (q > m) nsuf += p.len[q];
+  }
+  d.general = npre + nsuf > (uint32_t)kWLit ? 1 : 0;
+  d.npre = (uint8_t)(d.general ? 0 : npre);
+  d.nsuf = (uint8_t)(d.general ? 0 : nsuf);
+  d.mid_off = m < p.n ? (uint32_t)p.off[m] : 0u;
+  d.mid_len = ml;
+#pragma unroll
+  for (int b = 0; b < kWLit; ++b) d.lit[b] = 0;
+  if (!d.general) {
+    uint32_t o = 0;
+    for (uint32_t q = 0; q < p.n; ++q) {
+      if (q == m) continue;
+      for (uint32_t b = 0; b < p.len[q]; ++b) {
+        uint8_t v;
+        if (!p.src[q]) {
+          v = p.lit[p.off[q] + b];
+        } else {
+          const uint64_t z = p.off[q] + b;
+          if (reg) { uint64_t run; v = e.seg[src_at(d.d0, d.l0, e.start_off, z, run)]; }
+          else v = src_byte(e.seg, e.frags, e.start_off, sr, z);
+        }
+        d.lit[o++] = v;
+      }
+    }
+  }
+  uint4* dst = reinterpret_cast<uint4*>(rd + j);
+  const uint4* s = reinterpret_cast<const uint4*>(&d);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) dst[k] = s[k];
+}
+
+// ------------------------------------------------------------------------------------------
+// k_write: the record-parallel WAL writer (Wal.WriteRecord wal.go:505-549 for every written record
+// at once). One wave per record, persistent waves striding over the records. A record's fragments
+// follow in closed form from its header offset (data up to the block end, continuation headers at
+// block starts). Per fragment the lanes take the 16 B units of its data in the output, aligned to
+// the output address, 64 consecutive units per round (lane 0 = the last unit of the round):
+//   fetch   the unit's bytes from the source payload: two aligned 16 B loads + byte shift when the
+//           bytes lie in one source piece and one source fragment, bytewise otherwise (literals,
+//           piece edges);
+//   store   one 16 B store, or single bytes for the units at the fragment edges;
+//   CRC     raw CRC-32C of the unit (slice-by-4, bytes outside the fragment zeroed), shifted to the
+//           round's end by A_{8*16*l} = A_{8*128*g} A_{8*16*h} (l = 8g + h: two lane-operator stages
+//           with XOR reductions over 8 lanes), Horner over rounds with A_{8*1024}; the zero bytes
+//           after the fragment end in its last unit are undone by A_{8t}^-1.
+// Lanes 0..6 then write the header (ComputeCRC32 utils.go:24-29 of the data, length, type). The
+// zero pad before a record that starts a block (wal.go:509-512) is written by that record.
+constexpr int kWT = 256;
+constexpr int kWopStride = 144;  // lane-operator tables 16 words apart in bank space: lanes h and
+                                 // h + 4 share a bank only when their nibbles match
+
+// one output WAL of a k_write launch
+struct WLay {
+  const uint64_t* da;    // the layout's y-coordinates (dense, N+1)
+  const uint64_t* fpos;  // file offset of each dense record's first header in this layout
+  const void* rd;        // RecDescW per dense record
+  uint8_t* out;
+  uint64_t pos, cap;     // file offset of out[0]; out capacity
+  uint32_t lay;          // layout slot in emisc
+};
+
+// the layout has blocks and fits the output (otherwise nothing is written; the result says so)
+__device__ __forceinline__ bool lay_ok(const uint64_t* __restrict__ emisc, const WLay& w) {
+  const uint64_t* X = emisc + X_LAY + w.lay * kLayStride;
+  return !(X[2] == X[4] - 1 || X[3] - w.pos > w.cap);
+}
+
+struct WArgs {
+  EncDev e;
+  WLay w[2];              // dst WAL and hint WAL of a compaction (nlay = 2), or the hint WAL
+  uint32_t nlay;
+  const uint64_t* emisc;
+  const uint32_t* wops;   // enc_ops + kEncWrOps
+  const uint32_t* initc;  // A_{8L}(0xFFFFFFFF)
+};
+
+__device__ __forceinline__ uint64_t blk_end(uint64_t P) { return P + kL - (P - 40) % kL; }
+
+// file offset just past a record whose first header is at P, with a payload of len > 0 bytes
+__device__ __forceinline__ uint64_t rec_end(uint64_t P, uint64_t len) {
+  const uint64_t be = blk_end(P), ds = P + kHdr;
+  if (ds + len <= be) return ds + len;
+  const uint64_t rem = len - (be - ds);
+  const uint64_t q = (rem - 1) / kM;  // whole continuation blocks before the last fragment
+  return be + q * kL + kHdr + (rem - q * kM);
+}
+
+__device__ __forceinline__ uint32_t op_apply_s(const uint32_t* __restrict__ op, uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r ^= op[i * 16 + ((x >> (4 * i)) & 15u)];
+  return r;
+}
+
+__device__ __forceinline__ uint32_t sel_byte(uint4 v, uint32_t b) {
+  const uint32_t w = (b & 8u) ? ((b & 4u) ? v.w : v.z) : ((b & 4u) ? v.y : v.x);
+  return (w >> (8 * (b & 3u))) & 0xffu;
+}
+
+// bytes [lo, hi) of a 16 B unit
+__device__ __forceinline__ uint4 range_mask(int32_t lo, int32_t hi) {
+  uint32_t m[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int32_t a = min(max(lo - 4 * k, 0), 4), b = min(max(hi - 4 * k, 0), 4);
+    m[k] = (uint32_t)(((1ull << (8 * b)) - 1) & ~((1ull << (8 * a)) - 1));
+  }
+  return make_uint4(m[0], m[1], m[2], m[3]);
+}
+
+// 16 bytes of a wave's staged literals starting at literal offset o (-16 < o <= kWLit)
+constexpr int kWLitWords = (16 + kWLit + 32) / 4;
+__device__ __forceinline__ uint4 lit_window(const uint32_t* __restrict__ sl, int32_t o) {
+  const uint32_t base = (uint32_t)(16 + o), w = base >> 2, sh = base & 3u;
+  const uint32_t x0 = sl[w], x1 = sl[w + 1], x2 = sl[w + 2], x3 = sl[w + 3], x4 = sl[w + 4];
+  return make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                    __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+}
+
+__device__ __forceinline__ uint32_t crc16_raw(const uint32_t* __restrict__ tab, uint4 v) {
+  uint32_t x = v.x;
+  x = tab[768 + (x & 0xffu)] ^ tab[512 + ((x >> 8) & 0xffu)] ^ tab[256 + ((x >> 16) & 0xffu)] ^ tab[x >> 24];
+  x ^= v.y;
+  x = tab[768 + (x & 0xffu)] ^ tab[512 + ((x >> 8) & 0xffu)] ^ tab[256 + ((x >> 16) & 0xffu)] ^ tab[x >> 24];
+  x ^= v.z;
+  x = tab[768 + (x & 0xffu)] ^ tab[512 + ((x >> 8) & 0xffu)] ^ tab[256 + ((x >> 16) & 0xffu)] ^ tab[x >> 24];
+  x ^= v.w;
+  return tab[768 + (x & 0xffu)] ^ tab[512 + ((x >> 8) & 0xffu)] ^ tab[256 + ((x >> 16) & 0xffu)] ^ tab[x >> 24];
+}
+
+__global__ __launch_bounds__(kWT) void k_write(WArgs A) {
   const uint64_t N = A.emisc[X_NDENSE];
-  const RecDesc* __restrict__ RD = static_cast<const RecDesc*>(A.rd);
-
-  __shared__ __attribute__((aligned(16))) uint32_t img[kL / 4 + kL / 128 + 8];
+  const EncDev& e = A.e;
   __shared__ uint32_t tab[4 * 256];
-  __shared__ uint32_t ops[2 * 16 * 128];
-  __shared__ uint32_t half[128];
-  __shared__ uint16_t f_hdr[kRecBatch], f_dat[kRecBatch], f_len[kRecBatch];
-  __shared__ uint8_t f_type[kRecBatch];
-  __shared__ uint32_t f_acc[kRecBatch], f_win[kRecBatch + 1];
-  __shared__ uint16_t j_img[kJobCap], j_len[kJobCap];
-  __shared__ uint64_t j_src[kJobCap];
-  __shared__ uint32_t j_pre[kJobCap + 1];
-  __shared__ uint32_t s_njobs, s_nrec, s_scan[kPWaves];
-
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // slice-by-4 tables (tab[256*k + b] = CRC of byte b followed by k zero bytes) and operators
-  for (uint32_t i = tid; i < 256; i += kPT) {
+  __shared__ uint32_t lop[16 * kWopStride + 128];
+  __shared__ uint32_t s_lit[kWT / 64][kWLitWords];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  for (uint32_t i = tid; i < 256; i += kWT) {
     uint32_t c = i;
     for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
     tab[i] = c;
   }
-  for (uint32_t i = tid; i < 2 * 16 * 128; i += kPT) ops[i] = A.crc_ops[i];
+  for (uint32_t i = tid; i < 16 * 128; i += kWT) lop[(i >> 7) * kWopStride + (i & 127u)] = A.wops[i];
+  for (uint32_t i = tid; i < 128; i += kWT) lop[16 * kWopStride + i] = A.wops[16 * 128 + i];
+  for (uint32_t i = tid; i < (kWT / 64) * kWLitWords; i += kWT) (&s_lit[0][0])[i] = 0;
   __syncthreads();
-  if (tid < 256) {
-    uint32_t c = tab[tid];
-    for (int k = 1; k < 4; ++k) { c = (c >> 8) ^ tab[c & 0xffu]; tab[256 * k + tid] = c; }
-  }
-  // A_{8*64}: 64 zero bytes (half-window join)
-  if (tid < 128) {
-    const uint32_t i = tid >> 4, n = tid & 15u;
-    uint32_t x = n << (4 * i);
-    for (int b = 0; b < 64; ++b) x = (x >> 8) ^ tab[x & 0xffu];
-    half[tid] = x;
+  for (uint32_t i = tid; i < 256; i += kWT) {
+    uint32_t c = tab[i];
+    for (int k = 1; k < 4; ++k) { c = (c >> 8) ^ tab[c & 0xffu]; tab[256 * k + i] = c; }
   }
   __syncthreads();
+  const uint32_t* lop_h = lop + (lane & 7u) * kWopStride;
+  const uint32_t* lop_g = lop + (8u + (lane >> 3)) * kWopStride;
+  const uint32_t* lop_c = lop + 16 * kWopStride;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* sl = s_lit[wv];
+  const uint64_t nw = (uint64_t)gridDim.x * (kWT / 64);
+  const uint64_t w0 = (uint64_t)blockIdx.x * (kWT / 64) + wv;
+  const bool ok0 = lay_ok(A.emisc, A.w[0]), ok1 = A.nlay > 1 && lay_ok(A.emisc, A.w[1]);
+  // items: the records of layout 0, then those of layout 1 (short hint records last)
+  for (uint64_t it = w0; it < N * A.nlay; it += nw) {
+    const uint32_t li = it >= N ? 1u : 0u;
+    const uint64_t j = it - (li ? N : 0);
+    const WLay Ly = li ? A.w[1] : A.w[0];
+    if (!(li ? ok1 : ok0)) continue;
+    const uint64_t obase = (uint64_t)(uintptr_t)Ly.out;
+    const uint4* sp = reinterpret_cast<const uint4*>(static_cast<const RecDescW*>(Ly.rd) + j);
+    const uint4 h0 = sp[0], h1 = sp[1];
+    if ((h1.w >> 24) != 0) continue;  // general record: k_write_general
+    const uint64_t P = Ly.fpos[j];
+    const uint64_t aj = Ly.da[j];
+    const uint64_t len = Ly.da[j + 1] - aj - kHdr;
+    const uint64_t d0 = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
+    const uint32_t l0 = h0.z;
+    SrcRec sr;
+    sr.f0 = h0.w;
+    sr.f1 = h1.x;
+    const uint32_t mid_off = h1.y, mid_len = h1.z;
+    const int32_t npre = (int32_t)(h1.w & 0xffu);
+    const bool regular = ((h1.w >> 16) & 0xffu) != 0;
+    const int64_t zA = npre, zB = (int64_t)npre + mid_len;
+    // stage the literal bytes in LDS (wave-private; the previous record's reads are done: LDS
+    // executes a wave's operations in order)
+    if (lane < kWLit / 16) {
+      const uint4 q = sp[2 + lane];
+      sl[4 + 4 * lane] = q.x;
+      sl[5 + 4 * lane] = q.y;
+      sl[6 + 4 * lane] = q.z;
+      sl[7 + 4 * lane] = q.w;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-  for (uint64_t kb = blockIdx.x; kb < K; kb += gridDim.x) {
-    const uint64_t k = b0 + kb;
-    const BlkDesc D = A.desc[kb];
-    const int64_t Y = D.Y;
-    const int64_t E = Y + (int64_t)kL - (int64_t)kHdr * D.c;
-    if (D.pad) for (uint32_t b = kL - D.pad + tid; b < kL; b += kPT) img_put(img, b, 0);
+    // zero pad before a record that starts a block (at most 6 bytes)
+    if ((P - 40) % kL == 0) {
+      const uint64_t prev = j == 0 ? Ly.pos : rec_end(Ly.fpos[j - 1], aj - Ly.da[j - 1] - kHdr);
+      if (prev + lane < P) Ly.out[prev + lane - Ly.pos] = 0;
+    }
 
-    for (uint64_t rb = D.first;; rb += kRecBatch) {
-      if (tid == 0) { s_njobs = 0; s_nrec = 0; }
-      __syncthreads();
-      // ---- (1) one record per thread: fragment geometry, literals, copy jobs ----
-      const uint64_t j = rb + tid;
-      bool act = false;
-      uint64_t aj = 0, aj1 = 0;
-      uint4 rv[5];  // descriptor bytes [0, 80): everything but the literals (static indexing only)
-      if (j < N) {
-        // the descriptor load does not depend on the y-coordinates: both in flight together
-        const uint4* sp = reinterpret_cast<const uint4*>(RD + j);
+    uint64_t hp = P, x0 = 0;
+    for (bool first = true;; first = false) {  // (a zero-length First leaves x0 at 0)
+      const uint64_t be = blk_end(hp), ds = hp + kHdr;
+      const uint64_t rem = len - x0;
+      const uint64_t flen = rem < be - ds ? rem : be - ds;
+      const bool last = flen == rem;
+      const uint32_t type = first ? (last ? BCW_RECORD_FULL : BCW_RECORD_FIRST)
+                                  : (last ? BCW_RECORD_LAST : BCW_RECORD_MIDDLE);
+      uint32_t acc = 0;
+      if (flen) {
+        const uint64_t as = obase + (ds - Ly.pos), ae = as + flen;  // output addresses of the data
+        const uint64_t ul = (ae - 1) >> 4;
+        const uint32_t nunits = (uint32_t)(ul - (as >> 4) + 1);
+        for (int32_t c = (int32_t)((nunits + 63) >> 6) - 1; c >= 0; --c) {
+          const uint32_t r = (uint32_t)c * 64 + lane;
+          uint32_t cu = 0;
+          if (r < nunits) {
+            const uint64_t ua = (ul - r) << 4;
+            const int32_t b0 = ua < as ? (int32_t)(as - ua) : 0;
+            const int32_t b1 = ua + 16 > ae ? (int32_t)(ae - ua) : 16;
+            const int64_t zb = (int64_t)x0 + (int64_t)(ua - as);  // payload offset of unit byte 0
+            const int32_t pm = (int32_t)min(max(zA - zb, (int64_t)b0), (int64_t)b1);  // prefix [b0, pm)
+            const int32_t mm = (int32_t)min(max(zB - zb, (int64_t)b0), (int64_t)b1);  // source [pm, mm), suffix [mm, b1)
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (pm < mm) {
+              const uint64_t zs = mid_off + (uint64_t)(zb + pm - zA);  // source payload offset of byte pm
+              bool done = false;
+              if (regular) {
+                uint64_t run;
+                const uint64_t S = src_at(d0, l0, e.start_off, zs, run);
+                if (run >= (uint64_t)(mm - pm) && S >= (uint64_t)pm) {
+                  const uint64_t B = S - pm, Ba = B & ~15ull;
+                  if (Ba + 32 <= e.src_len) {
+                    const uint4 v0 = *reinterpret_cast<const uint4*>(e.seg + Ba);
+                    const uint4 v1 = *reinterpret_cast<const uint4*>(e.seg + Ba + 16);
+                    v = shift16(v0, v1, (uint32_t)(B & 15u));
+                    done = true;
+                  }
+                }
+              }
+              if (!done) {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (int32_t b = pm; b < mm; ++b) {
+                  const uint32_t by = src_byte(e.seg, e.frags, e.start_off, sr, zs + (uint64_t)(b - pm));
 #pragma unroll
-        for (int q = 0; q < 5; ++q) rv[q] = sp[q];
-        aj = A.da[j];
-        aj1 = A.da[j + 1];
-        act = ((int64_t)aj < Y) || ((int64_t)aj + (int64_t)kHdr <= E);
-      }
-      if (act) atomicAdd(&s_nrec, 1u);
-      f_acc[tid] = 0;
-      if (act) {
-        const bool cont = (int64_t)aj < Y;
-        const int64_t y0 = cont ? Y : (int64_t)aj + kHdr;
-        const int64_t y1 = (int64_t)aj1 < E ? (int64_t)aj1 : E;
-        const uint32_t hdr = cont ? 0u : (uint32_t)(kHdr * D.c + ((int64_t)aj - Y));
-        const uint32_t d0 = hdr + kHdr;
-        const uint32_t len = (uint32_t)(y1 - y0);
-        const bool ends = (int64_t)aj1 <= E;
-        f_hdr[tid] = (uint16_t)hdr;
-        f_dat[tid] = (uint16_t)d0;
-        f_len[tid] = (uint16_t)len;
-        f_type[tid] = cont ? (ends ? BCW_RECORD_LAST : BCW_RECORD_MIDDLE) : (ends ? BCW_RECORD_FULL : BCW_RECORD_FIRST);
-        const uint64_t x0 = (uint64_t)(y0 - (int64_t)aj - kHdr), x1 = x0 + len;
-        const uint8_t* litg = RD[j].lit;  // literal bytes straight from the (cached) descriptor line
-        struct {
-          uint64_t d0;
-          uint32_t l0, f0, f1;
-          bool regular;
-        } d;
-        d.d0 = (uint64_t)rv[0].x | ((uint64_t)rv[0].y << 32);
-        d.l0 = rv[0].z;
-        d.f0 = rv[0].w;
-        d.f1 = rv[1].x;
-        d.regular = (rv[1].y & 0xffffu) != 0;
-        const uint32_t npieces = (rv[1].y >> 16) & 0xffu, psrc = rv[1].y >> 24;
-        const uint32_t plen[6] = {rv[1].z, rv[1].w, rv[2].x, rv[2].y, rv[2].z, rv[2].w};
-        const uint32_t poff[6] = {rv[3].x, rv[3].y, rv[3].z, rv[3].w, rv[4].x, rv[4].y};
-        uint64_t pb = 0;
-        bool slow = false;
-#pragma unroll
-        for (uint32_t q = 0; q < 6; ++q) {
-          if (q >= npieces) break;
-          const uint64_t pe = pb + plen[q];
-          const uint64_t s0 = pb > x0 ? pb : x0, s1 = pe < x1 ? pe : x1;
-          if (s0 < s1) {
-            uint32_t io = d0 + (uint32_t)(s0 - x0);
-            if (!((psrc >> q) & 1u)) {
-              for (uint64_t s = s0; s < s1; ++s) img_put(img, io++, litg[poff[q] + (s - pb)]);
+                  for (int k = 0; k < 4; ++k)
+                    if ((b >> 2) == k) w[k] |= by << (8 * (b & 3));
+                }
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+              }
+              const uint4 m = range_mask(pm, mm);
+              v.x &= m.x; v.y &= m.y; v.z &= m.z; v.w &= m.w;
+            }
+            if (b0 < pm) {
+              const uint4 q = lit_window(sl, (int32_t)zb), m = range_mask(b0, pm);
+              v.x |= q.x & m.x; v.y |= q.y & m.y; v.z |= q.z & m.z; v.w |= q.w & m.w;
+            }
+            if (mm < b1) {
+              const uint4 q = lit_window(sl, (int32_t)(zb - zB + npre)), m = range_mask(mm, b1);
+              v.x |= q.x & m.x; v.y |= q.y & m.y; v.z |= q.z & m.z; v.w |= q.w & m.w;
+            }
+            uint8_t* dst = reinterpret_cast<uint8_t*>((uintptr_t)ua);
+            if (b1 - b0 == 16) {
+              __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(dst));
+              __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(dst) + 1);
+              __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(dst) + 2);
+              __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(dst) + 3);
             } else {
-              uint64_t z = poff[q] + (s0 - pb), l = s1 - s0;
-              // irregular source records: walk their fragments
-              uint32_t f = d.f0;
-              Frag F{};
-              uint64_t cum = 0;
-              if (!d.regular) {
-                F = e.frags[f];
-                while (z >= cum + F.len && f < d.f1) { cum += F.len; ++f; F = e.frags[f]; }
-              }
-              while (l > 0) {
-                uint64_t src, take;
-                if (d.regular) {
-                  src = src_at(d.d0, d.l0, e.start_off, z, take);
-                } else {
-                  const uint64_t in = z - cum;
-                  take = F.len - in;
-                  if (f >= d.f1) take = l;
-                  src = frag_file(F, e.start_off) + in;
-                }
-                if (take > l) take = l;
-                uint32_t slot = kJobCap;
-                if (!slow) {
-                  slot = atomicAdd(&s_njobs, 1u);
-                  if (slot >= kJobCap) slow = true;
-                }
-                if (slow) {
-                  for (uint64_t b = 0; b < take; ++b) img_put(img, io + (uint32_t)b, e.seg[src + b]);
-                } else {
-                  j_img[slot] = (uint16_t)io;
-                  j_len[slot] = (uint16_t)take;
-                  j_src[slot] = src;
-                }
-                io += (uint32_t)take;
-                z += take;
-                l -= take;
-                if (!d.regular && l > 0) { cum += F.len; ++f; F = e.frags[f]; }
-              }
+              for (int32_t b = b0; b < b1; ++b) dst[b] = (uint8_t)sel_byte(v, (uint32_t)b);
             }
+            cu = crc16_raw(tab, v);
           }
-          pb = pe;
+          cu = op_apply_s(lop_h, cu);
+          cu ^= __shfl_xor(cu, 1, 64);
+          cu ^= __shfl_xor(cu, 2, 64);
+          cu ^= __shfl_xor(cu, 4, 64);
+          cu = op_apply_s(lop_g, cu);
+          cu ^= __shfl_xor(cu, 8, 64);
+          cu ^= __shfl_xor(cu, 16, 64);
+          cu ^= __shfl_xor(cu, 32, 64);
+          acc = op_apply_s(lop_c, acc) ^ cu;
         }
+        const uint32_t t = (uint32_t)(((ul + 1) << 4) - ae);
+        if (t) acc = op_apply_s(A.wops + (17 + t) * 128, acc);
       }
-      __syncthreads();
-      const uint32_t nrec = s_nrec;
-      const uint32_t njobs = min(s_njobs, (uint32_t)kJobCap);
-      if (nrec == 0) break;
-      // ---- (2) copy jobs: prefix of the jobs' 16 B image chunks, then every thread takes 4 chunks
-      //      per round (job lookup, both loads of all 4 issued before any LDS write) ----
-      for (uint32_t base = 0; base < njobs; base += kPT) {
-        const uint32_t q = base + tid;
-        uint32_t cnt = 0;
-        if (q < njobs) {
-          const uint32_t o = j_img[q], l = j_len[q];
-          cnt = l ? ((o + l + 15) >> 4) - (o >> 4) : 0;
-        }
-        uint32_t incl = cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) { const uint32_t t = __shfl_up(incl, d, 64); if (lane >= (uint32_t)d) incl += t; }
-        if (lane == 63) s_scan[wave] = incl;
-        __syncthreads();
-        uint32_t pre = base ? j_pre[base] : 0;
-        for (uint32_t w = 0; w < wave; ++w) pre += s_scan[w];
-        if (q < njobs) j_pre[q + 1] = pre + incl;
-        if (q == 0) j_pre[0] = 0;
-        __syncthreads();
-      }
-      const uint32_t nunits = (njobs && !(A.abl & 2)) ? j_pre[njobs] : 0;
-      for (uint32_t u0 = tid; u0 < nunits; u0 += 4 * kPT) {
-        uint4 v0[4], v1[4];
-        uint32_t c0s[4], c1s[4];
-        uint64_t ss[4];
-        bool full[4];
-#pragma unroll
-        for (int k2 = 0; k2 < 4; ++k2) {
-          const uint32_t u = u0 + (uint32_t)k2 * kPT;
-          full[k2] = false;
-          c0s[k2] = c1s[k2] = 0;
-          ss[k2] = 0;
-          if (u < nunits) {
-            uint32_t lo = 0, hi = njobs;  // largest q with j_pre[q] <= u
-            while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (j_pre[mid] <= u) lo = mid; else hi = mid; }
-            const uint32_t o = j_img[lo], l = j_len[lo];
-            const uint32_t c = (o >> 4) + (u - j_pre[lo]);
-            const uint32_t c0 = c * 16 > o ? c * 16 : o;
-            const uint32_t c1 = c * 16 + 16 < o + l ? c * 16 + 16 : o + l;
-            const uint64_t sv = j_src[lo] + (c0 - o);
-            c0s[k2] = c0;
-            c1s[k2] = c1;
-            ss[k2] = sv;
-            if (c1 - c0 == 16 && (sv & ~15ull) + 32 <= e.src_len) {
-              full[k2] = true;
-              v0[k2] = *reinterpret_cast<const uint4*>(e.seg + (sv & ~15ull));
-              v1[k2] = *reinterpret_cast<const uint4*>(e.seg + (sv & ~15ull) + 16);
-            }
-          }
-        }
-#pragma unroll
-        for (int k2 = 0; k2 < 4; ++k2) {
-          if (full[k2]) {
-            *reinterpret_cast<uint4*>(&img[iw(c0s[k2] >> 2)]) = shift16(v0[k2], v1[k2], (uint32_t)(ss[k2] & 15u));
-          } else {
-            for (uint32_t b = c0s[k2]; b < c1s[k2]; ++b) img_put(img, b, e.seg[ss[k2] + (b - c0s[k2])]);
-          }
-        }
-      }
-      // window counts of the fragments (128 B windows, end-aligned)
-      {
-        const uint32_t cw = (tid < nrec) ? ((uint32_t)f_len[tid] + 127u) >> 7 : 0u;
-        uint32_t incl = cw;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) { const uint32_t t = __shfl_up(incl, d, 64); if (lane >= (uint32_t)d) incl += t; }
-        if (lane == 63) s_scan[wave] = incl;
-        __syncthreads();  // also: the copies are complete
-        uint32_t pre = 0;
-        for (uint32_t w = 0; w < wave; ++w) pre += s_scan[w];
-        f_win[tid + 1] = pre + incl;
-        if (tid == 0) f_win[0] = 0;
-        __syncthreads();
-      }
-      // ---- (3) CRC windows ----
-      const uint32_t nwin = (A.abl & 1) ? 0 : f_win[nrec];
-      for (uint32_t w = tid; w < nwin; w += kPT) {
-        uint32_t lo = 0, hi = nrec;
-        while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (f_win[mid] <= w) lo = mid; else hi = mid; }
-        const uint32_t f = lo;
-        const uint32_t m = f_win[f + 1] - 1 - w;  // windows between this one and the fragment end
-        const int32_t fs = f_dat[f];
-        const int32_t we = fs + (int32_t)f_len[f] - 128 * (int32_t)m;
-        const int32_t base = we - 128;
-        const int32_t dw = base >> 2;  // arithmetic: negative bases read clamped (masked) words
-        const uint32_t sh = (uint32_t)(base & 3);
-        uint32_t wv[32];
-        uint32_t prev = dw >= 0 ? img[iw((uint32_t)dw)] : 0u;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-          const int32_t idx = dw + 1 + i;
-          const uint32_t nx = idx >= 0 ? img[iw((uint32_t)idx)] : 0u;
-          wv[i] = __builtin_amdgcn_alignbyte(nx, prev, sh);
-          prev = nx;
-        }
-        // zero the bytes before the fragment start (first window only)
-        const int32_t zb = fs - base;  // bytes to clear
-        if (zb > 0) {
-#pragma unroll
-          for (int i = 0; i < 32; ++i) {
-            int32_t t = zb - 4 * i;
-            t = t < 0 ? 0 : (t > 4 ? 4 : t);
-            wv[i] &= (uint32_t)(0xffffffffull << (8 * t));
-          }
-        }
-        uint32_t ca = 0, cb2 = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          ca ^= wv[i];
-          ca = tab[768 + (ca & 0xffu)] ^ tab[512 + ((ca >> 8) & 0xffu)] ^ tab[256 + ((ca >> 16) & 0xffu)] ^ tab[ca >> 24];
-          cb2 ^= wv[16 + i];
-          cb2 = tab[768 + (cb2 & 0xffu)] ^ tab[512 + ((cb2 >> 8) & 0xffu)] ^ tab[256 + ((cb2 >> 16) & 0xffu)] ^ tab[cb2 >> 24];
-        }
-        uint32_t c = op_apply(half, ca) ^ cb2;
-        if (m & 15u) c = op_apply(&ops[(m & 15u) * 128], c);
-        if (m >> 4) c = op_apply(&ops[2048 + (m >> 4) * 128], c);
-        atomicXor(&f_acc[f], c);
-      }
-      __syncthreads();
-      if (tid < nrec) {
-        const uint32_t len = f_len[tid];
-        const uint32_t crc = ~(f_acc[tid] ^ A.initc[len]);
+      if (lane < kHdr) {
+        const uint32_t crc = ~(acc ^ A.initc[flen]);
         const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
-        const uint32_t h = f_hdr[tid];
-        img_put(img, h + 0, (uint8_t)masked);
-        img_put(img, h + 1, (uint8_t)(masked >> 8));
-        img_put(img, h + 2, (uint8_t)(masked >> 16));
-        img_put(img, h + 3, (uint8_t)(masked >> 24));
-        img_put(img, h + 4, (uint8_t)len);
-        img_put(img, h + 5, (uint8_t)(len >> 8));
-        img_put(img, h + 6, f_type[tid]);
+        const uint32_t by = lane < 4 ? (masked >> (8 * lane)) : lane == 4 ? (uint32_t)flen
+                          : lane == 5 ? (uint32_t)(flen >> 8) : type;
+        Ly.out[hp - Ly.pos + lane] = (uint8_t)by;
       }
-      __syncthreads();
-      if (nrec < kRecBatch) break;
+      x0 += flen;
+      if (last) break;
+      hp = be;
     }
-    // ---- (4) store image [lo, hi) at out[file - pos]: aligned 16 B stores, bytes at the edges ----
-    if (!(A.abl & 8)) {
-      const int64_t base = (int64_t)(40 + k * kL) - (int64_t)A.pos;  // out offset of image byte 0
-      const int64_t o0 = base + D.lo, o1 = base + D.hi;
-      const int64_t a0 = (o0 + 15) & ~15ll, a1 = o1 & ~15ll;
-      if (a0 >= a1) {
-        for (int64_t o = o0 + tid; o < o1; o += kPT) A.out[o] = img_get(img, (uint32_t)(o - base));
-      } else {
-        for (int64_t o = o0 + tid; o < a0; o += kPT) A.out[o] = img_get(img, (uint32_t)(o - base));
-        for (int64_t o = a1 + tid; o < o1; o += kPT) A.out[o] = img_get(img, (uint32_t)(o - base));
-        const uint32_t sh = (uint32_t)((a0 - base) & 3);
-        for (int64_t o = a0 + 16 * (int64_t)tid; o < a1; o += 16 * kPT) {
-          const uint32_t ib = (uint32_t)(o - base);
-          const uint32_t w0 = ib >> 2;
-          uint4 v;
-          if (sh == 0) {
-            if ((w0 & 3u) == 0) v = *reinterpret_cast<const uint4*>(&img[iw(w0)]);
-            else v = make_uint4(img[iw(w0)], img[iw(w0 + 1)], img[iw(w0 + 2)], img[iw(w0 + 3)]);
-          } else {
-            const uint32_t x0 = img[iw(w0)], x1 = img[iw(w0 + 1)], x2 = img[iw(w0 + 2)], x3 = img[iw(w0 + 3)],
-                           x4 = img[iw(w0 + 4)];
-            v = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                           __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
-          }
-          __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(A.out + o));
-          __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(A.out + o) + 1);
-          __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(A.out + o) + 2);
-          __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(A.out + o) + 3);
-        }
-      }
+  }
+}
+
+// The general records of k_write (literal bytes beyond kWLit): one thread per record, bytewise.
+template <int PM>
+__global__ __launch_bounds__(256) void k_write_general(WArgs WA, uint32_t li, const uint32_t* __restrict__ dsrc,
+                                                        const uint64_t* __restrict__ dst_da,
+                                                        const uint64_t* __restrict__ dpos,
+                                                        const uint8_t* __restrict__ mflag) {
+  const WLay A = li ? WA.w[1] : WA.w[0];
+  __shared__ uint32_t t0[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += 256) {
+    uint32_t c = i;
+    for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    t0[i] = c;
+  }
+  __syncthreads();
+  if (!lay_ok(WA.emisc, A)) return;
+  const uint64_t j = blockIdx.x * 256ull + threadIdx.x;
+  if (j >= WA.emisc[X_NDENSE]) return;
+  const RecDescW* D = static_cast<const RecDescW*>(A.rd) + j;
+  if (!D->general) return;
+  const EncDev& e = WA.e;
+  const uint64_t row = dsrc[j];
+  Prog p;
+  prog_of<PM>(e, j, row, dst_da, dpos, mflag, p);
+  const SrcRec sr = src_rec(e.t, e.frags, row);
+  const uint64_t P = A.fpos[j];
+  const uint64_t len = A.da[j + 1] - A.da[j] - kHdr;
+  if ((P - 40) % kL == 0) {
+    const uint64_t prev = j == 0 ? A.pos : rec_end(A.fpos[j - 1], A.da[j] - A.da[j - 1] - kHdr);
+    for (uint64_t b = prev; b < P; ++b) A.out[b - A.pos] = 0;
+  }
+  uint64_t hp = P, z = 0;
+  uint32_t q = 0;
+  uint64_t qb = 0;  // payload offset of piece q
+  for (bool first = true;; first = false) {
+    const uint64_t be = blk_end(hp), ds = hp + kHdr;
+    const uint64_t rem = len - z;
+    const uint64_t flen = rem < be - ds ? rem : be - ds;
+    const bool last = flen == rem;
+    const uint32_t type = first ? (last ? BCW_RECORD_FULL : BCW_RECORD_FIRST)
+                                : (last ? BCW_RECORD_LAST : BCW_RECORD_MIDDLE);
+    uint32_t crc = 0xffffffffu;
+    for (uint64_t i = 0; i < flen; ++i, ++z) {
+      while (z >= qb + p.len[q]) { qb += p.len[q]; ++q; }
+      const uint32_t by = p.src[q] ? src_byte(e.seg, e.frags, e.start_off, sr, p.off[q] + (z - qb))
+                                   : p.lit[p.off[q] + (z - qb)];
+      A.out[ds + i - A.pos] = (uint8_t)by;
+      crc = (crc >> 8) ^ t0[(crc ^ by) & 0xffu];
     }
-    __syncthreads();  // the image is reused by the next block
+    crc = ~crc;
+    const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;
+    uint8_t* h = A.out + (hp - A.pos);
+    h[0] = (uint8_t)masked;
+    h[1] = (uint8_t)(masked >> 8);
+    h[2] = (uint8_t)(masked >> 16);
+    h[3] = (uint8_t)(masked >> 24);
+    h[4] = (uint8_t)flen;
+    h[5] = (uint8_t)(flen >> 8);
+    h[6] = (uint8_t)type;
+    if (last) break;
+    hp = be;
   }
 }
 
@@ -1060,8 +1000,6 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
   const bool compact = L.p.mode == BCW_ENC_COMPACT;
   TileSum* tiles = static_cast<TileSum*>(s.tiles);
   Ev* evs = static_cast<Ev*>(s.ev);
-  BlkDesc* desc_w = static_cast<BlkDesc*>(s.desc_w);
-  BlkDesc* desc_h = static_cast<BlkDesc*>(s.desc_h);
   (void)hipMemsetAsync(s.emisc, 0, 64 * sizeof(uint64_t), st);
   (void)hipMemsetAsync(s.emisc + X_ERR, 0xff, sizeof(uint64_t), st);
   pr.begin(K_ENC_PREP, st, ev0);
@@ -1073,90 +1011,66 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     k_tile_scan<<<1, 1024, 0, st>>>(tiles, s.emisc, over_rows, lay, da);
     k_tile_scatter<<<ntiles, 256, 0, st>>>(sz, s.emisc, over_rows, tiles, s.dsrc, da);
   };
-  auto layout = [&](int lay, const uint64_t* da, uint64_t pos, BlkDesc* desc, uint64_t desc_cap) {
+
+  WArgs W{};
+  W.e = e;
+  W.emisc = s.emisc;
+  W.wops = L.crc_ops + kEncWrOps;
+  W.initc = L.initc;
+  const uint32_t rgrid = (uint32_t)((rows + 255) / 256) + 1;
+  RecDescW* wd = static_cast<RecDescW*>(s.recdesc);
+  RecDescW* wh = static_cast<RecDescW*>(s.recdesc_h);
+  // persistent write grid: as many 4-wave workgroups per CU as are resident (one wave per record)
+  static const int wpc = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_write, kWT, 0) != hipSuccess || n < 1) n = 4;
+    return n;
+  }();
+  const uint32_t wgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((2 * rows + 3) / 4, (uint64_t)L.num_cus * wpc));
+  auto layout = [&](int lay, const uint64_t* da, uint64_t pos) {
     const int kid = lay == 1 ? K_ENC_EVENTS_HINT : K_ENC_EVENTS;
     pr.begin(kid, st, ev0);
     k_events<<<1, kEvThreads, 0, st>>>(da, s.emisc, lay, pos - 40, evs, s.evb);
     pr.end(kid, st, ev0);
-    k_blkdesc<<<(uint32_t)((desc_cap + 255) / 256), 256, 0, st>>>(da, s.emisc, lay, evs, desc, desc_cap);
   };
-  PackArgs A{};
-  A.e = e;
-  A.rd = s.recdesc;
-  A.emisc = s.emisc;
-  A.crc_ops = L.crc_ops;
-  A.initc = L.initc;
-  {
-    static const char* ev = getenv("BCW_PACK_ABL");
-    A.abl = ev ? (uint32_t)atoi(ev) : 0u;
-  }
-  const uint32_t rgrid = (uint32_t)((rows + 255) / 256) + 1;
-  RecDesc* rdp = static_cast<RecDesc*>(s.recdesc);
-  // persistent pack grid: two 512-thread workgroups per CU (LDS ~75 KiB each)
-  auto pgrid = [&](uint64_t blocks) { return (uint32_t)std::min<uint64_t>(blocks, (uint64_t)L.num_cus * 2); };
   if (compact) {
     pr.begin(K_ENC_SCAN, st, ev0);
     scan(s.sz, 1, 0, s.da);
     pr.end(K_ENC_SCAN, st, ev0);
-    layout(0, s.da, L.p.wal_pos, desc_w, s.blk_cap_w);
+    layout(0, s.da, L.p.wal_pos);
     k_recoff<<<rgrid, 256, 0, st>>>(s.da, s.dsrc, s.emisc, 0, evs, s.evb, s.dpos, L.out.rec_off);
-    A.da = s.da;
-    A.desc = desc_w;
-    A.lay = 0;
-    A.out = L.out.wal;
-    A.pos = L.p.wal_pos;
-    A.cap = L.out.wal_cap;
-    pr.begin(K_ENC_PACK, st, ev0);
-    k_recdesc<PM_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, rdp);
-    k_pack<PM_DST><<<pgrid(s.blk_cap_w), kPT, 0, st>>>(A);
-    pr.end(K_ENC_PACK, st, ev0);
-    // the hint WAL only needs the dst offsets: its layout and pack run on the auxiliary stream,
-    // beside the dst pack
-    hipStream_t sh = L.aux ? L.aux : st;
-    if (L.aux) {
-      (void)hipEventRecord(L.ev_fork, st);
-      (void)hipStreamWaitEvent(sh, L.ev_fork, 0);
-    }
-    k_hint_sizes<<<rgrid, 256, 0, sh>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.hsz);
-    {
-      hipStream_t keep = st;
-      st = sh;
-      scan(s.hsz, 0, 1, s.hda);
-      layout(1, s.hda, L.p.hint_pos, desc_h, s.blk_cap_h);
-      st = keep;
-    }
-    PackArgs H = A;
-    H.da = s.hda;
-    H.rd = s.recdesc_h;
-    H.desc = desc_h;
-    H.lay = 1;
-    H.out = L.out.hint;
-    H.pos = L.p.hint_pos;
-    H.cap = L.out.hint_cap;
-    pr.begin(K_ENC_PACK_HINT, sh, ev0);
-    k_recdesc<PM_HINT_DST><<<rgrid, 256, 0, sh>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag,
-                                                  static_cast<RecDesc*>(s.recdesc_h));
-    k_pack<PM_HINT_DST><<<pgrid(s.blk_cap_h), kPT, 0, sh>>>(H);
-    pr.end(K_ENC_PACK_HINT, sh, ev0);
-    if (L.aux) {
-      (void)hipEventRecord(L.ev_join, sh);
-      (void)hipStreamWaitEvent(st, L.ev_join, 0);
-    }
+    // the hint WAL's layout needs the dst offsets (its records carry them)
+    pr.begin(K_ENC_HINT_LAYOUT, st, ev0);
+    k_hint_sizes<<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.hsz);
+    scan(s.hsz, 0, 1, s.hda);
+    pr.end(K_ENC_HINT_LAYOUT, st, ev0);
+    layout(1, s.hda, L.p.hint_pos);
+    k_recoff<<<rgrid, 256, 0, st>>>(s.hda, s.dsrc, s.emisc, 1, evs, s.evb, s.hpos, nullptr);
+    // both WALs in one persistent launch: dst records, then hint records
+    W.w[0] = WLay{s.da, s.dpos, wd, L.out.wal, L.p.wal_pos, L.out.wal_cap, 0};
+    W.w[1] = WLay{s.hda, s.hpos, wh, L.out.hint, L.p.hint_pos, L.out.hint_cap, 1};
+    W.nlay = 2;
+    pr.begin(K_ENC_WRITE, st, ev0);
+    k_recdesc_w<PM_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, wd);
+    k_recdesc_w<PM_HINT_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag, wh);
+    k_write<<<wgrid, kWT, 0, st>>>(W);
+    k_write_general<PM_DST><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr, s.mflag);
+    k_write_general<PM_HINT_DST><<<rgrid, 256, 0, st>>>(W, 1, s.dsrc, s.da, s.dpos, s.mflag);
+    pr.end(K_ENC_WRITE, st, ev0);
   } else {
     pr.begin(K_ENC_SCAN, st, ev0);
     scan(s.sz, 1, 0, s.hda);
     pr.end(K_ENC_SCAN, st, ev0);
-    layout(0, s.hda, L.p.hint_pos, desc_h, s.blk_cap_h);
-    A.da = s.hda;
-    A.desc = desc_h;
-    A.lay = 0;
-    A.out = L.out.hint;
-    A.pos = L.p.hint_pos;
-    A.cap = L.out.hint_cap;
-    pr.begin(K_ENC_PACK_HINT, st, ev0);
-    k_recdesc<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, rdp);
-    k_pack<PM_HINT_SRC><<<pgrid(s.blk_cap_h), kPT, 0, st>>>(A);
-    pr.end(K_ENC_PACK_HINT, st, ev0);
+    layout(0, s.hda, L.p.hint_pos);
+    k_recoff<<<rgrid, 256, 0, st>>>(s.hda, s.dsrc, s.emisc, 0, evs, s.evb, s.hpos, nullptr);
+    W.w[0] = WLay{s.hda, s.hpos, wd, L.out.hint, L.p.hint_pos, L.out.hint_cap, 0};
+    W.w[1] = W.w[0];
+    W.nlay = 1;
+    pr.begin(K_ENC_WRITE, st, ev0);
+    k_recdesc_w<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, wd);
+    k_write<<<wgrid, kWT, 0, st>>>(W);
+    k_write_general<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr, s.mflag);
+    pr.end(K_ENC_WRITE, st, ev0);
   }
   k_enc_finalize<<<1, 1, 0, st>>>(s.emisc, L.p.mode, L.p.wal_pos, L.out.wal_cap, L.p.hint_pos, L.out.hint_cap,
                                   L.d_src_result, L.d_result);
@@ -1164,8 +1078,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
 }
 
 size_t enc_sizeof_ev() { return sizeof(enc::Ev); }
-size_t enc_sizeof_recdesc() { return sizeof(enc::RecDesc); }
-size_t enc_sizeof_desc() { return sizeof(enc::BlkDesc); }
+size_t enc_sizeof_recdesc() { return sizeof(enc::RecDescW); }
 size_t enc_sizeof_tile() { return sizeof(enc::TileSum); }
 int enc_tile_items() { return enc::kTileItems; }
 int enc_ev_win() { return enc::kEvWin; }

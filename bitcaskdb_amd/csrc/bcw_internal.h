@@ -46,8 +46,10 @@ struct Tables {
   uint32_t* half;    // [8][16] A_{8*64} (nibble images)
   uint32_t* initc;   // [kBlock+1] A_{8L}(0xFFFFFFFF)
   uint32_t* lds_image;  // k_crc's LDS table image, laid out exactly as in LDS (see kLdsImage)
-  uint32_t* enc_ops;    // [2][16][8][16] A_{8*128*m}, A_{8*2048*m} (m < 16) nibble images (k_pack)
+  uint32_t* enc_ops;    // [kEncOpsWords] encode shift operators (nibble images, see build_enc_ops)
 };
+constexpr int kEncWrOps = 2 * 16 * 128;              // k_write's operators follow k_pack's
+constexpr int kEncOpsWords = kEncWrOps + 33 * 128;
 
 // k_crc LDS table image (dwords): slice-by-2 tables as 256-B rows {T1[e] x32, T0[e] x32} (lane l
 // reads bank l % 32), lane operators transposed to [8][16][64 lanes], then the carry and half operators.
@@ -77,7 +79,7 @@ struct Scratch {
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
 // stream around every kernel of the pipeline.
-enum KernelId { K_CHASE = 0, K_CRC, K_RECORDS, K_ENC_PREP, K_ENC_SCAN, K_ENC_EVENTS, K_ENC_PACK, K_ENC_PACK_HINT,
+enum KernelId { K_CHASE = 0, K_CRC, K_RECORDS, K_ENC_PREP, K_ENC_SCAN, K_ENC_EVENTS, K_ENC_WRITE, K_ENC_HINT_LAYOUT,
                 K_ENC_EVENTS_HINT, K_NUM };
 struct Prof {
   uint32_t mask = 0;  // bit k: time kernel id k
@@ -107,9 +109,9 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
 hipError_t launch_export_frags(const Scratch& s, const bcw_frag_table& out, uint32_t start_off, hipStream_t stream,
                                uint64_t n);
 
-// Encode scratch (grow-only, per context). rows: source table rows; blk_cap_*: output blocks.
+// Encode scratch (grow-only, per context). rows: source table rows.
 struct EncScratch {
-  uint64_t rows_cap = 0, blk_cap_w = 0, blk_cap_h = 0;
+  uint64_t rows_cap = 0;
   uint32_t* sz = nullptr;     // [rows] payload size per source row (0: not written)
   uint8_t* mflag = nullptr;   // [rows] meta dropped by Record.Encode
   uint32_t* dsrc = nullptr;   // [rows] dense record -> source row
@@ -117,13 +119,12 @@ struct EncScratch {
   uint64_t* hda = nullptr;    // [rows+1] hint WAL y-coordinates
   uint32_t* hsz = nullptr;    // [rows] hint payload sizes (compaction)
   uint64_t* dpos = nullptr;   // [rows] dst record offsets
+  uint64_t* hpos = nullptr;   // [rows] hint record offsets (compaction)
   void* tiles = nullptr;      // scan tile sums
   void* ev = nullptr;         // [rows+2] layout events
   uint32_t* evb = nullptr;    // [rows/win+2] governing event per k_events window
-  void* desc_w = nullptr;     // [blk_cap_w] block descriptors (dst WAL)
-  void* desc_h = nullptr;     // [blk_cap_h] (hint WAL)
-  void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc -> k_pack), dst WAL
-  void* recdesc_h = nullptr;  // [rows] the same for the hint WAL (packed beside the dst WAL)
+  void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc_w -> k_write), dst WAL
+  void* recdesc_h = nullptr;  // [rows] the same for the hint WAL
   uint64_t* emisc = nullptr;  // [64] counters
 };
 
@@ -140,14 +141,11 @@ struct EncLaunch {
   const uint32_t* crc_ops;
   const uint32_t* initc;
   int num_cus;
-  hipStream_t aux;            // second stream of the context (the hint WAL of a compaction), or null
-  hipEvent_t ev_fork, ev_join;
 };
 
 hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t stream, Prof* prof);
 size_t enc_sizeof_ev();
 size_t enc_sizeof_recdesc();
-size_t enc_sizeof_desc();
 size_t enc_sizeof_tile();
 int enc_tile_items();
 int enc_ev_win();

@@ -103,8 +103,8 @@ def test_compact_layout_events(ctx, target):
 
 
 def test_compact_tiny_records(ctx):
-    """NsSize 0, empty keys/values: 5-byte payloads, ~2700 fragments per output block (batched pack,
-    job-list overflow path)."""
+    """NsSize 0, empty keys/values: 5-byte payloads, ~2700 fragments per output block (one wave per
+    12-byte record, every unit an edge unit)."""
     rng = random.Random(3)
     payloads = [O.record_encode(b"", b"", b"", b"", 0, False, b"", BASE) for _ in range(20000)]
     payloads += [rec_of(rng, i, ns=0, vlen=rng.randrange(0, 30), klen=rng.randrange(0, 4)) for i in range(5000)]
@@ -119,6 +119,18 @@ def test_compact_large_records(ctx):
     src = make_src(payloads)
     keep = np.array([i % 3 != 1 for i in range(len(payloads))], dtype=np.uint8)
     run_compact(ctx, src, keep, pre_wal=5000, pre_hint=77)
+
+
+@pytest.mark.parametrize("ns", [60, 100, 150])
+def test_compact_large_namespace(ctx, ns):
+    """NsSize large enough that a record's (or hint's) re-encoded header bytes exceed the writer's
+    96-byte literal descriptor: those records take the bytewise general path."""
+    rng = random.Random(ns)
+    payloads = [rec_of(rng, i, ns=ns) for i in range(300)]
+    src = make_src(payloads)
+    keep = np.array([rng.random() < 0.8 for _ in payloads], dtype=np.uint8)
+    run_compact(ctx, src, keep, ns=ns, pre_wal=32768 - 50, pre_hint=100, seed=ns)
+    run_hint(ctx, src, ns=ns)
 
 
 def test_compact_config_shape(ctx):
