@@ -91,8 +91,8 @@ static void nibble_image(const uint32_t* img, uint32_t* t) {
 
 // encode shift operators (nibble images, 128 words each):
 //   k_pack:  [m] = A_{8*128*m}, [16 + m] = A_{8*2048*m} (m < 16)
-//   k_write (from kEncWrOps): [h] = A_{8*16*h}, [8 + g] = A_{8*128*g} (h, g < 8), [16] = A_{8*1024},
-//            [17 + t] = A_{8t}^-1 (t < 16)
+//   k_write (from kEncWrOps): [n] = A_{8*16*n}, [16 + n] = A_{8*256*n} (n < 16), [32 + n] = A_{8*4096*n}
+//            (n < 8), [40 + t] = A_{8t}^-1 (t < 16)
 static void build_enc_ops(uint32_t* ops) {
   uint32_t t0[256];
   byte_table(t0);
@@ -103,14 +103,13 @@ static void build_enc_ops(uint32_t* ops) {
       nibble_image(img, ops + (h * 16 + m) * 128);
     }
   uint32_t* w = ops + kEncWrOps;
-  for (int h = 0; h < 8; ++h) { shift_basis(t0, 16ull * h, img); nibble_image(img, w + h * 128); }
-  for (int g = 0; g < 8; ++g) { shift_basis(t0, 128ull * g, img); nibble_image(img, w + (8 + g) * 128); }
-  shift_basis(t0, 1024, img);
-  nibble_image(img, w + 16 * 128);
+  for (int n = 0; n < 16; ++n) { shift_basis(t0, 16ull * n, img); nibble_image(img, w + n * 128); }
+  for (int n = 0; n < 16; ++n) { shift_basis(t0, 256ull * n, img); nibble_image(img, w + (16 + n) * 128); }
+  for (int n = 0; n < 8; ++n) { shift_basis(t0, 4096ull * n, img); nibble_image(img, w + (32 + n) * 128); }
   for (int t = 0; t < 16; ++t) {
     shift_basis(t0, (uint64_t)t, img);
     invert_basis(img, inv);
-    nibble_image(inv, w + (17 + t) * 128);
+    nibble_image(inv, w + (40 + t) * 128);
   }
 }
 

@@ -602,21 +602,23 @@ __global__ __launch_bounds__(256) void k_recdesc_w(EncDev e, const uint64_t* __r
 // k_write: the record-parallel WAL writer (Wal.WriteRecord wal.go:505-549 for every written record
 // at once). One wave per record, persistent waves striding over the records. A record's fragments
 // follow in closed form from its header offset (data up to the block end, continuation headers at
-// block starts). Per fragment the lanes take the 16 B units of its data in the output, aligned to
-// the output address, 64 consecutive units per round (lane 0 = the last unit of the round):
-//   fetch   the unit's bytes from the source payload: two aligned 16 B loads + byte shift when the
-//           bytes lie in one source piece and one source fragment, bytewise otherwise (literals,
-//           piece edges);
+// block starts). A fragment's data is cut into 16 B units aligned to the output address; lane l
+// takes k = ceil(units/64) consecutive units (one pass per fragment) and, per unit:
+//   fetch   the bytes from the source payload: a lane whose units all lie in the record's source
+//           range of one source fragment streams aligned 16 B loads (kWBatch in flight) and shifts
+//           each unit out of two neighbours; edge units (fragment ends, literal prefix/suffix, a source
+//           fragment boundary) assemble up to four masked pieces;
 //   store   one 16 B store, or single bytes for the units at the fragment edges;
-//   CRC     raw CRC-32C of the unit (slice-by-4, bytes outside the fragment zeroed), shifted to the
-//           round's end by A_{8*16*l} = A_{8*128*g} A_{8*16*h} (l = 8g + h: two lane-operator stages
-//           with XOR reductions over 8 lanes), Horner over rounds with A_{8*1024}; the zero bytes
-//           after the fragment end in its last unit are undone by A_{8t}^-1.
-// Lanes 0..6 then write the header (ComputeCRC32 utils.go:24-29 of the data, length, type). The
-// zero pad before a record that starts a block (wal.go:509-512) is written by that record.
-constexpr int kWT = 256;
-constexpr int kWopStride = 144;  // lane-operator tables 16 words apart in bank space: lanes h and
-                                 // h + 4 share a bank only when their nibbles match
+//   CRC     a raw CRC-32C chain over its units (slice-by-8, bytes outside the fragment zeroed).
+// Each lane's chain is shifted to the end of the fragment's last unit by A_{8*16*d} (d = units after
+// it, three nibble operator stages), XOR-ed over the wave, and the zero bytes after the fragment end
+// are undone by A_{8t}^-1. Lanes 0..6 then write the header (ComputeCRC32 utils.go:24-29 of the data,
+// length, type). The zero pad before a record that starts a block (wal.go:509-512) is written by that
+// record.
+constexpr int kWT = 512;
+constexpr int kWopStride = 144;  // shift-operator tables 16 words apart in bank space: lanes with
+                                 // different operators collide only on equal nibbles
+constexpr int kWBatch = 5;       // source loads in flight per lane (a 4 KiB record: 5 units per lane)
 
 // one output WAL of a k_write launch
 struct WLay {
@@ -686,52 +688,119 @@ __device__ __forceinline__ uint4 lit_window(const uint32_t* __restrict__ sl, int
                     __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
 }
 
-__device__ __forceinline__ uint32_t crc16_raw(const uint32_t* __restrict__ tab, uint4 v) {
-  uint32_t x = v.x;
-  x = tab[768 + (x & 0xffu)] ^ tab[512 + ((x >> 8) & 0xffu)] ^ tab[256 + ((x >> 16) & 0xffu)] ^ tab[x >> 24];
-  x ^= v.y;
-  x = tab[768 + (x & 0xffu)] ^ tab[512 + ((x >> 8) & 0xffu)] ^ tab[256 + ((x >> 16) & 0xffu)] ^ tab[x >> 24];
-  x ^= v.z;
-  x = tab[768 + (x & 0xffu)] ^ tab[512 + ((x >> 8) & 0xffu)] ^ tab[256 + ((x >> 16) & 0xffu)] ^ tab[x >> 24];
-  x ^= v.w;
-  return tab[768 + (x & 0xffu)] ^ tab[512 + ((x >> 8) & 0xffu)] ^ tab[256 + ((x >> 16) & 0xffu)] ^ tab[x >> 24];
+// CRC-32C state after 16 more bytes (raw, slice-by-8: t8[256 k + b] = CRC of byte b and k zeros)
+__device__ __forceinline__ uint32_t crc_step16(const uint32_t* __restrict__ t8, uint32_t c, uint4 v) {
+  uint32_t x = c ^ v.x, y = v.y;
+  c = t8[1792 + (x & 0xffu)] ^ t8[1536 + ((x >> 8) & 0xffu)] ^ t8[1280 + ((x >> 16) & 0xffu)] ^ t8[1024 + (x >> 24)] ^
+      t8[768 + (y & 0xffu)] ^ t8[512 + ((y >> 8) & 0xffu)] ^ t8[256 + ((y >> 16) & 0xffu)] ^ t8[y >> 24];
+  x = c ^ v.z;
+  y = v.w;
+  return t8[1792 + (x & 0xffu)] ^ t8[1536 + ((x >> 8) & 0xffu)] ^ t8[1280 + ((x >> 16) & 0xffu)] ^ t8[1024 + (x >> 24)] ^
+         t8[768 + (y & 0xffu)] ^ t8[512 + ((y >> 8) & 0xffu)] ^ t8[256 + ((y >> 16) & 0xffu)] ^ t8[y >> 24];
+}
+
+// 16 source bytes starting at file offset S (two aligned loads; the caller checks the bounds)
+__device__ __forceinline__ uint4 src16(const uint8_t* __restrict__ seg, uint64_t S) {
+  const uint64_t Ba = S & ~15ull;
+  const uint4 v0 = *reinterpret_cast<const uint4*>(seg + Ba);
+  const uint4 v1 = *reinterpret_cast<const uint4*>(seg + Ba + 16);
+  return shift16(v0, v1, (uint32_t)(S & 15u));
+}
+
+__device__ __forceinline__ void or_masked(uint4& v, uint4 q, uint4 m) {
+  v.x |= q.x & m.x;
+  v.y |= q.y & m.y;
+  v.z |= q.z & m.z;
+  v.w |= q.w & m.w;
+}
+
+// per-record view for the unit assembly
+struct WRec {
+  uint64_t d0;
+  uint32_t l0;
+  SrcRec sr;
+  uint32_t mid_off;
+  int64_t zA, zB;  // payload offsets of the source range
+  int32_t npre;
+  bool regular;
+};
+
+// bytes [b0, b1) of the unit whose byte 0 is payload offset zb (other bytes 0): literal prefix,
+// source range (at most two source fragments: every fragment after the first holds M >= 16 bytes),
+// literal suffix
+__device__ __forceinline__ uint4 unit_general(const EncDev& e, const WRec& R, const uint32_t* __restrict__ sl,
+                                              int64_t zb, int32_t b0, int32_t b1) {
+  const int32_t pm = (int32_t)min(max(R.zA - zb, (int64_t)b0), (int64_t)b1);  // prefix [b0, pm)
+  const int32_t mm = (int32_t)min(max(R.zB - zb, (int64_t)b0), (int64_t)b1);  // source [pm, mm), suffix [mm, b1)
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (pm < mm) {
+    const uint64_t zs = R.mid_off + (uint64_t)(zb + pm - R.zA);  // source payload offset of byte pm
+    bool done = false;
+    if (R.regular) {
+      uint64_t run;
+      const uint64_t S = src_at(R.d0, R.l0, e.start_off, zs, run);
+      const int32_t m1 = (int32_t)min((uint64_t)mm, (uint64_t)pm + run);  // first source run [pm, m1)
+      if (S >= (uint64_t)pm && ((S - pm) & ~15ull) + 32 <= e.src_len) {
+        or_masked(v, src16(e.seg, S - pm), range_mask(pm, m1));
+        done = true;
+        if (m1 < mm) {
+          uint64_t run2;
+          const uint64_t S2 = src_at(R.d0, R.l0, e.start_off, zs + (uint64_t)(m1 - pm), run2);
+          if (S2 >= (uint64_t)m1 && ((S2 - m1) & ~15ull) + 32 <= e.src_len) or_masked(v, src16(e.seg, S2 - m1), range_mask(m1, mm));
+          else done = false;
+        }
+      }
+    }
+    if (!done) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (int32_t b = pm; b < mm; ++b) {
+        const uint32_t by = src_byte(e.seg, e.frags, e.start_off, R.sr, zs + (uint64_t)(b - pm));
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((b >> 2) == k) w[k] |= by << (8 * (b & 3));
+      }
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+  if (b0 < pm) or_masked(v, lit_window(sl, (int32_t)zb), range_mask(b0, pm));
+  if (mm < b1) or_masked(v, lit_window(sl, (int32_t)(zb - R.zB + R.npre)), range_mask(mm, b1));
+  return v;
 }
 
 __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
   const uint64_t N = A.emisc[X_NDENSE];
   const EncDev& e = A.e;
-  __shared__ uint32_t tab[4 * 256];
-  __shared__ uint32_t lop[16 * kWopStride + 128];
+  __shared__ uint32_t t8[8 * 256];
+  __shared__ uint32_t sop[40 * kWopStride];  // A_{8*16*n}, A_{8*256*n} (n < 16), A_{8*4096*n} (n < 8)
+  __shared__ uint32_t sinv[16 * 128];        // A_{8t}^-1
   __shared__ uint32_t s_lit[kWT / 64][kWLitWords];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   for (uint32_t i = tid; i < 256; i += kWT) {
     uint32_t c = i;
     for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
-    tab[i] = c;
+    t8[i] = c;
   }
-  for (uint32_t i = tid; i < 16 * 128; i += kWT) lop[(i >> 7) * kWopStride + (i & 127u)] = A.wops[i];
-  for (uint32_t i = tid; i < 128; i += kWT) lop[16 * kWopStride + i] = A.wops[16 * 128 + i];
+  for (uint32_t i = tid; i < 40 * 128; i += kWT) sop[(i >> 7) * kWopStride + (i & 127u)] = A.wops[i];
+  for (uint32_t i = tid; i < 16 * 128; i += kWT) sinv[i] = A.wops[40 * 128 + i];
   for (uint32_t i = tid; i < (kWT / 64) * kWLitWords; i += kWT) (&s_lit[0][0])[i] = 0;
   __syncthreads();
   for (uint32_t i = tid; i < 256; i += kWT) {
-    uint32_t c = tab[i];
-    for (int k = 1; k < 4; ++k) { c = (c >> 8) ^ tab[c & 0xffu]; tab[256 * k + i] = c; }
+    uint32_t c = t8[i];
+    for (int k = 1; k < 8; ++k) { c = (c >> 8) ^ t8[c & 0xffu]; t8[256 * k + i] = c; }
   }
   __syncthreads();
-  const uint32_t* lop_h = lop + (lane & 7u) * kWopStride;
-  const uint32_t* lop_g = lop + (8u + (lane >> 3)) * kWopStride;
-  const uint32_t* lop_c = lop + 16 * kWopStride;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* sl = s_lit[wv];
   const uint64_t nw = (uint64_t)gridDim.x * (kWT / 64);
   const uint64_t w0 = (uint64_t)blockIdx.x * (kWT / 64) + wv;
   const bool ok0 = lay_ok(A.emisc, A.w[0]), ok1 = A.nlay > 1 && lay_ok(A.emisc, A.w[1]);
+
   // items: the records of layout 0, then those of layout 1 (short hint records last)
   for (uint64_t it = w0; it < N * A.nlay; it += nw) {
     const uint32_t li = it >= N ? 1u : 0u;
     const uint64_t j = it - (li ? N : 0);
     const WLay Ly = li ? A.w[1] : A.w[0];
-    if (!(li ? ok1 : ok0)) continue;
+    if (!(li ? ok1 : ok0)) continue;  // nothing to write / does not fit (the result says so)
     const uint64_t obase = (uint64_t)(uintptr_t)Ly.out;
     const uint4* sp = reinterpret_cast<const uint4*>(static_cast<const RecDescW*>(Ly.rd) + j);
     const uint4 h0 = sp[0], h1 = sp[1];
@@ -739,15 +808,16 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
     const uint64_t P = Ly.fpos[j];
     const uint64_t aj = Ly.da[j];
     const uint64_t len = Ly.da[j + 1] - aj - kHdr;
-    const uint64_t d0 = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
-    const uint32_t l0 = h0.z;
-    SrcRec sr;
-    sr.f0 = h0.w;
-    sr.f1 = h1.x;
-    const uint32_t mid_off = h1.y, mid_len = h1.z;
-    const int32_t npre = (int32_t)(h1.w & 0xffu);
-    const bool regular = ((h1.w >> 16) & 0xffu) != 0;
-    const int64_t zA = npre, zB = (int64_t)npre + mid_len;
+    WRec R;
+    R.d0 = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
+    R.l0 = h0.z;
+    R.sr.f0 = h0.w;
+    R.sr.f1 = h1.x;
+    R.mid_off = h1.y;
+    R.npre = (int32_t)(h1.w & 0xffu);
+    R.zA = R.npre;
+    R.zB = (int64_t)R.npre + h1.z;
+    R.regular = ((h1.w >> 16) & 0xffu) != 0;
     // stage the literal bytes in LDS (wave-private; the previous record's reads are done: LDS
     // executes a wave's operations in order)
     if (lane < kWLit / 16) {
@@ -775,85 +845,82 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
       const bool last = flen == rem;
       const uint32_t type = first ? (last ? BCW_RECORD_FULL : BCW_RECORD_FIRST)
                                   : (last ? BCW_RECORD_LAST : BCW_RECORD_MIDDLE);
+      const uint32_t ic = A.initc[flen];  // in flight during the pass
       uint32_t acc = 0;
       if (flen) {
         const uint64_t as = obase + (ds - Ly.pos), ae = as + flen;  // output addresses of the data
-        const uint64_t ul = (ae - 1) >> 4;
-        const uint32_t nunits = (uint32_t)(ul - (as >> 4) + 1);
-        for (int32_t c = (int32_t)((nunits + 63) >> 6) - 1; c >= 0; --c) {
-          const uint32_t r = (uint32_t)c * 64 + lane;
-          uint32_t cu = 0;
-          if (r < nunits) {
-            const uint64_t ua = (ul - r) << 4;
-            const int32_t b0 = ua < as ? (int32_t)(as - ua) : 0;
-            const int32_t b1 = ua + 16 > ae ? (int32_t)(ae - ua) : 16;
-            const int64_t zb = (int64_t)x0 + (int64_t)(ua - as);  // payload offset of unit byte 0
-            const int32_t pm = (int32_t)min(max(zA - zb, (int64_t)b0), (int64_t)b1);  // prefix [b0, pm)
-            const int32_t mm = (int32_t)min(max(zB - zb, (int64_t)b0), (int64_t)b1);  // source [pm, mm), suffix [mm, b1)
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (pm < mm) {
-              const uint64_t zs = mid_off + (uint64_t)(zb + pm - zA);  // source payload offset of byte pm
-              bool done = false;
-              if (regular) {
-                uint64_t run;
-                const uint64_t S = src_at(d0, l0, e.start_off, zs, run);
-                if (run >= (uint64_t)(mm - pm) && S >= (uint64_t)pm) {
-                  const uint64_t B = S - pm, Ba = B & ~15ull;
-                  if (Ba + 32 <= e.src_len) {
-                    const uint4 v0 = *reinterpret_cast<const uint4*>(e.seg + Ba);
-                    const uint4 v1 = *reinterpret_cast<const uint4*>(e.seg + Ba + 16);
-                    v = shift16(v0, v1, (uint32_t)(B & 15u));
-                    done = true;
-                  }
-                }
-              }
-              if (!done) {
-                uint32_t w[4] = {0, 0, 0, 0};
-                for (int32_t b = pm; b < mm; ++b) {
-                  const uint32_t by = src_byte(e.seg, e.frags, e.start_off, sr, zs + (uint64_t)(b - pm));
+        const uint64_t uf = as >> 4, ul = (ae - 1) >> 4;
+        const uint32_t nunits = (uint32_t)(ul - uf + 1);
+        // lane l takes units l, l + 64, ...: per lane a Horner chain acc = A_{8*1024}(acc) ^ crc(unit)
+        uint32_t c = 0;
+        for (uint32_t r0 = lane; r0 - lane < nunits; r0 += 128) {
+          uint4 va[2][2];
+          uint32_t shv[2];
+          bool fast[2], valid[2];
 #pragma unroll
-                  for (int k = 0; k < 4; ++k)
-                    if ((b >> 2) == k) w[k] |= by << (8 * (b & 3));
+          for (int q = 0; q < 2; ++q) {
+            const uint32_t r = r0 + 64u * q;
+            valid[q] = r < nunits;
+            fast[q] = false;
+            shv[q] = 0;
+            if (valid[q]) {
+              const uint64_t ua = (uf + r) << 4;
+              const int64_t zb = (int64_t)x0 + (int64_t)ua - (int64_t)as;
+              if (ua >= as && ua + 16 <= ae && R.regular && zb >= R.zA && zb + 16 <= R.zB) {
+                uint64_t run;
+                const uint64_t S = src_at(R.d0, R.l0, e.start_off, R.mid_off + (uint64_t)(zb - R.zA), run);
+                if (run >= 16 && (S & ~15ull) + 32 <= e.src_len) {
+                  const uint4* sp2 = reinterpret_cast<const uint4*>(e.seg + (S & ~15ull));
+                  va[q][0] = sp2[0];
+                  va[q][1] = sp2[1];
+                  shv[q] = (uint32_t)(S & 15u);
+                  fast[q] = true;
                 }
-                v = make_uint4(w[0], w[1], w[2], w[3]);
               }
-              const uint4 m = range_mask(pm, mm);
-              v.x &= m.x; v.y &= m.y; v.z &= m.z; v.w &= m.w;
             }
-            if (b0 < pm) {
-              const uint4 q = lit_window(sl, (int32_t)zb), m = range_mask(b0, pm);
-              v.x |= q.x & m.x; v.y |= q.y & m.y; v.z |= q.z & m.z; v.w |= q.w & m.w;
-            }
-            if (mm < b1) {
-              const uint4 q = lit_window(sl, (int32_t)(zb - zB + npre)), m = range_mask(mm, b1);
-              v.x |= q.x & m.x; v.y |= q.y & m.y; v.z |= q.z & m.z; v.w |= q.w & m.w;
-            }
-            uint8_t* dst = reinterpret_cast<uint8_t*>((uintptr_t)ua);
-            if (b1 - b0 == 16) {
-              __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(dst));
-              __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(dst) + 1);
-              __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(dst) + 2);
-              __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(dst) + 3);
-            } else {
-              for (int32_t b = b0; b < b1; ++b) dst[b] = (uint8_t)sel_byte(v, (uint32_t)b);
-            }
-            cu = crc16_raw(tab, v);
           }
-          cu = op_apply_s(lop_h, cu);
-          cu ^= __shfl_xor(cu, 1, 64);
-          cu ^= __shfl_xor(cu, 2, 64);
-          cu ^= __shfl_xor(cu, 4, 64);
-          cu = op_apply_s(lop_g, cu);
-          cu ^= __shfl_xor(cu, 8, 64);
-          cu ^= __shfl_xor(cu, 16, 64);
-          cu ^= __shfl_xor(cu, 32, 64);
-          acc = op_apply_s(lop_c, acc) ^ cu;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            if (!valid[q]) continue;
+            const uint64_t ua = (uf + r0 + 64u * q) << 4;
+            uint4 v;
+            int32_t b0 = 0, b1 = 16;
+            if (fast[q]) {
+              v = shift16(va[q][0], va[q][1], shv[q]);
+            } else {
+              b0 = ua < as ? (int32_t)(as - ua) : 0;
+              b1 = ua + 16 > ae ? (int32_t)(ae - ua) : 16;
+              v = unit_general(e, R, sl, (int64_t)x0 + (int64_t)ua - (int64_t)as, b0, b1);
+            }
+            uint8_t* d = reinterpret_cast<uint8_t*>((uintptr_t)ua);
+            if (b1 - b0 == 16) {
+              __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(d));
+              __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(d) + 1);
+              __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(d) + 2);
+              __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(d) + 3);
+            } else {
+              for (int32_t b = b0; b < b1; ++b) d[b] = (uint8_t)sel_byte(v, (uint32_t)b);
+            }
+            c = op_apply_s(sop + (16 + 4) * kWopStride, c) ^ crc_step16(t8, 0u, v);  // A_{8*1024}
+          }
         }
+        // shift each lane's chain to the end of the fragment's last unit (d < 64 units follow it)
+        if (lane < nunits) {
+          const uint32_t dn = (nunits - 1 - lane) & 63u;
+          if (dn & 15u) c = op_apply_s(sop + (dn & 15u) * kWopStride, c);
+          if (dn >> 4) c = op_apply_s(sop + (16u + (dn >> 4)) * kWopStride, c);
+        }
+        c ^= __shfl_xor(c, 1, 64);
+        c ^= __shfl_xor(c, 2, 64);
+        c ^= __shfl_xor(c, 4, 64);
+        c ^= __shfl_xor(c, 8, 64);
+        c ^= __shfl_xor(c, 16, 64);
+        c ^= __shfl_xor(c, 32, 64);
         const uint32_t t = (uint32_t)(((ul + 1) << 4) - ae);
-        if (t) acc = op_apply_s(A.wops + (17 + t) * 128, acc);
+        acc = t ? op_apply_s(sinv + t * 128, c) : c;
       }
       if (lane < kHdr) {
-        const uint32_t crc = ~(acc ^ A.initc[flen]);
+        const uint32_t crc = ~(acc ^ ic);
         const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
         const uint32_t by = lane < 4 ? (masked >> (8 * lane)) : lane == 4 ? (uint32_t)flen
                           : lane == 5 ? (uint32_t)(flen >> 8) : type;

@@ -49,7 +49,7 @@ struct Tables {
   uint32_t* enc_ops;    // [kEncOpsWords] encode shift operators (nibble images, see build_enc_ops)
 };
 constexpr int kEncWrOps = 2 * 16 * 128;              // k_write's operators follow k_pack's
-constexpr int kEncOpsWords = kEncWrOps + 33 * 128;
+constexpr int kEncOpsWords = kEncWrOps + 56 * 128;
 
 // k_crc LDS table image (dwords): slice-by-2 tables as 256-B rows {T1[e] x32, T0[e] x32} (lane l
 // reads bank l % 32), lane operators transposed to [8][16][64 lanes], then the carry and half operators.
