@@ -618,7 +618,7 @@ __global__ __launch_bounds__(256) void k_recdesc_w(EncDev e, const uint64_t* __r
 constexpr int kWT = 512;
 constexpr int kWopStride = 144;  // shift-operator tables 16 words apart in bank space: lanes with
                                  // different operators collide only on equal nibbles
-constexpr int kWBatch = 5;       // source loads in flight per lane (a 4 KiB record: 5 units per lane)
+constexpr int kWRounds = 3;      // rounds of units whose source loads are in flight together
 
 // one output WAL of a k_write launch
 struct WLay {
@@ -767,14 +767,15 @@ __device__ __forceinline__ uint4 unit_general(const EncDev& e, const WRec& R, co
   return v;
 }
 
+template <int kG>
 __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
   const uint64_t N = A.emisc[X_NDENSE];
   const EncDev& e = A.e;
   __shared__ uint32_t t8[8 * 256];
   __shared__ uint32_t sop[40 * kWopStride];  // A_{8*16*n}, A_{8*256*n} (n < 16), A_{8*4096*n} (n < 8)
   __shared__ uint32_t sinv[16 * 128];        // A_{8t}^-1
-  __shared__ uint32_t s_lit[kWT / 64][kWLitWords];
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  __shared__ uint32_t s_lit[kWT / kG][kWLitWords];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, gl = tid & (kG - 1), gb = lane & ~(uint32_t)(kG - 1);
   for (uint32_t i = tid; i < 256; i += kWT) {
     uint32_t c = i;
     for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
@@ -782,50 +783,78 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
   }
   for (uint32_t i = tid; i < 40 * 128; i += kWT) sop[(i >> 7) * kWopStride + (i & 127u)] = A.wops[i];
   for (uint32_t i = tid; i < 16 * 128; i += kWT) sinv[i] = A.wops[40 * 128 + i];
-  for (uint32_t i = tid; i < (kWT / 64) * kWLitWords; i += kWT) (&s_lit[0][0])[i] = 0;
+  for (uint32_t i = tid; i < (kWT / kG) * kWLitWords; i += kWT) (&s_lit[0][0])[i] = 0;
   __syncthreads();
   for (uint32_t i = tid; i < 256; i += kWT) {
     uint32_t c = t8[i];
     for (int k = 1; k < 8; ++k) { c = (c >> 8) ^ t8[c & 0xffu]; t8[256 * k + i] = c; }
   }
   __syncthreads();
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t* sl = s_lit[wv];
-  const uint64_t nw = (uint64_t)gridDim.x * (kWT / 64);
-  const uint64_t w0 = (uint64_t)blockIdx.x * (kWT / 64) + wv;
+  uint32_t* sl = s_lit[tid / kG];
+  const uint64_t ng = (uint64_t)gridDim.x * (kWT / kG);    // groups in the grid
+  const uint64_t g0 = (uint64_t)blockIdx.x * (kWT / kG) + tid / kG;
   const bool ok0 = lay_ok(A.emisc, A.w[0]), ok1 = A.nlay > 1 && lay_ok(A.emisc, A.w[1]);
+  const uint32_t* hop = sop + (kG < 16 ? kG : 16 + kG / 16) * kWopStride;  // A_{8*16*kG}: one round of the group
 
-  // items: the records of layout 0, then those of layout 1 (short hint records last)
-  for (uint64_t it = w0; it < N * A.nlay; it += nw) {
+  // items: the records of layout 0, then those of layout 1 (short hint records last), one per group
+  // of kG lanes. An item's descriptor is loaded one item ahead: the RecDescW spread over the group's
+  // lanes 0-7 (header, then the literal bytes), da[j], da[j+1] and fpos[j] in every lane.
+  static_assert(kG >= 8 && kG <= 64, "group size");
+  const uint64_t nitems = N * A.nlay;
+  struct Pre {
+    uint4 q;
+    uint64_t a0, a1, fp;
+  };
+  auto fetch = [&](uint64_t it2, Pre& p) {
+    p.q = make_uint4(0, 0, 0, 0);
+    p.a0 = p.a1 = p.fp = 0;
+    if (it2 >= nitems) return;
+    const bool l2 = it2 >= N;
+    const uint64_t j2 = it2 - (l2 ? N : 0);
+    const WLay& W2 = l2 ? A.w[1] : A.w[0];
+    if (gl < 8) p.q = reinterpret_cast<const uint4*>(static_cast<const RecDescW*>(W2.rd) + j2)[gl];
+    p.a0 = W2.da[j2];
+    p.a1 = W2.da[j2 + 1];
+    p.fp = W2.fpos[j2];
+  };
+  // the group's lane k holds word x
+  auto gw = [&](uint32_t x, uint32_t k) { return (uint32_t)__shfl((int)x, (int)(gb + k), 64); };
+  Pre pn;
+  fetch(g0, pn);
+  for (uint64_t it = g0; it < nitems; it += ng) {
+    const Pre pc = pn;
+    const uint4 qc = pc.q;
+    fetch(it + ng, pn);  // in flight while this item is written
     const uint32_t li = it >= N ? 1u : 0u;
     const uint64_t j = it - (li ? N : 0);
-    const WLay Ly = li ? A.w[1] : A.w[0];
+    const WLay& Ly = li ? A.w[1] : A.w[0];
     if (!(li ? ok1 : ok0)) continue;  // nothing to write / does not fit (the result says so)
-    const uint64_t obase = (uint64_t)(uintptr_t)Ly.out;
-    const uint4* sp = reinterpret_cast<const uint4*>(static_cast<const RecDescW*>(Ly.rd) + j);
-    const uint4 h0 = sp[0], h1 = sp[1];
-    if ((h1.w >> 24) != 0) continue;  // general record: k_write_general
-    const uint64_t P = Ly.fpos[j];
-    const uint64_t aj = Ly.da[j];
-    const uint64_t len = Ly.da[j + 1] - aj - kHdr;
+    const uint32_t h1w = gw(qc.w, 1);
+    if ((h1w >> 24) != 0) continue;  // general record: k_write_general
+    uint8_t* const out = Ly.out;
+    const uint64_t pos = Ly.pos;
+    const uint64_t obase = (uint64_t)(uintptr_t)out;
+    const uint64_t P = pc.fp;
+    const uint64_t aj = pc.a0;
+    const uint64_t len = pc.a1 - aj - kHdr;
     WRec R;
-    R.d0 = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
-    R.l0 = h0.z;
-    R.sr.f0 = h0.w;
-    R.sr.f1 = h1.x;
-    R.mid_off = h1.y;
-    R.npre = (int32_t)(h1.w & 0xffu);
+    R.d0 = (uint64_t)gw(qc.x, 0) | ((uint64_t)gw(qc.y, 0) << 32);
+    R.l0 = gw(qc.z, 0);
+    R.sr.f0 = gw(qc.w, 0);
+    R.sr.f1 = gw(qc.x, 1);
+    R.mid_off = gw(qc.y, 1);
+    R.npre = (int32_t)(h1w & 0xffu);
     R.zA = R.npre;
-    R.zB = (int64_t)R.npre + h1.z;
-    R.regular = ((h1.w >> 16) & 0xffu) != 0;
-    // stage the literal bytes in LDS (wave-private; the previous record's reads are done: LDS
+    R.zB = (int64_t)R.npre + gw(qc.z, 1);
+    R.regular = ((h1w >> 16) & 0xffu) != 0;
+    // stage the literal bytes in LDS (group-private; the previous record's reads are done: LDS
     // executes a wave's operations in order)
-    if (lane < kWLit / 16) {
-      const uint4 q = sp[2 + lane];
-      sl[4 + 4 * lane] = q.x;
-      sl[5 + 4 * lane] = q.y;
-      sl[6 + 4 * lane] = q.z;
-      sl[7 + 4 * lane] = q.w;
+    if (gl >= 2 && gl < 8) {
+      uint32_t* d = sl + 4 + 4 * (gl - 2);
+      d[0] = qc.x;
+      d[1] = qc.y;
+      d[2] = qc.z;
+      d[3] = qc.w;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -833,8 +862,8 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
 
     // zero pad before a record that starts a block (at most 6 bytes)
     if ((P - 40) % kL == 0) {
-      const uint64_t prev = j == 0 ? Ly.pos : rec_end(Ly.fpos[j - 1], aj - Ly.da[j - 1] - kHdr);
-      if (prev + lane < P) Ly.out[prev + lane - Ly.pos] = 0;
+      const uint64_t prev = j == 0 ? pos : rec_end(Ly.fpos[j - 1], aj - Ly.da[j - 1] - kHdr);
+      if (prev + gl < P) out[prev + gl - pos] = 0;
     }
 
     uint64_t hp = P, x0 = 0;
@@ -848,41 +877,52 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
       const uint32_t ic = A.initc[flen];  // in flight during the pass
       uint32_t acc = 0;
       if (flen) {
-        const uint64_t as = obase + (ds - Ly.pos), ae = as + flen;  // output addresses of the data
+        const uint64_t as = obase + (ds - pos), ae = as + flen;  // output addresses of the data
         const uint64_t uf = as >> 4, ul = (ae - 1) >> 4;
         const uint32_t nunits = (uint32_t)(ul - uf + 1);
-        // lane l takes units l, l + 64, ...: per lane a Horner chain acc = A_{8*1024}(acc) ^ crc(unit)
+        // lane gl takes units gl, gl + kG, ...: per lane a Horner chain acc = A_{8*16*kG}(acc) ^ crc(unit).
+        // Interior units of the source range advance their source address incrementally (S, run:
+        // bytes left in that source fragment); edge units go through unit_general.
         uint32_t c = 0;
-        for (uint32_t r0 = lane; r0 - lane < nunits; r0 += 128) {
-          uint4 va[2][2];
-          uint32_t shv[2];
-          bool fast[2], valid[2];
+        const uint32_t rlast = nunits - 1;
+        int64_t zb = (int64_t)x0 + (int64_t)((uf + gl) << 4) - (int64_t)as;  // payload offset of unit byte 0
+        uint64_t S = 0;
+        int64_t run = -1;
+        constexpr int64_t kStep = 16 * kG;
+        for (uint32_t r0 = gl; r0 - gl < nunits; r0 += kG * kWRounds) {
+          uint4 va[kWRounds][2];
+          uint32_t shv[kWRounds];
+          bool fast[kWRounds];
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const uint32_t r = r0 + 64u * q;
-            valid[q] = r < nunits;
+          for (int q = 0; q < kWRounds; ++q) {
+            const uint32_t r = r0 + kG * q;
+            const int64_t z = zb + kStep * q;
             fast[q] = false;
             shv[q] = 0;
-            if (valid[q]) {
-              const uint64_t ua = (uf + r) << 4;
-              const int64_t zb = (int64_t)x0 + (int64_t)ua - (int64_t)as;
-              if (ua >= as && ua + 16 <= ae && R.regular && zb >= R.zA && zb + 16 <= R.zB) {
-                uint64_t run;
-                const uint64_t S = src_at(R.d0, R.l0, e.start_off, R.mid_off + (uint64_t)(zb - R.zA), run);
-                if (run >= 16 && (S & ~15ull) + 32 <= e.src_len) {
-                  const uint4* sp2 = reinterpret_cast<const uint4*>(e.seg + (S & ~15ull));
-                  va[q][0] = sp2[0];
-                  va[q][1] = sp2[1];
-                  shv[q] = (uint32_t)(S & 15u);
-                  fast[q] = true;
-                }
+            if (r < rlast && r != 0 && R.regular && z >= R.zA && z + 16 <= R.zB) {
+              if (run < 16) {
+                uint64_t ru;
+                S = src_at(R.d0, R.l0, e.start_off, R.mid_off + (uint64_t)(z - R.zA), ru);
+                run = (int64_t)ru;
               }
+              if (run >= 16 && (S & ~15ull) + 32 <= e.src_len) {
+                const uint4* sp2 = reinterpret_cast<const uint4*>(e.seg + (S & ~15ull));
+                va[q][0] = sp2[0];
+                va[q][1] = sp2[1];
+                shv[q] = (uint32_t)(S & 15u);
+                fast[q] = true;
+              }
+            } else {
+              run = -1;
             }
+            S += kStep;
+            run -= kStep;
           }
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            if (!valid[q]) continue;
-            const uint64_t ua = (uf + r0 + 64u * q) << 4;
+          for (int q = 0; q < kWRounds; ++q) {
+            const uint32_t r = r0 + kG * q;
+            if (r >= nunits) continue;
+            const uint64_t ua = (uf + r) << 4;
             uint4 v;
             int32_t b0 = 0, b1 = 16;
             if (fast[q]) {
@@ -890,7 +930,7 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
             } else {
               b0 = ua < as ? (int32_t)(as - ua) : 0;
               b1 = ua + 16 > ae ? (int32_t)(ae - ua) : 16;
-              v = unit_general(e, R, sl, (int64_t)x0 + (int64_t)ua - (int64_t)as, b0, b1);
+              v = unit_general(e, R, sl, zb + kStep * q, b0, b1);
             }
             uint8_t* d = reinterpret_cast<uint8_t*>((uintptr_t)ua);
             if (b1 - b0 == 16) {
@@ -901,30 +941,27 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
             } else {
               for (int32_t b = b0; b < b1; ++b) d[b] = (uint8_t)sel_byte(v, (uint32_t)b);
             }
-            c = op_apply_s(sop + (16 + 4) * kWopStride, c) ^ crc_step16(t8, 0u, v);  // A_{8*1024}
+            c = op_apply_s(hop, c) ^ crc_step16(t8, 0u, v);
           }
+          zb += kStep * kWRounds;
         }
-        // shift each lane's chain to the end of the fragment's last unit (d < 64 units follow it)
-        if (lane < nunits) {
-          const uint32_t dn = (nunits - 1 - lane) & 63u;
+        // shift each lane's chain to the end of the fragment's last unit (d < kG units follow it)
+        if (gl < nunits) {
+          const uint32_t dn = (nunits - 1 - gl) & (kG - 1);
           if (dn & 15u) c = op_apply_s(sop + (dn & 15u) * kWopStride, c);
           if (dn >> 4) c = op_apply_s(sop + (16u + (dn >> 4)) * kWopStride, c);
         }
-        c ^= __shfl_xor(c, 1, 64);
-        c ^= __shfl_xor(c, 2, 64);
-        c ^= __shfl_xor(c, 4, 64);
-        c ^= __shfl_xor(c, 8, 64);
-        c ^= __shfl_xor(c, 16, 64);
-        c ^= __shfl_xor(c, 32, 64);
+#pragma unroll
+        for (int m = 1; m < kG; m <<= 1) c ^= __shfl_xor(c, m, 64);
         const uint32_t t = (uint32_t)(((ul + 1) << 4) - ae);
         acc = t ? op_apply_s(sinv + t * 128, c) : c;
       }
-      if (lane < kHdr) {
+      if (gl < kHdr) {
         const uint32_t crc = ~(acc ^ ic);
         const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
-        const uint32_t by = lane < 4 ? (masked >> (8 * lane)) : lane == 4 ? (uint32_t)flen
-                          : lane == 5 ? (uint32_t)(flen >> 8) : type;
-        Ly.out[hp - Ly.pos + lane] = (uint8_t)by;
+        const uint32_t by = gl < 4 ? (masked >> (8 * gl)) : gl == 4 ? (uint32_t)flen
+                          : gl == 5 ? (uint32_t)(flen >> 8) : type;
+        out[hp - pos + gl] = (uint8_t)by;
       }
       x0 += flen;
       if (last) break;
@@ -1087,13 +1124,18 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
   const uint32_t rgrid = (uint32_t)((rows + 255) / 256) + 1;
   RecDescW* wd = static_cast<RecDescW*>(s.recdesc);
   RecDescW* wh = static_cast<RecDescW*>(s.recdesc_h);
-  // persistent write grid: as many 4-wave workgroups per CU as are resident (one wave per record)
-  static const int wpc = [] {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_write, kWT, 0) != hipSuccess || n < 1) n = 4;
-    return n;
-  }();
-  const uint32_t wgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((2 * rows + 3) / 4, (uint64_t)L.num_cus * wpc));
+  // persistent write grid: as many workgroups per CU as are resident
+  auto wgrid = [&](int g) {
+    static int wpc[17] = {};
+    int& n = wpc[g];
+    if (n == 0) {
+      hipError_t rc = g == 8 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_write<8>, kWT, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_write<16>, kWT, 0);
+      if (rc != hipSuccess || n < 1) n = 2;
+    }
+    const uint64_t groups = (uint64_t)kWT / g;
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((rows + groups - 1) / groups, (uint64_t)L.num_cus * n));
+  };
   auto layout = [&](int lay, const uint64_t* da, uint64_t pos) {
     const int kid = lay == 1 ? K_ENC_EVENTS_HINT : K_ENC_EVENTS;
     pr.begin(kid, st, ev0);
@@ -1116,11 +1158,20 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     // both WALs in one persistent launch: dst records, then hint records
     W.w[0] = WLay{s.da, s.dpos, wd, L.out.wal, L.p.wal_pos, L.out.wal_cap, 0};
     W.w[1] = WLay{s.hda, s.hpos, wh, L.out.hint, L.p.hint_pos, L.out.hint_cap, 1};
-    W.nlay = 2;
+    W.nlay = 1;
+    WArgs H = W;
+    H.w[0] = W.w[1];
+    static const int abl = [] { const char* v = getenv("BCW_ENC_ABL"); return v ? atoi(v) : 0; }();
+    static const int hg = [] { const char* v = getenv("BCW_HINT_G"); return v ? atoi(v) : 8; }();
     pr.begin(K_ENC_WRITE, st, ev0);
     k_recdesc_w<PM_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, wd);
     k_recdesc_w<PM_HINT_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag, wh);
-    k_write<<<wgrid, kWT, 0, st>>>(W);
+    // measurement-only ablation (BCW_ENC_ABL: 1 = dst WAL only, 2 = hint WAL only); 0 in the product
+    if (abl != 2) k_write<16><<<wgrid(16), kWT, 0, st>>>(W);
+    if (abl != 1) {
+      if (hg == 16) k_write<16><<<wgrid(16), kWT, 0, st>>>(H);
+      else k_write<8><<<wgrid(8), kWT, 0, st>>>(H);
+    }
     k_write_general<PM_DST><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr, s.mflag);
     k_write_general<PM_HINT_DST><<<rgrid, 256, 0, st>>>(W, 1, s.dsrc, s.da, s.dpos, s.mflag);
     pr.end(K_ENC_WRITE, st, ev0);
@@ -1135,7 +1186,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     W.nlay = 1;
     pr.begin(K_ENC_WRITE, st, ev0);
     k_recdesc_w<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, wd);
-    k_write<<<wgrid, kWT, 0, st>>>(W);
+    k_write<8><<<wgrid(8), kWT, 0, st>>>(W);
     k_write_general<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr, s.mflag);
     pr.end(K_ENC_WRITE, st, ev0);
   }
