@@ -714,6 +714,15 @@ __device__ __forceinline__ void or_masked(uint4& v, uint4 q, uint4 m) {
   v.w |= q.w & m.w;
 }
 
+// value of the next lane in the same row of 16 (lane 15: lane 0), DPP row_ror:15
+__device__ __forceinline__ uint32_t rot16(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x12f, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint64_t rot16_u64(uint64_t x) {
+  return (uint64_t)rot16((uint32_t)x) | ((uint64_t)rot16((uint32_t)(x >> 32)) << 32);
+}
+__device__ __forceinline__ uint4 rot16_u4(uint4 v) { return make_uint4(rot16(v.x), rot16(v.y), rot16(v.z), rot16(v.w)); }
+
 // per-record view for the unit assembly
 struct WRec {
   uint64_t d0;
@@ -889,6 +898,83 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
         uint64_t S = 0;
         int64_t run = -1;
         constexpr int64_t kStep = 16 * kG;
+        if constexpr (kG == 16) {
+        for (uint32_t r0 = gl; r0 - gl < nunits; r0 += kG * kWRounds) {
+          // source of the fast units: one aligned block per lane and round; the block after it is the
+          // next lane's (lane 15: lane 0's of the next round, or its own extra load in the last round),
+          // moved over with a DPP row rotation. Units whose neighbour block is not contiguous take the
+          // general path.
+          uint4 blk[kWRounds], tail = make_uint4(0, 0, 0, 0);
+          uint64_t Bq[kWRounds];
+          uint32_t shv[kWRounds];
+          bool fast[kWRounds];
+#pragma unroll
+          for (int q = 0; q < kWRounds; ++q) {
+            const uint32_t r = r0 + kG * q;
+            const int64_t z = zb + kStep * q;
+            fast[q] = false;
+            shv[q] = 0;
+            Bq[q] = ~0ull;
+            blk[q] = make_uint4(0, 0, 0, 0);
+            if (r < rlast && r != 0 && R.regular && z >= R.zA && z + 16 <= R.zB) {
+              if (run < 16) {
+                uint64_t ru;
+                S = src_at(R.d0, R.l0, e.start_off, R.mid_off + (uint64_t)(z - R.zA), ru);
+                run = (int64_t)ru;
+              }
+              if (run >= 16 && (S & ~15ull) + 32 <= e.src_len) {
+                Bq[q] = S & ~15ull;
+                blk[q] = *reinterpret_cast<const uint4*>(e.seg + Bq[q]);
+                shv[q] = (uint32_t)(S & 15u);
+                fast[q] = true;
+              }
+            } else {
+              run = -1;
+            }
+            S += kStep;
+            run -= kStep;
+          }
+          if (gl == kG - 1 && fast[kWRounds - 1]) tail = *reinterpret_cast<const uint4*>(e.seg + Bq[kWRounds - 1] + 16);
+          uint64_t nbB[kWRounds + 1];
+#pragma unroll
+          for (int q = 0; q < kWRounds; ++q) nbB[q] = rot16_u64(Bq[q]);
+#pragma unroll
+          for (int q = 0; q < kWRounds; ++q) {
+            const uint64_t nb = gl == kG - 1 ? (q + 1 < kWRounds ? nbB[q + 1] : Bq[q] + 16) : nbB[q];
+            fast[q] = fast[q] && nb == Bq[q] + 16;
+          }
+          uint4 rb[kWRounds];
+#pragma unroll
+          for (int q = 0; q < kWRounds; ++q) rb[q] = rot16_u4(blk[q]);
+#pragma unroll
+          for (int q = 0; q < kWRounds; ++q) {
+            const uint32_t r = r0 + kG * q;
+            if (r >= nunits) continue;
+            const uint64_t ua = (uf + r) << 4;
+            uint4 v;
+            int32_t b0 = 0, b1 = 16;
+            if (fast[q]) {
+              const uint4 nx = gl == kG - 1 ? (q + 1 < kWRounds ? rb[q + 1] : tail) : rb[q];
+              v = shift16(blk[q], nx, shv[q]);
+            } else {
+              b0 = ua < as ? (int32_t)(as - ua) : 0;
+              b1 = ua + 16 > ae ? (int32_t)(ae - ua) : 16;
+              v = unit_general(e, R, sl, zb + kStep * q, b0, b1);
+            }
+            uint8_t* d = reinterpret_cast<uint8_t*>((uintptr_t)ua);
+            if (b1 - b0 == 16) {
+              __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(d));
+              __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(d) + 1);
+              __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(d) + 2);
+              __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(d) + 3);
+            } else {
+              for (int32_t b = b0; b < b1; ++b) d[b] = (uint8_t)sel_byte(v, (uint32_t)b);
+            }
+            c = op_apply_s(hop, c) ^ crc_step16(t8, 0u, v);
+          }
+          zb += kStep * kWRounds;
+        }
+        } else {
         for (uint32_t r0 = gl; r0 - gl < nunits; r0 += kG * kWRounds) {
           uint4 va[kWRounds][2];
           uint32_t shv[kWRounds];
@@ -944,6 +1030,7 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
             c = op_apply_s(hop, c) ^ crc_step16(t8, 0u, v);
           }
           zb += kStep * kWRounds;
+        }
         }
         // shift each lane's chain to the end of the fragment's last unit (d < kG units follow it)
         if (gl < nunits) {
