@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
-STEPS=${STEPS:-tests,smoke,bench,prof}
+STEPS=${STEPS:-tests,smoke,bench,prof,enc}
 run() { echo "== $1 ($(date +%T))"; }
 if [[ $STEPS == *tests* ]]; then
   run tests
@@ -40,5 +40,16 @@ if [[ $STEPS == *pmc* ]]; then
       python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1 || { tail -30 "$OUT/pmc_$c.log"; exit 1; }
   done
   find "$OUT" -name "*counter_collection*" | head
+fi
+if [[ $STEPS == *enc* ]]; then
+  run enc
+  export TMPDIR=/tmp
+  timeout -k 10 400 python -u tools/bench_encode.py --records ${RECORDS:-10000000} --out "$OUT/encode_bench.json" \
+    > "$OUT/benc.log" 2>&1 || { tail -30 "$OUT/benc.log"; exit 1; }
+  tail -1 "$OUT/benc.log" | cut -c1-400
+  rm -rf "$OUT/prof_enc"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_enc" -o run --output-format csv -- \
+    python3 tools/bench_encode.py --records ${RECORDS:-10000000} --steps 3 > "$OUT/prof_enc.log" 2>&1 || { tail -30 "$OUT/prof_enc.log"; exit 1; }
+  find "$OUT/prof_enc" -name "*stats*" | head
 fi
 echo "== done ($(date +%T))"
