@@ -96,6 +96,7 @@ def _load():
         "bcw_ctx_sync": (C.c_int, [vp]),
         "bcw_ctx_device": (C.c_int, [vp]),
         "bcw_ctx_set_profiling": (C.c_int, [vp, C.c_int]),
+        "bcw_ctx_set_profiling_sample": (C.c_int, [vp, C.c_int]),
         "bcw_ctx_kernel_times": (C.c_int, [vp, C.POINTER(C.c_double), u64p, C.c_int]),
         "bcw_kernel_name": (C.c_char_p, [C.c_int]),
         "bcw_crc32c_masked": (C.c_uint32, [vp, C.c_uint64]),

@@ -438,6 +438,13 @@ int bcw_ctx_set_profiling(bcw_ctx* c, int mask) {
   return BCW_OK;
 }
 
+int bcw_ctx_set_profiling_sample(bcw_ctx* c, int every) {
+  if (!c || every < 1) return BCW_E_INVAL;
+  c->prof.every = (uint32_t)every;
+  for (uint32_t& q : c->prof.seq) q = 0;
+  return BCW_OK;
+}
+
 int bcw_ctx_kernel_times(bcw_ctx* c, double* total_ms, uint64_t* launches, int n) {
   if (!c || n < 0) return BCW_E_INVAL;
   if (hipStreamSynchronize(c->cur) != hipSuccess) return BCW_E_HIP;

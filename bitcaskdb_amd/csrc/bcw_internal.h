@@ -82,7 +82,10 @@ struct Scratch {
 enum KernelId { K_CHASE = 0, K_CRC, K_RECORDS, K_ENC_PREP, K_ENC_SCAN, K_ENC_EVENTS, K_ENC_WRITE, K_ENC_HINT_LAYOUT,
                 K_ENC_EVENTS_HINT, K_NUM };
 struct Prof {
-  uint32_t mask = 0;  // bit k: time kernel id k
+  uint32_t mask = 0;   // bit k: time kernel id k
+  uint32_t every = 1;  // time every `every`-th launch of a selected kernel
+  uint32_t seq[K_NUM] = {};
+  bool open[K_NUM] = {};
   struct Mark { int kid; hipEvent_t a, b; };
   std::vector<Mark> marks;
   std::vector<hipEvent_t> pool;
@@ -93,9 +96,13 @@ struct Prof {
     return e;
   }
   bool on(int kid) const { return (mask >> kid) & 1u; }
-  void begin(int kid, hipStream_t s, hipEvent_t& a) { if (on(kid)) { a = get(); (void)hipEventRecord(a, s); } }
+  void begin(int kid, hipStream_t s, hipEvent_t& a) {
+    open[kid] = on(kid) && (seq[kid]++ % every) == 0;
+    if (open[kid]) { a = get(); (void)hipEventRecord(a, s); }
+  }
   void end(int kid, hipStream_t s, hipEvent_t a) {
-    if (!on(kid)) return;
+    if (!open[kid]) return;
+    open[kid] = false;
     hipEvent_t b = get();
     (void)hipEventRecord(b, s);
     marks.push_back({kid, a, b});

@@ -174,6 +174,9 @@ int bcw_ctx_device(bcw_ctx* ctx);
  * bcw_ctx_kernel_times synchronises, fills total_ms[k] / launches[k] for kernel ids k < n
  * accumulated since the last call, resets, and returns the number of kernel ids. */
 int bcw_ctx_set_profiling(bcw_ctx* ctx, int mask);
+/* Time only every `every`-th launch of each selected kernel (default 1: every launch); the others
+ * run without events. */
+int bcw_ctx_set_profiling_sample(bcw_ctx* ctx, int every);
 int bcw_ctx_kernel_times(bcw_ctx* ctx, double* total_ms, uint64_t* launches, int n);
 const char* bcw_kernel_name(int kernel_id);
 
