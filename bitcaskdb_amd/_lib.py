@@ -36,7 +36,8 @@ class RecordTable(C.Structure):
 class DecodeResult(C.Structure):
     _fields_ = [("n_records", C.c_uint64), ("n_records_total", C.c_uint64), ("n_frags", C.c_uint64),
                 ("err_frag", C.c_uint64), ("err_file_off", C.c_uint64), ("err_class", C.c_int32),
-                ("first_bad_record", C.c_int32), ("n_blocks", C.c_uint64), ("retry_frag_capacity", C.c_uint64)]
+                ("first_bad_record", C.c_int32), ("n_blocks", C.c_uint64), ("retry_frag_capacity", C.c_uint64),
+                ("generation", C.c_uint64)]
 
 
 class FragTable(C.Structure):
@@ -51,7 +52,8 @@ class EncodeParams(C.Structure):
 
 
 class EncodeOut(C.Structure):
-    _fields_ = [("wal", u8p), ("wal_cap", C.c_uint64), ("hint", u8p), ("hint_cap", C.c_uint64), ("rec_off", u64p)]
+    _fields_ = [("wal", u8p), ("wal_cap", C.c_uint64), ("hint", u8p), ("hint_cap", C.c_uint64), ("rec_off", u64p),
+                ("rec_off_cap", C.c_uint64)]
 
 
 class EncodeResult(C.Structure):
@@ -77,7 +79,7 @@ ERR_NONE, ERR_CRC, ERR_TYPE, ERR_PANIC = 0, 1, 2, 3
 SB_OK, SB_SHORT, SB_CRC, SB_MAGIC, SB_BLOCKSIZE = 0, 1, 2, 3, 4
 E_CAPACITY = -4
 ENC_COMPACT, ENC_HINT = 0, 1
-ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC = 0, 1, 2, 3
+ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC, ENC_ERR_TABLE, ENC_ERR_STALE = 0, 1, 2, 3, 4, 5
 
 
 def _load():
@@ -99,6 +101,9 @@ def _load():
         "bcw_ctx_set_profiling_sample": (C.c_int, [vp, C.c_int]),
         "bcw_ctx_kernel_times": (C.c_int, [vp, C.POINTER(C.c_double), u64p, C.c_int]),
         "bcw_kernel_name": (C.c_char_p, [C.c_int]),
+        "bcw_ctx_reserve_fragments": (C.c_int, [vp, C.c_uint64]),
+        "bcw_wal_record_size": (C.c_uint64, [C.c_uint64, C.c_uint64]),
+        "bcw_wal_block_index_range": (None, [C.c_uint64, C.c_uint64, u64p, u64p, u64p]),
         "bcw_crc32c_masked": (C.c_uint32, [vp, C.c_uint64]),
         "bcw_load_super_block": (C.c_int, [vp, C.c_uint64, C.POINTER(SuperBlock)]),
         "bcw_write_super_block": (None, [vp, C.c_uint64, C.c_uint64]),

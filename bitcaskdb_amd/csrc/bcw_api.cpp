@@ -4,6 +4,7 @@
 #include <nmmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -146,6 +147,9 @@ using namespace bcw;
 
 struct bcw_ctx {
   int device = 0;
+  uint64_t id = 0;         // unique per context (high half of every decode generation)
+  uint64_t gen_seq = 0;    // decodes issued on this context
+  uint64_t frag_gen = 0;   // generation of the decode whose fragment table the scratch holds
   int num_cus = 256;
   hipStream_t own = nullptr;
   hipStream_t cur = nullptr;
@@ -175,6 +179,23 @@ struct bcw_ctx {
   do {                                     \
     if ((x) != hipSuccess) return BCW_E_HIP; \
   } while (0)
+
+namespace {
+// Every entry point that touches the device selects the context's device on the calling thread and
+// restores the caller's current device when it returns.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+std::atomic<uint64_t> g_ctx_ids{1};
+}  // namespace
 
 extern "C" {
 
@@ -233,6 +254,36 @@ int bcw_load_super_block(const uint8_t* p, uint64_t n, bcw_super_block* out) {
   return BCW_SB_OK;
 }
 
+// WalRecordSize (wal.go:61-86), same uint64 arithmetic (offset below 40 wraps as in Go)
+uint64_t bcw_wal_record_size(uint64_t offset, uint64_t size) {
+  uint64_t left = size, phy = 0;
+  offset -= BCW_SUPER_BLOCK_SIZE;
+  while (left > 0) {
+    uint64_t leftover = BCW_BLOCK_SIZE - (offset % BCW_BLOCK_SIZE);
+    if (leftover < BCW_HEADER_SIZE) {
+      phy += leftover;
+      offset += leftover;
+      leftover = BCW_BLOCK_SIZE;
+    }
+    const uint64_t frag = std::min(left, leftover - BCW_HEADER_SIZE);
+    phy += BCW_HEADER_SIZE + frag;
+    offset += BCW_HEADER_SIZE + frag;
+    left -= frag;
+  }
+  return phy;
+}
+
+// WalBlockIndexRange (wal.go:88-97)
+void bcw_wal_block_index_range(uint64_t offset, uint64_t size, uint64_t* first_blk_idx, uint64_t* first_blk_off,
+                               uint64_t* blk_num) {
+  const uint64_t rs = bcw_wal_record_size(offset, size);
+  const uint64_t first = (offset - BCW_SUPER_BLOCK_SIZE) / BCW_BLOCK_SIZE;
+  const uint64_t last = (offset - BCW_SUPER_BLOCK_SIZE + rs) / BCW_BLOCK_SIZE;
+  if (first_blk_idx) *first_blk_idx = first;
+  if (first_blk_off) *first_blk_off = first * BCW_BLOCK_SIZE + BCW_SUPER_BLOCK_SIZE;
+  if (blk_num) *blk_num = last - first + 1;
+}
+
 uint64_t bcw_max_fragments(uint64_t seg_len, uint32_t start_off) {
   if (seg_len <= start_off) return 0;
   return (seg_len - start_off) / BCW_HEADER_SIZE + 1;
@@ -247,7 +298,9 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
   bcw_ctx* c = new (std::nothrow) bcw_ctx();
   if (!c) return BCW_E_NOMEM;
   c->device = device;
-  if (hipSetDevice(device) != hipSuccess) { delete c; return BCW_E_HIP; }
+  c->id = g_ctx_ids.fetch_add(1);
+  DeviceGuard dg(device);
+  if (!dg.ok) { delete c; return BCW_E_HIP; }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->num_cus = prop.multiProcessorCount;
@@ -311,7 +364,7 @@ static void free_enc_scratch(EncScratch& e) {
 
 int bcw_ctx_destroy(bcw_ctx* c) {
   if (!c) return BCW_E_INVAL;
-  (void)hipSetDevice(c->device);
+  DeviceGuard dg(c->device);
   if (c->cur) (void)hipStreamSynchronize(c->cur);
   free_scratch(c->s);
   free_enc_scratch(c->es);
@@ -387,11 +440,15 @@ int bcw_decode_segment_async(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_
       !t->emit_frag || !t->hdr_size || !t->flags || !t->etag_off || !t->status)
     return BCW_E_INVAL;
   if (p->mode == BCW_MODE_HINT && (!t->aux0 || !t->aux1)) return BCW_E_INVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
   c->last_start_off = p->start_off;
+  const uint64_t gen = (c->id << 32) | (++c->gen_seq & 0xffffffffull);
+  c->frag_gen = gen;  // from here on the fragment scratch belongs to this decode
   bcw_decode_result r{};
   r.err_frag = ~0ull;
   r.first_bad_record = -1;
+  r.generation = gen;
   if ((uint64_t)p->start_off > p->seg_len) {
     // wal_iterator.go:49,55: bufSize < 0 -> i.buf[:bufSize] panics before any fragment
     r.err_class = BCW_ERR_PANIC;
@@ -404,9 +461,8 @@ int bcw_decode_segment_async(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_
     HIPCHK(hipMemcpyAsync(d_result, &r, sizeof r, hipMemcpyHostToDevice, c->cur));
     return BCW_OK;
   }
-  // fragment ids are u32: segments may be any size as long as they hold < 2^32 - 16 fragments (a retry
-  // that asks for more is refused)
-  if (c->frag_hint >= 0xfffffff0ull) return BCW_E_INVAL;
+  // fragment ids are u32: segments may be any size as long as they hold < 2^32 - 16 fragments
+  // (bcw_ctx_reserve_fragments refuses more)
   // first guess of the fragment count (a retry sizes it exactly): 4 KiB-class records average ~4 KiB
   // per fragment; hint WALs hold ~130 B records
   const uint64_t per = p->mode == BCW_MODE_HINT ? 96 : 256;
@@ -416,7 +472,8 @@ int bcw_decode_segment_async(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_
   want = std::min<uint64_t>(want, 0xfffffff0ull);
   int rc = ensure_scratch(c, nblocks, want);
   if (rc != BCW_OK) return rc;
-  if (launch_decode(d_seg, *p, *t, d_result, c->tabs, c->s, nblocks, c->cur, c->num_cus, &c->prof) != hipSuccess)
+  if (launch_decode(d_seg, *p, *t, d_result, c->tabs, c->s, nblocks, gen, c->cur, c->num_cus, &c->prof) !=
+      hipSuccess)
     return BCW_E_HIP;
   return BCW_OK;
 }
@@ -424,13 +481,20 @@ int bcw_decode_segment_async(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_
 int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
   if (!c || !d_frags) return BCW_E_INVAL;
   if (!c->s.misc) return BCW_OK;
-  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
   const uint64_t n = std::min(c->s.frag_cap, d_frags->capacity);
   return launch_export_frags(c->s, *d_frags, c->last_start_off, c->cur, n) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 
 static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_records", "k_enc_prep", "k_enc_scan", "k_events",
                                           "k_write", "k_hint_layout", "k_events_hint"};
+
+int bcw_ctx_reserve_fragments(bcw_ctx* c, uint64_t n) {
+  if (!c || n >= 0xfffffff0ull) return BCW_E_INVAL;
+  c->frag_hint = std::max(c->frag_hint, n);
+  return BCW_OK;
+}
 
 int bcw_ctx_set_profiling(bcw_ctx* c, int mask) {
   if (!c) return BCW_E_INVAL;
@@ -468,7 +532,8 @@ int bcw_decode_fragments(bcw_ctx* c, const bcw_frag_table* h, uint64_t* n_total)
   if (!c || !h) return BCW_E_INVAL;
   if (n_total) *n_total = 0;
   if (!c->s.misc) return BCW_OK;
-  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
   uint64_t misc[16];
   HIPCHK(hipMemcpyAsync(misc, c->s.misc, sizeof misc, hipMemcpyDeviceToHost, c->cur));
   HIPCHK(hipStreamSynchronize(c->cur));
@@ -531,7 +596,8 @@ int bcw_decode_segment(bcw_ctx* c, const uint8_t* h_seg, const bcw_decode_params
                        const bcw_record_table* h, bcw_decode_result* h_result) {
   if (!c || !p || !h || !h_result) return BCW_E_INVAL;
   if (p->seg_len && !h_seg) return BCW_E_INVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
   if (p->seg_len > c->d_seg_cap) {
     (void)hipStreamSynchronize(c->cur);
     (void)hipFree(c->d_seg);
@@ -549,7 +615,7 @@ int bcw_decode_segment(bcw_ctx* c, const uint8_t* h_seg, const bcw_decode_params
     HIPCHK(hipMemcpyAsync(h_result, c->d_result, sizeof *h_result, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(hipStreamSynchronize(c->cur));
     if (!h_result->retry_frag_capacity) break;
-    c->frag_hint = h_result->retry_frag_capacity + 64;
+    if (bcw_ctx_reserve_fragments(c, h_result->retry_frag_capacity + 64) != BCW_OK) return BCW_E_CAPACITY;
   }
   if (h_result->retry_frag_capacity) return BCW_E_NOMEM;
   const uint64_t n = std::min(h_result->n_records, h->capacity);
@@ -605,7 +671,8 @@ int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_
     return BCW_E_INVAL;
   if (!c->s.frags) return BCW_E_INVAL;  // no decode on this context yet
   if (t->capacity >= 0xffffff00ull) return BCW_E_INVAL;  // u32 dense record ids
-  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
   int rc = ensure_enc_scratch(c, t->capacity);
   if (rc != BCW_OK) return rc;
   EncLaunch L{};
@@ -621,6 +688,7 @@ int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_
   L.crc_ops = c->tabs.enc_ops;
   L.initc = c->tabs.initc;
   L.num_cus = c->num_cus;
+  L.gen = c->frag_gen;
   return launch_encode(L, c->es, c->cur, &c->prof) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 
@@ -628,7 +696,8 @@ int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params
                        uint64_t n_keep, const bcw_encode_out* h, bcw_encode_result* h_result) {
   if (!c || !p || !h || !h_result) return BCW_E_INVAL;
   if (p->src_len && !h_src) return BCW_E_INVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return BCW_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
   // decode the source (record mode) into the context's table
   bcw_super_block sb{};
   bcw_decode_params dp{};
@@ -660,7 +729,7 @@ int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params
       HIPCHK(hipMemcpyAsync(&dres, c->d_result, sizeof dres, hipMemcpyDeviceToHost, c->cur));
       HIPCHK(hipStreamSynchronize(c->cur));
       if (!dres.retry_frag_capacity) break;
-      c->frag_hint = dres.retry_frag_capacity + 64;
+      if (bcw_ctx_reserve_fragments(c, dres.retry_frag_capacity + 64) != BCW_OK) return BCW_E_CAPACITY;
     }
     if (dres.retry_frag_capacity) return BCW_E_NOMEM;
     if (dres.n_records <= c->d_tab.capacity) break;
@@ -703,12 +772,16 @@ int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params
   HIPCHK(hipMemcpyAsync(h_result, c->d_eres, sizeof *h_result, hipMemcpyDeviceToHost, c->cur));
   HIPCHK(hipStreamSynchronize(c->cur));
   if (!h_result->fits) return BCW_E_CAPACITY;
+  if (h->rec_off && h->rec_off_cap < h_result->n_in) return BCW_E_CAPACITY;
   if (h->wal && h_result->wal_need && p->mode == BCW_ENC_COMPACT)
     HIPCHK(hipMemcpyAsync(h->wal, d.wal, h_result->wal_need, hipMemcpyDeviceToHost, c->cur));
   if (h->hint && h_result->hint_need)
     HIPCHK(hipMemcpyAsync(h->hint, d.hint, h_result->hint_need, hipMemcpyDeviceToHost, c->cur));
-  const uint64_t nr = std::min(dres.n_records, rows);
+  // rows >= n_in are never written (UINT64_MAX): copy only rows the encode can have written
+  const uint64_t nr = std::min(h_result->n_in, rows);
   if (h->rec_off && nr) HIPCHK(hipMemcpyAsync(h->rec_off, d.rec_off, nr * 8, hipMemcpyDeviceToHost, c->cur));
+  if (h->rec_off)
+    for (uint64_t i = nr; i < h->rec_off_cap && i < dres.n_records; ++i) h->rec_off[i] = ~0ull;
   HIPCHK(hipStreamSynchronize(c->cur));
   return BCW_OK;
 }

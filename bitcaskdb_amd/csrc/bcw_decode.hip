@@ -1,19 +1,14 @@
 // bcw_decode.hip -- MI355X (gfx950) kernels for bitcaskDB WAL segment decode + CRC verify.
 //
-// Pipeline (one HIP stream, no host synchronisation inside; DESIGN.md "decode pipeline"):
-//   k_chase_count    one lane per 32 KiB block: header chase, workgroup scan of fragment counts
-//                    (wal_iterator.go:45-77)
-//   k_scan_wg        scan of the workgroup totals -> global fragment index of every block
-//   k_chase_write    second chase (headers now cache-resident): compact fragment table
-//   k_crc            per-fragment masked CRC-32C verify as a zero test  wal_iterator.go:79 /
-//                    utils.go:24-29 (LDS slice-by-2 tables, 128 B window per lane, lane
-//                    shift operators + segmented XOR scan across lanes)
-//   k_blocksum       per-block transform of the iterator's record state machine wal_iterator.go:69-96
-//                    + workgroup scan of the transforms
-//   k_xscan_wg       scan of the workgroup aggregates: record bases, first error
-//   k_records        record emission + RecordFromBytes / HintRecord.Decode   record.go:140-239,
-//                    hint.go:50-84, one wave per block
-//   k_finalize       bcw_decode_result
+// Pipeline (one HIP stream, no host synchronisation inside):
+//   k_chase    one lane per 32 KiB block: header chase (wal_iterator.go:45-77), workgroup scan of the
+//              fragment counts, decoupled look-back over workgroups, fragment table
+//   k_crc      one workgroup per CU: per-fragment masked CRC-32C verify as a zero test
+//              (wal_iterator.go:79 / utils.go:24-29), then the record-state transforms of the iterator's
+//              state machine (wal_iterator.go:69-96) per block, per wave, per workgroup; the last
+//              workgroup scans the workgroup aggregates (record bases, first error)
+//   k_records  record emission + RecordFromBytes (record.go:140-239) / HintRecord.Decode
+//              (hint.go:50-84), one lane per record; the last workgroup writes bcw_decode_result
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -944,10 +939,15 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     if (lane < (uint32_t)kCrcWaves) wpre[(uint64_t)blockIdx.x * kCrcWaves + lane] = lane > 0 ? prev : xf_identity();
     if (lane == (uint32_t)kCrcWaves - 1) xf_store_agent(&wgx[blockIdx.x], incl);
   }
-  // ---- the last workgroup scans the workgroup aggregates (stored with agent-scope atomics) ----
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  // ---- the last workgroup scans the workgroup aggregates ----
+  // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, row 1): the aggregate is stored with `sc1`
+  // (write-through) 8-byte stores by lane kCrcWaves-1, which waits for them (vmcnt(0)) before its
+  // agent-scope add to the one completion counter; the workgroup whose add returns last reads every
+  // aggregate with `sc1` loads (xf_load_agent). Without the wait the add can overtake a store.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   uint64_t gorder = 0;
-  if (lane == (uint32_t)kCrcWaves - 1) gorder = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_DONE_CRC]), 1ull);
+  if (lane == (uint32_t)kCrcWaves - 1)
+    gorder = __hip_atomic_fetch_add(&misc[M_DONE_CRC], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   gorder = (uint64_t)__shfl((long long)gorder, kCrcWaves - 1, 64);
   if (gorder != gridDim.x - 1u) return;
   if (lane == 0) misc[M_T_SCAN0] = wall_clock64();
@@ -1068,9 +1068,9 @@ __device__ __forceinline__ void parse_record(const bcw_decode_params& p, RecRead
   }
 }
 
-__device__ __forceinline__ void finalize(const uint64_t* __restrict__ misc, uint64_t nblocks, uint64_t frag_total,
+__device__ __forceinline__ void finalize(uint64_t* __restrict__ misc, uint64_t nblocks, uint64_t frag_total,
                            uint64_t frag_cap, const Frag* __restrict__ frags, uint32_t start_off, uint32_t tail_panic,
-                           bcw_decode_result* __restrict__ res) {
+                           uint64_t gen, bcw_decode_result* __restrict__ res) {
   bcw_decode_result r{};
   r.n_records = misc[M_NREC];
   r.n_records_total = misc[M_NREC];
@@ -1085,10 +1085,12 @@ __device__ __forceinline__ void finalize(const uint64_t* __restrict__ misc, uint
     const Frag f = frags[r.err_frag];
     r.err_file_off = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start - kHdr;
   }
-  const uint64_t fb = __hip_atomic_load(&misc[M_FIRST_BAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t fb = __hip_atomic_fetch_or(&misc[M_FIRST_BAD], 0ull, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
   r.first_bad_record = fb == ~0ull ? -1 : (int32_t)(fb < 0x7fffffffull ? fb : 0x7fffffffull);
   r.n_blocks = nblocks;
   r.retry_frag_capacity = frag_total > frag_cap ? frag_total : 0;
+  r.generation = gen;
   *res = r;
 }
 
@@ -1098,7 +1100,7 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
                                                  uint64_t frag_cap, const Xf* __restrict__ lpre,
                                                  const Xf* __restrict__ wpre, const Xf* __restrict__ wgx, uint64_t nw,
                                                  bcw_record_table tab,
-                                                 uint64_t* __restrict__ misc, uint32_t tail_panic,
+                                                 uint64_t* __restrict__ misc, uint32_t tail_panic, uint64_t gen,
                                                  bcw_decode_result* __restrict__ res) {
   __shared__ __attribute__((aligned(16))) uint8_t s_stage[kRecWaves][64][kStageArea];
   const uint32_t lane = threadIdx.x & 63u;
@@ -1224,15 +1226,15 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
   }
   } while (0);
   }
-  // the last workgroup to finish writes the segment result
+  // The last workgroup to finish writes the segment result. The finalizer reads M_FIRST_BAD, which any
+  // wave may have lowered with a no-return atomicMin: every wave waits for its own atomics to complete
+  // (vmcnt(0)) before the workgroup barrier, and only then does one lane count the workgroup done; the
+  // finalizer reads the value with an atomic (performed where the atomicMins were).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  __shared__ uint32_t s_last;
   if (threadIdx.x == 0) {
-    // the finalizer only reads counters updated by atomics (M_FIRST_BAD) or by earlier kernels, so a
-    // workgroup-scope release (this workgroup's atomics have completed) is enough before counting
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    s_last = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_DONE_REC]), 1ull) == gridDim.x - 1u;
-    if (s_last) finalize(misc, nblocks, misc[M_NFRAGS], frag_cap, frags, p.start_off, tail_panic, res);
+    const uint64_t done = __hip_atomic_fetch_add(&misc[M_DONE_REC], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1u) finalize(misc, nblocks, misc[M_NFRAGS], frag_cap, frags, p.start_off, tail_panic, gen, res);
   }
 }
 
@@ -1254,7 +1256,7 @@ __global__ void k_export_frags(const Frag* __restrict__ frags, const uint64_t* _
 // ------------------------------------------------------------------------------------------
 hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const bcw_record_table& t,
                          bcw_decode_result* d_result, const Tables& tabs, Scratch& s, uint64_t nblocks,
-                         hipStream_t stream, int num_cus, Prof* prof) {
+                         uint64_t gen, hipStream_t stream, int num_cus, Prof* prof) {
   Prof dummy;
   Prof& pr = prof ? *prof : dummy;
   hipEvent_t ev = nullptr;
@@ -1280,7 +1282,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   if (rec_wgs > (uint64_t)num_cus * 2) rec_wgs = (uint64_t)num_cus * 2;
   k_records<<<(uint32_t)rec_wgs, 64 * kRecWaves, 0, stream>>>(
       d_seg, p.seg_len, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg, s.wgx, nw, t, s.misc, tail_panic,
-      d_result);
+      gen, d_result);
   pr.end(K_RECORDS, stream, ev);
   return hipGetLastError();
 }

@@ -50,6 +50,7 @@ enum {
   X_ERR = 1,      // min over rows of (row << 2 | class) of Record.Encode failures
   X_SRCERR = 2,   // source error class (BCW_ENC_ERR_SRC when iteration stopped on a bad row / fragment)
   X_NDENSE = 3,   // records written
+  X_FAIL = 4,     // BCW_ENC_ERR_TABLE / BCW_ENC_ERR_STALE: the source inputs are unusable, nothing encoded
   X_LAY = 8,      // per layout (wal: 8, hint: 16): +0 A_N, +1 nev, +2 k_end, +3 end, +4 b0, +5 U, +6 ok
 };
 constexpr int kLayStride = 8;
@@ -115,6 +116,7 @@ struct EncDev {
   const bcw_decode_result* sres;
   const uint8_t* keep;
   uint64_t dst_base, fid;
+  uint64_t gen;  // generation of the context's latest decode (its fragment table is `frags`)
   uint32_t start_off, mode, ns, etag;
 };
 
@@ -131,14 +133,18 @@ __global__ __launch_bounds__(256) void k_enc_prep(EncDev e, uint64_t rows, uint3
   const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
   const bcw_decode_result* R = e.sres;
   const uint64_t nrec = R->n_records;
-  const uint64_t nin = (R->first_bad_record >= 0 && (uint64_t)R->first_bad_record < nrec)
+  // the source must be the context's latest decode (its fragment table) and fit the table
+  const uint32_t fail = R->generation != e.gen ? BCW_ENC_ERR_STALE : nrec > rows ? BCW_ENC_ERR_TABLE : 0u;
+  const uint64_t nin = fail ? 0
+                       : (R->first_bad_record >= 0 && (uint64_t)R->first_bad_record < nrec)
                            ? (uint64_t)R->first_bad_record : nrec;
   if (i == 0) {
     emisc[X_NIN] = nin;
-    emisc[X_SRCERR] = (nin < nrec || R->err_class != BCW_ERR_NONE) ? 1u : 0u;
+    emisc[X_FAIL] = fail;
+    emisc[X_SRCERR] = (!fail && (nin < nrec || R->err_class != BCW_ERR_NONE)) ? 1u : 0u;
   }
   if (i >= rows) return;
-  if (rec_off && i < nrec) rec_off[i] = ~0ull;
+  if (rec_off && i < nrec && !fail) rec_off[i] = ~0ull;
   if (i >= nin) { sz[i] = 0; return; }
   const bcw_record_table& t = e.t;
   const uint64_t klen = t.key_len[i];
@@ -1143,7 +1149,9 @@ __global__ void k_enc_finalize(const uint64_t* __restrict__ emisc, uint32_t mode
   o.n_written = emisc[X_NDENSE];
   o.err_record = -1;
   o.src_err_class = sres->err_class;
-  if ((err >> 2) < nin) {
+  if (emisc[X_FAIL]) {
+    o.err_class = (int32_t)emisc[X_FAIL];
+  } else if ((err >> 2) < nin) {
     o.err_class = (int32_t)(err & 3u);
     o.err_record = (int64_t)(err >> 2);
     o.n_in = err >> 2;  // the callback error stops the iteration there
@@ -1187,6 +1195,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
   e.mode = L.p.mode;
   e.ns = L.p.ns_size;
   e.etag = L.p.etag_size;
+  e.gen = L.gen;
   const uint64_t rows = L.rows;
   const bool compact = L.p.mode == BCW_ENC_COMPACT;
   TileSum* tiles = static_cast<TileSum*>(s.tiles);

@@ -112,7 +112,7 @@ struct Prof {
 // Launch the full decode pipeline on `stream`. Defined in bcw_decode.hip.
 hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const bcw_record_table& t,
                          bcw_decode_result* d_result, const Tables& tabs, Scratch& s, uint64_t nblocks,
-                         hipStream_t stream, int num_cus, Prof* prof);
+                         uint64_t gen, hipStream_t stream, int num_cus, Prof* prof);
 hipError_t launch_export_frags(const Scratch& s, const bcw_frag_table& out, uint32_t start_off, hipStream_t stream,
                                uint64_t n);
 
@@ -148,6 +148,7 @@ struct EncLaunch {
   const uint32_t* crc_ops;
   const uint32_t* initc;
   int num_cus;
+  uint64_t gen;  // generation of the context's latest decode (the owner of `frags`)
 };
 
 hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t stream, Prof* prof);

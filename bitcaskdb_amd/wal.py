@@ -153,7 +153,7 @@ class Context:
             hint = np.zeros(max(hcap, 1), dtype=np.uint8)
             offs = np.full(nrows, np.iinfo(np.uint64).max, dtype=np.uint64)
             out = L.EncodeOut(wal.ctypes.data_as(L.u8p), wcap, hint.ctypes.data_as(L.u8p), hcap,
-                              offs.ctypes.data_as(L.u64p))
+                              offs.ctypes.data_as(L.u64p), nrows)
             res = L.EncodeResult()
             rc = L.lib.bcw_encode_segment(self._h, src.ctypes.data_as(C.c_void_p) if n else None, C.byref(p),
                                           keep.ctypes.data_as(C.c_void_p) if keep.size else None, keep.size,
@@ -161,6 +161,7 @@ class Context:
             if rc == L.E_CAPACITY:
                 wcap = max(wcap, int(res.wal_need))
                 hcap = max(hcap, int(res.hint_need))
+                nrows = max(nrows, int(res.n_in))
                 continue
             if rc != 0:
                 raise RuntimeError(f"bcw_encode_segment: {L.lib.bcw_strerror(rc).decode()}")
@@ -396,6 +397,29 @@ def _src_error(res, dec_class, status):
     return _frag_error(type("R", (), {"err_class": dec_class})())
 
 
+def _encode_fails(expire: int, dst_base: int) -> bool:
+    """Record.Encode (record.go:63-78) fails on this row: "invalid expire" or the 5-byte varint panic."""
+    return expire != 0 and (expire < dst_base or expire - dst_base >= 1 << 35)
+
+
+def _filter_rows(src: Wal, flt, dst_base: int, ns_size: int, etag_size: int, ctx: Context) -> np.ndarray:
+    """The keep mask of compactOneWal's loop (compaction.go:299-311) with a doFilter callback, called in
+    record order exactly as the reference calls it: not for rows at or after the first row
+    RecordFromBytes rejects, and not after the first kept row whose Record.Encode fails."""
+    dec = ctx.decode(src.data, src.start_off, src.base_time, ns_size, etag_size, L.MODE_RECORD, with_frags=True)
+    t = dec.table
+    rows = []
+    for r in range(dec.n_records):
+        if int(t["status"][r]) != L.ST_OK:
+            break
+        rec = _record_of(dec, r, dec.record_bytes(r))
+        k = not flt(rec, src.fid, int(t["foff"][r]) - HEADER)
+        rows.append(k)
+        if k and _encode_fails(int(t["expire"][r]), dst_base):
+            break
+    return np.array(rows, dtype=np.uint8)
+
+
 def compact_one_wal(dst: WalFile, hint: WalFile, src: Wal, keep, ns_size: int = 20, etag_size: int = 20,
                     ctx: Context | None = None):
     """compactOneWal (compaction.go:294-327): every delivered source record with keep[i] (the doFilter
@@ -404,13 +428,7 @@ def compact_one_wal(dst: WalFile, hint: WalFile, src: Wal, keep, ns_size: int = 
     after appending what the reference appends before it."""
     ctx = ctx or default_context()
     if callable(keep):  # doFilter(record, fid, off) -> True drops the record (compaction.go:329-348)
-        rows = []
-        try:
-            iterate_record(src, lambda r, foff, size: rows.append(not keep(r, src.fid, foff - HEADER)),
-                           ns_size, etag_size, ctx)
-        except WalError:
-            pass  # raised again below, after the records before it are appended
-        keep = np.array(rows, dtype=np.uint8)
+        keep = _filter_rows(src, keep, dst.base_time, ns_size, etag_size, ctx)
     res, wal, hb, offs = ctx.encode(src.data, L.ENC_COMPACT, src.start_off, dst.base_time, dst.fid, dst.size(),
                                     hint.size(), ns_size, etag_size, keep)
     dst.data += wal

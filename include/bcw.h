@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define BCW_ABI_VERSION 1
+#define BCW_ABI_VERSION 2
 
 /* ---- return codes ---- */
 #define BCW_OK 0
@@ -140,8 +140,12 @@ typedef struct bcw_decode_result {
   int32_t first_bad_record; /* first row < n_records with status != OK, or -1 (capped at INT32_MAX) */
   uint64_t n_blocks;
   /* != 0: the context's fragment scratch was too small for this segment; the outputs are invalid.
-   * The next call on this context sizes its scratch to this value (the sync API retries itself). */
+   * Call bcw_ctx_reserve_fragments(ctx, retry_frag_capacity) and decode again (the sync API does
+   * this itself). */
   uint64_t retry_frag_capacity;
+  /* decode generation (unique per context and call): bcw_encode_segment_async checks that the result
+   * it is given belongs to the context's latest decode, whose fragment table it reads */
+  uint64_t generation;
 } bcw_decode_result;
 
 /* Fragment table (device arrays, `capacity` entries, global fragment order). */
@@ -179,6 +183,9 @@ int bcw_ctx_set_profiling(bcw_ctx* ctx, int mask);
 int bcw_ctx_set_profiling_sample(bcw_ctx* ctx, int every);
 int bcw_ctx_kernel_times(bcw_ctx* ctx, double* total_ms, uint64_t* launches, int n);
 const char* bcw_kernel_name(int kernel_id);
+/* Size the context's fragment scratch for at least n fragments on the next decode (after a decode
+ * reported retry_frag_capacity). n must be < 2^32 - 16 (BCW_E_INVAL otherwise, nothing stored). */
+int bcw_ctx_reserve_fragments(bcw_ctx* ctx, uint64_t n);
 
 /* ---- host helpers (no device work) ---- */
 uint32_t bcw_crc32c_masked(const uint8_t* p, uint64_t n);
@@ -186,6 +193,14 @@ int bcw_load_super_block(const uint8_t* p, uint64_t n, bcw_super_block* out);
 void bcw_write_super_block(uint8_t out[40], uint64_t create_time, uint64_t base_time);
 /* Upper bound of records / fragments a segment of seg_len bytes can hold. */
 uint64_t bcw_max_fragments(uint64_t seg_len, uint32_t start_off);
+/* WalRecordSize (wal.go:61-86): physical footprint (headers, data and any padding the writer puts
+ * inside the record's span) of a size-byte payload whose first header is at file offset `offset`
+ * (offset >= 40; the reference's uint64 arithmetic wraps below, so does this). */
+uint64_t bcw_wal_record_size(uint64_t offset, uint64_t size);
+/* WalBlockIndexRange (wal.go:88-97): first block index, its file offset, and the number of blocks the
+ * record's span touches (uint64 arithmetic as in the reference). */
+void bcw_wal_block_index_range(uint64_t offset, uint64_t size, uint64_t* first_blk_idx, uint64_t* first_blk_off,
+                               uint64_t* blk_num);
 
 /* ---- decode ----
  * Async, device-resident: d_seg is a device pointer to the whole file image (super block
@@ -225,6 +240,9 @@ int bcw_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_t seed
 #define BCW_ENC_ERR_EXPIRE 2 /* Record.Encode: errors.New("invalid expire") (record.go:74) at err_record */
 #define BCW_ENC_ERR_PANIC 3  /* Record.Encode panics at err_record: expire delta >= 2^35 overflows
                                 `var expireBytes [binary.MaxVarintLen32]byte` (record.go:67,78) */
+#define BCW_ENC_ERR_TABLE 4  /* the source table is smaller than the decode's n_records: nothing encoded */
+#define BCW_ENC_ERR_STALE 5  /* d_src_result is not the context's latest decode (its fragment table was
+                                replaced, e.g. by a hint decode): nothing encoded */
 
 typedef struct bcw_encode_params {
   uint64_t src_len;       /* source WAL file size */
@@ -239,15 +257,18 @@ typedef struct bcw_encode_params {
 } bcw_encode_params;
 
 /* Outputs. wal / hint receive the bytes appended to each file: out[0] is file offset wal_pos /
- * hint_pos (the super block of a new file is bcw_write_super_block's job). rec_off (one per
- * source table row, may be NULL): the offset WriteRecord returned for the row's record in the
- * dst WAL, UINT64_MAX when not written. Device pointers for the async API, host for the sync one. */
+ * hint_pos (the super block of a new file is bcw_write_super_block's job). rec_off (may be NULL):
+ * per source row, the offset WriteRecord returned for the row's record in the dst WAL, UINT64_MAX
+ * when not written. Async API: device arrays; rec_off has the source table's capacity (rec_off_cap is
+ * ignored). Sync API: host arrays; rec_off has rec_off_cap entries, rows >= n_in are never written,
+ * and BCW_E_CAPACITY is returned (result filled, nothing copied) when rec_off_cap < n_in. */
 typedef struct bcw_encode_out {
   uint8_t* wal;
   uint64_t wal_cap;
   uint8_t* hint;
   uint64_t hint_cap;
   uint64_t* rec_off;
+  uint64_t rec_off_cap;
 } bcw_encode_out;
 
 typedef struct bcw_encode_result {
@@ -268,14 +289,15 @@ typedef struct bcw_encode_result {
 
 /* Async, device-resident. d_src / d_table / d_src_result must be the inputs and outputs of the most
  * recent bcw_decode_segment_async (BCW_MODE_RECORD) on this context: the encode reads the context's
- * fragment table. d_keep[i] != 0 keeps source row i (the doFilter verdict, compaction.go:303;
+ * fragment table, and reports BCW_ENC_ERR_STALE (nothing written) when d_src_result->generation is not
+ * that decode's. d_keep[i] != 0 keeps source row i (the doFilter verdict, compaction.go:303;
  * ignored for BCW_ENC_HINT). Launches on the context stream; d_result (device) receives the outcome. */
 int bcw_encode_segment_async(bcw_ctx* ctx, const uint8_t* d_src, const bcw_encode_params* p,
                              const bcw_record_table* d_table, const bcw_decode_result* d_src_result,
                              const uint8_t* d_keep, const bcw_encode_out* d_out, bcw_encode_result* d_result);
 /* Synchronous, host in / host out: decodes h_src, then encodes (n_keep entries of h_keep, missing
  * ones count as dropped). Returns BCW_E_CAPACITY (result filled, nothing copied) when an output is
- * too small: h_result->wal_need / hint_need tell the sizes. */
+ * too small: h_result->wal_need / hint_need / n_in tell the sizes. */
 int bcw_encode_segment(bcw_ctx* ctx, const uint8_t* h_src, const bcw_encode_params* p, const uint8_t* h_keep,
                        uint64_t n_keep, const bcw_encode_out* h_out, bcw_encode_result* h_result);
 

@@ -704,3 +704,95 @@ oc_writer* oc_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_
   free(ns); free(key); free(val); free(rec);
   return w;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* framing size maths: wal.go:61-97                                                            */
+/* ------------------------------------------------------------------------------------------ */
+uint64_t oc_wal_record_size(uint64_t offset, uint64_t size) {
+  /* WalRecordSize (wal.go:61-86): uint64 arithmetic, `offset -= SuperBlockSize` wraps below 40 */
+  uint64_t left = size, phy = 0;
+  offset -= OC_SUPER_SIZE;
+  while (left > 0) {
+    uint64_t leftover = OC_BLOCK_SIZE - (offset % OC_BLOCK_SIZE);
+    if (leftover < OC_HEADER_SIZE) {
+      phy += leftover;
+      offset += leftover;
+      leftover = OC_BLOCK_SIZE;
+    }
+    uint64_t avail = leftover - OC_HEADER_SIZE;
+    uint64_t frag = left < avail ? left : avail;
+    phy += OC_HEADER_SIZE + frag;
+    offset += OC_HEADER_SIZE + frag;
+    left -= frag;
+  }
+  return phy;
+}
+
+void oc_wal_block_index_range(uint64_t offset, uint64_t size, uint64_t* first_idx, uint64_t* first_off,
+                              uint64_t* blk_num) {
+  /* WalBlockIndexRange (wal.go:88-97) */
+  uint64_t rs = oc_wal_record_size(offset, size);
+  *first_idx = (offset - OC_SUPER_SIZE) / OC_BLOCK_SIZE;
+  *first_off = *first_idx * OC_BLOCK_SIZE + OC_SUPER_SIZE;
+  uint64_t last = (offset - OC_SUPER_SIZE + rs) / OC_BLOCK_SIZE;
+  *blk_num = last - *first_idx + 1;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* payload hashes for full-size parity checks (test infrastructure)                            */
+/* ------------------------------------------------------------------------------------------ */
+static uint64_t oc_hash_bytes(uint64_t h, const uint8_t* p, uint64_t n) {
+  /* 64-bit multiply-rotate over 8-byte words; the length is mixed in by the caller */
+  uint64_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, p + i, 8);
+    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+    h = (h << 27) | (h >> 37);
+  }
+  if (i < n) {
+    uint64_t w = 0;
+    memcpy(&w, p + i, (size_t)(n - i));
+    h = (h ^ w ^ ((n - i) << 56)) * 0xC2B2AE3D27D4EB4Full;
+    h = (h << 31) | (h >> 33);
+  }
+  return h;
+}
+
+/* hash of every record payload of an oracle decode */
+void oc_decode_payload_hashes(const oc_decode* d, uint64_t* out) {
+  for (uint64_t r = 0; r < d->n_recs; ++r) {
+    uint64_t n = d->byte_offs[r + 1] - d->byte_offs[r];
+    out[r] = oc_hash_bytes(0x5EEDull ^ n, d->bytes + d->byte_offs[r], n);
+  }
+}
+
+/* the same hash over payloads gathered from a (device-produced) fragment table: record r's bytes are
+ * the data of fragments [first[r], emit[r]] (data_off / flen per fragment); the words are streamed
+ * across fragment boundaries exactly as over the concatenation */
+void oc_gather_payload_hashes(const uint8_t* seg, uint64_t seg_len, const uint64_t* data_off, const uint32_t* flen,
+                              uint64_t n_frags, const uint32_t* first, const uint32_t* emit, const uint64_t* size,
+                              uint64_t n_recs, uint64_t* out) {
+  uint8_t* tmp = NULL;
+  uint64_t cap = 0;
+  for (uint64_t r = 0; r < n_recs; ++r) {
+    uint64_t f0 = first[r], f1 = emit[r];
+    if (f1 >= n_frags || f0 > f1) { out[r] = 0; continue; }
+    if (f0 == f1) {
+      uint64_t o = data_off[f0], n = flen[f0];
+      out[r] = (o + n <= seg_len) ? oc_hash_bytes(0x5EEDull ^ n, seg + o, n) : 0;
+      continue;
+    }
+    uint64_t n = size[r];
+    if (n > cap) { cap = n * 2 + 64; tmp = (uint8_t*)realloc(tmp, cap); }
+    uint64_t w = 0;
+    for (uint64_t g = f0; g <= f1 && w <= n; ++g) {
+      uint64_t o = data_off[g], l = flen[g];
+      if (o + l > seg_len || w + l > n) { w = n + 1; break; }
+      memcpy(tmp + w, seg + o, l);
+      w += l;
+    }
+    out[r] = (w == n) ? oc_hash_bytes(0x5EEDull ^ n, tmp, n) : 0;
+  }
+  free(tmp);
+}

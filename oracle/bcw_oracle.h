@@ -156,6 +156,17 @@ void oc_hint_by_wal(oc_writer* hint, uint64_t fid, const uint8_t* seg, uint64_t 
 oc_writer* oc_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_t seed, uint32_t ns_size,
                             uint32_t key_len, uint32_t value_len, int value_mode, uint64_t base_time);
 
+/* ---- framing size maths (wal.go:61-97) ---- */
+uint64_t oc_wal_record_size(uint64_t offset, uint64_t size);
+void oc_wal_block_index_range(uint64_t offset, uint64_t size, uint64_t* first_idx, uint64_t* first_off,
+                              uint64_t* blk_num);
+
+/* ---- payload hashes for full-size parity checks ---- */
+void oc_decode_payload_hashes(const oc_decode* d, uint64_t* out);
+void oc_gather_payload_hashes(const uint8_t* seg, uint64_t seg_len, const uint64_t* data_off, const uint32_t* flen,
+                              uint64_t n_frags, const uint32_t* first, const uint32_t* emit, const uint64_t* size,
+                              uint64_t n_recs, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

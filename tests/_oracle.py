@@ -73,6 +73,14 @@ lib.oc_hint_by_wal.argtypes = [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, C.c_u
                                _i32p, _i64p, _u64p]
 lib.oc_meta_app_size_zero.restype = C.c_int
 lib.oc_meta_app_size_zero.argtypes = [vp, C.c_size_t]
+lib.oc_wal_record_size.restype = C.c_uint64
+lib.oc_wal_record_size.argtypes = [C.c_uint64, C.c_uint64]
+lib.oc_wal_block_index_range.restype = None
+lib.oc_wal_block_index_range.argtypes = [C.c_uint64, C.c_uint64, _u64p, _u64p, _u64p]
+lib.oc_decode_payload_hashes.restype = None
+lib.oc_decode_payload_hashes.argtypes = [vp, vp]
+lib.oc_gather_payload_hashes.restype = None
+lib.oc_gather_payload_hashes.argtypes = [vp, C.c_uint64, vp, vp, C.c_uint64, vp, vp, vp, C.c_uint64, vp]
 lib.oc_synth_segment.restype = vp
 lib.oc_synth_segment.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
                                  C.c_uint64]
@@ -145,12 +153,13 @@ def hint_encode(ns: bytes, key: bytes, fid: int, off: int, size: int) -> bytes:
 
 
 class Decoded:
-    def __init__(self, frags, recs, err_frag, err_class, payloads):
+    def __init__(self, frags, recs, err_frag, err_class, payloads, hashes=None):
         self.frags, self.recs, self.err_frag, self.err_class, self.payloads = frags, recs, err_frag, err_class, payloads
+        self.hashes = hashes
 
 
 def decode(seg, start_off: int, base_time: int, ns_size: int, etag_size: int, mode: int = 0,
-           want_bytes: bool = True) -> Decoded:
+           want_bytes: bool = True, want_hashes: bool = False) -> Decoded:
     seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
     h = lib.oc_decode_segment(_ptr(seg), seg.size, start_off, base_time, ns_size, etag_size, mode)
     nf, nr, ef, nb = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
@@ -168,8 +177,39 @@ def decode(seg, start_off: int, base_time: int, ns_size: int, etag_size: int, mo
         offs = np.zeros(nr.value + 1, dtype=np.uint64)
         lib.oc_decode_bytes(h, buf.ctypes.data_as(vp), offs.ctypes.data_as(vp))
         payloads = [bytes(buf[offs[i]:offs[i + 1]]) for i in range(nr.value)]
+    hashes = None
+    if want_hashes:
+        hashes = np.zeros(max(nr.value, 1), dtype=np.uint64)
+        lib.oc_decode_payload_hashes(h, hashes.ctypes.data_as(vp))
+        hashes = hashes[:nr.value]
     lib.oc_decode_free(h)
-    return Decoded(frags, recs, int(ef.value), int(ec.value), payloads)
+    return Decoded(frags, recs, int(ef.value), int(ec.value), payloads, hashes)
+
+
+def gather_payload_hashes(seg, frags: dict, table: dict) -> np.ndarray:
+    """Hash of every record payload gathered from a (device) fragment + record table, comparable with
+    decode(..., want_hashes=True).hashes."""
+    seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+    d_off = np.ascontiguousarray(frags["data_off"], dtype=np.uint64)
+    f_len = np.ascontiguousarray(frags["len"], dtype=np.uint32)
+    first = np.ascontiguousarray(table["first_frag"], dtype=np.uint32)
+    emit = np.ascontiguousarray(table["emit_frag"], dtype=np.uint32)
+    size = np.ascontiguousarray(table["size"], dtype=np.uint64)
+    n = int(first.size)
+    out = np.zeros(max(n, 1), dtype=np.uint64)
+    lib.oc_gather_payload_hashes(_ptr(seg), seg.size, _ptr(d_off), _ptr(f_len), d_off.size, _ptr(first), _ptr(emit),
+                                 _ptr(size), n, out.ctypes.data_as(vp))
+    return out[:n]
+
+
+def wal_record_size(offset: int, size: int) -> int:
+    return int(lib.oc_wal_record_size(offset, size))
+
+
+def wal_block_index_range(offset: int, size: int):
+    a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    lib.oc_wal_block_index_range(offset, size, C.byref(a), C.byref(b), C.byref(c))
+    return int(a.value), int(b.value), int(c.value)
 
 
 def decode_fast(seg, start_off, base_time, ns_size, etag_size):

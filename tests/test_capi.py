@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
     assert len(syms) >= 15
     for name in syms:
         assert hasattr(L.lib, name), f"libbcw.so does not export {name}"
-    assert L.lib.bcw_abi_version() == 1
+    assert L.lib.bcw_abi_version() == 2
     assert L.lib.bcw_strerror(-4) == b"output capacity too small"
 
 
@@ -73,3 +73,37 @@ def test_max_fragments():
     assert L.lib.bcw_max_fragments(40, 40) == 0
     assert L.lib.bcw_max_fragments(47, 40) == 2
     assert L.lib.bcw_max_fragments(40 + 32768, 40) == 32768 // 7 + 1
+
+
+def test_wal_record_size_and_block_range():
+    """WalRecordSize / WalBlockIndexRange (wal.go:61-97) through the C-ABI against the oracle, and against
+    the physical span the writer (wal.go:490-553) actually gives each record."""
+    rng = random.Random(5)
+    cases = [(40, 0), (40, 1), (40, 32761), (40, 32762), (32768 + 40 - 7, 10), (32768 + 40 - 6, 10),
+             (32768 + 40 - 8, 1), (100, 200000), (2**40 + 40, 70000)]
+    cases += [(40 + rng.randrange(0, 1 << 20), rng.choice([0, 1, 5, 4222, 32761, rng.randrange(0, 300000)]))
+              for _ in range(300)]
+    for off, size in cases:
+        assert L.lib.bcw_wal_record_size(off, size) == O.wal_record_size(off, size), (off, size)
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        L.lib.bcw_wal_block_index_range(off, size, C.byref(a), C.byref(b), C.byref(c))
+        assert (a.value, b.value, c.value) == O.wal_block_index_range(off, size), (off, size)
+    # the footprint of every record the writer appends = the bytes from its offset to the next record's
+    # first header or the padding before it (WalRecordSize counts no padding at the record start)
+    w = O.Writer(1, 1)
+    offs, sizes = [], []
+    for i in range(400):
+        n = rng.choice([5, 4222, 32761 - 7, 32761, 32754, rng.randrange(5, 70000)])
+        offs.append(w.write(bytes(n)))
+        sizes.append(n)
+    end = w.size()
+    for i, (off, n) in enumerate(zip(offs, sizes)):
+        rs = int(L.lib.bcw_wal_record_size(off, n))
+        nxt = offs[i + 1] if i + 1 < len(offs) else end
+        pad = (32768 - (off + rs - 40) % 32768) if (off + rs - 40) % 32768 > 32768 - 7 else 0
+        assert off + rs == nxt or off + rs + pad == nxt, (i, off, n, rs, nxt)
+
+
+def test_reserve_fragments_rejects_oversize():
+    # no device needed: the call only records a sizing hint (ctx NULL is refused)
+    assert L.lib.bcw_ctx_reserve_fragments(None, 10) == -1

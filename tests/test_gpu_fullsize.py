@@ -1,0 +1,128 @@
+"""Full-size GPU parity: the benchmark configurations themselves (BASELINE.json configs A, B, C and E),
+decoded / encoded on the MI355X through the C-ABI and compared with the CPU oracle column by column.
+
+At these sizes every k_crc wave owns many 32 KiB blocks (config B: ~10.7 per wave), the k_chase
+look-back crosses many workgroups and the last-workgroup scans run over all 256 aggregates -- the
+regimes the small parity tests never reach. Record payloads are compared through a 64-bit hash of the
+bytes gathered from the device fragment table (oracle/bcw_oracle.c oc_gather_payload_hashes) against
+the same hash of the oracle's own payloads."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import cases
+from bitcaskdb_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+BASE = cases.BASE
+
+
+def full_parity(ctx, data, p, name):
+    ref = O.decode(data, p["start_off"], p["base_time"], p["ns_size"], p["etag_size"], p["mode"], want_bytes=False,
+                   want_hashes=True)
+    seg = np.frombuffer(data, dtype=np.uint8)
+    got = ctx.decode(seg, p["start_off"], p["base_time"], p["ns_size"], p["etag_size"], p["mode"], with_frags=True)
+    res = got.result
+    assert res.err_class == ref.err_class, (name, res.err_class, ref.err_class)
+    if ref.err_class in (L.ERR_CRC, L.ERR_TYPE):
+        assert res.err_frag == ref.err_frag, (name, res.err_frag, ref.err_frag)
+    assert res.n_records == len(ref.recs), (name, res.n_records, len(ref.recs))
+    nf = len(ref.frags)
+    gf = got.frags
+    assert len(gf["data_off"]) >= nf
+    for col in ("data_off", "len", "stored_crc", "type", "crc_ok"):
+        np.testing.assert_array_equal(gf[col][:nf], ref.frags[col], err_msg=f"{name}: frag {col}")
+    t, r = got.table, ref.recs
+    for col in ("foff", "size", "first_frag", "emit_frag", "status", "hdr_size", "flags", "etag_off", "expire"):
+        np.testing.assert_array_equal(t[col].astype(np.uint64), r[col].astype(np.uint64), err_msg=f"{name}: {col}")
+    if p["mode"] == 0:
+        for col in ("key_len", "val_len", "meta_len"):
+            np.testing.assert_array_equal(t[col].astype(np.uint64), r[col] & 0xFFFFFFFF, err_msg=f"{name}: {col}")
+    else:
+        np.testing.assert_array_equal(t["aux0"], r["val_len"], err_msg=f"{name}: hint off")
+        np.testing.assert_array_equal(t["aux1"], r["meta_len"], err_msg=f"{name}: hint size")
+    h = O.gather_payload_hashes(seg, gf, t)
+    bad = np.nonzero(h != ref.hashes)[0]
+    assert bad.size == 0, f"{name}: {bad.size} payloads differ, first at record {bad[:1]}"
+    st = np.nonzero(r["status"] != 0)[0]
+    assert res.first_bad_record == (int(st[0]) if len(st) else -1)
+    return got, ref
+
+
+def test_config_a_64mib(ctx):
+    """config A: one 64 MiB segment, 100 B keys / 4 KiB values (15,868 records)."""
+    data = O.synth(64 << 20, 0, 0x5EED)
+    got, _ = full_parity(ctx, data, cases.params(), "A")
+    assert got.n_records == 15868 and got.result.err_class == 0
+
+
+@pytest.fixture(scope="module")
+def config_b():
+    return O.synth(1 << 30, 0, 42)
+
+
+def test_config_b_1gib(ctx, config_b):
+    """config B: 1 GiB, 4 KiB values (253,899 records, 32,775 blocks, ~10.7 blocks per k_crc wave)."""
+    got, ref = full_parity(ctx, config_b, cases.params(), "B")
+    assert got.n_records == 253899 and got.result.err_class == 0
+    assert got.result.n_blocks == 32775
+
+
+@pytest.mark.parametrize("where", [0.5, 0.97, 0.9999])
+def test_config_b_corruption(ctx, config_b, where):
+    """one flipped byte in the middle / last workgroups' ranges of a 1 GiB segment: the same first failing
+    fragment, error class, delivered records and their payloads."""
+    bad = bytearray(config_b)
+    pos = int(len(bad) * where)
+    bad[pos] ^= 0x5A
+    got, ref = full_parity(ctx, bytes(bad), cases.params(), f"B flip@{pos}")
+    assert got.result.err_class in (L.ERR_CRC, L.ERR_TYPE)
+    assert 0 < got.n_records < 253899
+
+
+def test_config_c_1gib_zipf(ctx):
+    """config C: 1 GiB, Zipf(1.1) 128 B - 64 KiB values (spanning records, zero-length Firsts, pads)."""
+    data = O.synth(1 << 30, 0, 42, value_mode=1)
+    got, ref = full_parity(ctx, data, cases.params(), "C")
+    assert got.result.err_class == 0 and got.n_records > 100000
+
+
+def test_dense_fragments_256mib(ctx):
+    """~230 fragments per block over 256 MiB (1.9 M fragments, several blocks per k_crc wave, a
+    fragment-table retry)."""
+    data = O.synth(256 << 20, 0, 21, 20, 100, 10, 0)
+    got, _ = full_parity(ctx, data, cases.params(), "dense256")
+    assert got.result.err_class == 0
+
+
+def test_hint_wal_fullsize(ctx):
+    """the hint WAL of a 1 GiB config-C data WAL, decoded in hint mode (IterateHint)."""
+    data = O.synth(1 << 30, 0, 43, value_mode=1)
+    ec, _, _, hint = O.hint_by_wal(data, 3, 40, BASE, 20, 20)
+    assert ec == 0
+    full_parity(ctx, hint, cases.params(mode=1), "hint-C")
+
+
+def test_config_e_compaction_200k(ctx):
+    """config E shape at 200,000 records (845 MB source): compaction re-encode and hint rebuild,
+    dst WAL + hint WAL bytes and the returned offsets bit-exact against oc_compact_append /
+    oc_hint_by_wal; a dst baseTime below the source's re-bases every expire-less record identically."""
+    n = 200000
+    src = O.synth(1 << 40, n, 42)
+    rng = np.random.default_rng(3)
+    keep = (rng.random(n) < 0.9).astype(np.uint8)
+    dst, hint = O.Writer(BASE, BASE), O.Writer(BASE, BASE)
+    ec, er, nin, offs = O.compact_append(dst, hint, 9, src, 40, BASE, BASE, 20, 20, keep)
+    assert ec == 0 and nin == n
+    res, wal, hb, goffs = ctx.encode(src, L.ENC_COMPACT, 40, BASE, 9, 40, 40, 20, 20, keep)
+    assert res.err_class == 0 and res.n_in == n and res.n_written == int(keep.sum())
+    assert wal == dst.data()[40:], "dst WAL differs"
+    assert hb == hint.data()[40:], "hint WAL differs"
+    np.testing.assert_array_equal(goffs[:n], offs[:n])
+    # hint rebuild of the same source (NewHintByWal)
+    ec2, _, nin2, ref_hint = O.hint_by_wal(src, 5, 40, BASE, 20, 20)
+    res2, _, hb2, _ = ctx.encode(src, L.ENC_HINT, 40, BASE, 5, 40, 40, 20, 20)
+    assert res2.err_class == ec2 == 0 and res2.n_in == nin2 == n
+    assert hb2 == ref_hint[40:], "hint-by-wal bytes differ"
