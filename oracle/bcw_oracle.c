@@ -796,3 +796,215 @@ void oc_gather_payload_hashes(const uint8_t* seg, uint64_t seg_len, const uint64
   }
   free(tmp);
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* index: IndexOperator.Hash (index.go:15-19) = murmur3.New64().Write(key).Sum64() of          */
+/* github.com/spaolacci/murmur3 v1.1.0 (go.mod:10; not vendored): MurmurHash3_x64_128 with     */
+/* seed 0, Sum64 = h1 (Austin Appleby's published algorithm, restated here)                    */
+/* ------------------------------------------------------------------------------------------ */
+static inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static inline uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+void oc_murmur3_128(const uint8_t* p, size_t n, uint64_t seed, uint64_t* o1, uint64_t* o2) {
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  uint64_t h1 = seed, h2 = seed;
+  size_t nb = n / 16;
+  for (size_t i = 0; i < nb; ++i) {
+    uint64_t k1 = get_u64(p + 16 * i), k2 = get_u64(p + 16 * i + 8);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+  }
+  const uint8_t* t = p + 16 * nb;
+  uint64_t k1 = 0, k2 = 0;
+  switch (n & 15) {
+    case 15: k2 ^= (uint64_t)t[14] << 48; /* fallthrough */
+    case 14: k2 ^= (uint64_t)t[13] << 40; /* fallthrough */
+    case 13: k2 ^= (uint64_t)t[12] << 32; /* fallthrough */
+    case 12: k2 ^= (uint64_t)t[11] << 24; /* fallthrough */
+    case 11: k2 ^= (uint64_t)t[10] << 16; /* fallthrough */
+    case 10: k2 ^= (uint64_t)t[9] << 8;   /* fallthrough */
+    case 9:  k2 ^= (uint64_t)t[8];
+             k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2; /* fallthrough */
+    case 8:  k1 ^= (uint64_t)t[7] << 56;  /* fallthrough */
+    case 7:  k1 ^= (uint64_t)t[6] << 48;  /* fallthrough */
+    case 6:  k1 ^= (uint64_t)t[5] << 40;  /* fallthrough */
+    case 5:  k1 ^= (uint64_t)t[4] << 32;  /* fallthrough */
+    case 4:  k1 ^= (uint64_t)t[3] << 24;  /* fallthrough */
+    case 3:  k1 ^= (uint64_t)t[2] << 16;  /* fallthrough */
+    case 2:  k1 ^= (uint64_t)t[1] << 8;   /* fallthrough */
+    case 1:  k1 ^= (uint64_t)t[0];
+             k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)n; h2 ^= (uint64_t)n;
+  h1 += h2; h2 += h1;
+  h1 = fmix64(h1); h2 = fmix64(h2);
+  h1 += h2; h2 += h1;
+  *o1 = h1; *o2 = h2;
+}
+
+uint64_t oc_murmur3_sum64(const uint8_t* p, size_t n) {
+  uint64_t h1, h2;
+  oc_murmur3_128(p, n, 0, &h1, &h2);
+  return h1;
+}
+
+/* The index's observable semantics (index.go:81-165 over map.go's ShardMap): a map from
+ * MergedKey(ns, key) = ns || key (utils.go:133-139) to IndexValue{fid, valueOff, valueSize}.
+ *   Put        -> Set (insert or replace)                       index.go:144-165, map.go:160-207
+ *   Delete     -> remove                                        index.go:107-124
+ *   SoftDelete -> Set(IndexValue{valueOff: 0}) (fid 0, size 0)   index.go:126-142
+ *   Get        -> value, ErrKeyNotFound, or ErrKeySoftDeleted when valueOff == 0  index.go:81-98
+ * Bucket placement (hash % 16 shards, hash % (cap/16) chains) is unobservable; the sampled
+ * approximate-LRU eviction (map.go:395-420, random slots) is not restated: this oracle and the
+ * device index hold every key (the reference's deterministic regime: capacity >= keys). */
+typedef struct oc_islot { uint8_t* key; uint32_t klen, live; uint64_t h, fid, off, size; } oc_islot;
+struct oc_index { oc_islot* s; uint64_t cap, used, live; };
+
+oc_index* oc_index_new(void) {
+  oc_index* x = (oc_index*)calloc(1, sizeof *x);
+  x->cap = 1024;
+  x->s = (oc_islot*)calloc(x->cap, sizeof(oc_islot));
+  return x;
+}
+void oc_index_free(oc_index* x) {
+  if (!x) return;
+  for (uint64_t i = 0; i < x->cap; ++i) free(x->s[i].key);
+  free(x->s);
+  free(x);
+}
+static oc_islot* oc_index_find(oc_index* x, const uint8_t* k, uint32_t kl, uint64_t h, int create) {
+  if (create && (x->used + 1) * 2 > x->cap) {
+    oc_islot* old = x->s;
+    uint64_t oc = x->cap;
+    x->cap *= 2;
+    x->s = (oc_islot*)calloc(x->cap, sizeof(oc_islot));
+    for (uint64_t i = 0; i < oc; ++i) {
+      if (!old[i].key) continue;
+      uint64_t j = old[i].h & (x->cap - 1);
+      while (x->s[j].key) j = (j + 1) & (x->cap - 1);
+      x->s[j] = old[i];
+    }
+    free(old);
+  }
+  uint64_t j = h & (x->cap - 1);
+  for (;;) {
+    oc_islot* e = &x->s[j];
+    if (!e->key) {
+      if (!create) return NULL;
+      e->key = (uint8_t*)malloc(kl ? kl : 1);
+      memcpy(e->key, k, kl);
+      e->klen = kl;
+      e->h = h;
+      e->live = 0;
+      x->used++;
+      return e;
+    }
+    if (e->h == h && e->klen == kl && memcmp(e->key, k, kl) == 0) return e;
+    j = (j + 1) & (x->cap - 1);
+  }
+}
+static uint8_t* merged_key(const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl) {
+  uint8_t* m = (uint8_t*)malloc(nsl + kl + 1);
+  if (nsl) memcpy(m, ns, nsl);
+  if (kl) memcpy(m + nsl, key, kl);
+  return m;
+}
+void oc_index_set(oc_index* x, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, int op, uint64_t fid,
+                  uint64_t off, uint64_t size) {
+  /* op 0: Put, 1: Delete, 2: SoftDelete */
+  uint8_t* m = merged_key(ns, nsl, key, kl);
+  uint64_t h = oc_murmur3_sum64(m, nsl + kl);
+  oc_islot* e = oc_index_find(x, m, (uint32_t)(nsl + kl), h, op != 1);
+  free(m);
+  if (!e) return;
+  if (op == 1) {
+    if (e->live) { e->live = 0; x->live--; }
+    return;
+  }
+  if (!e->live) { e->live = 1; x->live++; }
+  e->fid = op == 0 ? fid : 0;
+  e->off = op == 0 ? off : 0;
+  e->size = op == 0 ? size : 0;
+}
+int oc_index_get(oc_index* x, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, uint64_t* fid,
+                 uint64_t* off, uint64_t* size) {
+  uint8_t* m = merged_key(ns, nsl, key, kl);
+  uint64_t h = oc_murmur3_sum64(m, nsl + kl);
+  oc_islot* e = oc_index_find(x, m, (uint32_t)(nsl + kl), h, 0);
+  free(m);
+  if (!e || !e->live) return 1; /* ErrKeyNotFound */
+  *fid = e->fid; *off = e->off; *size = e->size;
+  return e->off == 0 ? 2 : 0;   /* ErrKeySoftDeleted */
+}
+uint64_t oc_index_live(const oc_index* x) { return x->live; }
+
+/* doFilter (compaction.go:329-348) without the user CompactionFilter: 1 = drop */
+int oc_do_filter(oc_index* x, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, uint64_t src_fid,
+                 uint64_t src_off) {
+  uint64_t fid = 0, off = 0, size = 0;
+  if (oc_index_get(x, ns, nsl, key, kl, &fid, &off, &size) != 0) return 1;
+  return (fid != src_fid || off != src_off) ? 1 : 0;
+}
+
+/* the record's ns and key spans inside its payload (RecordFromBytes record.go:140-239 / HintRecord.Decode
+ * hint.go:50-84 layouts) */
+static void rec_ns_key(const oc_rec* r, const uint8_t* payload, uint32_t ns_size, int mode, const uint8_t** ns,
+                       const uint8_t** key, uint64_t* kl) {
+  *ns = payload + (mode == 0 ? 1 : 0);
+  *key = payload + r->hdr_size;
+  *kl = r->key_len;
+}
+
+/* the callback loops of recovery / compaction that feed the index, over the oracle decode:
+ *   mode 0 (data WAL)  recoverFromWal    db_impl.go:305-313: Put(ns, key, fid, foff - 7, size)
+ *   mode 1 (hint WAL)  recoverFromWal    db_impl.go:290-299: Put(ns, key, fid, h.off, h.size)
+ *                      (use_rec_fid: onePhase compaction.go:248-251: Put(ns, key, h.fid, h.off, h.size))
+ * Rows are put in order up to the first row the iteration rejects; returns the iteration's error
+ * (OC_ERR_* of the fragment, or 16 + OC_ST_* of the failing row), *n_put = rows put. */
+int oc_index_put_segment(oc_index* x, const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                         uint32_t ns_size, uint32_t etag_size, int mode, uint64_t fid, int use_rec_fid,
+                         uint64_t* n_put) {
+  oc_decode* d = oc_decode_segment(seg, len, start_off, base_time, ns_size, etag_size, mode);
+  int ret = d->err_class;
+  uint64_t r = 0;
+  for (; r < d->n_recs; ++r) {
+    const oc_rec* rc = &d->recs[r];
+    if (rc->status != OC_ST_OK) { ret = 16 + rc->status; break; }
+    const uint8_t *ns, *key;
+    uint64_t kl;
+    rec_ns_key(rc, d->bytes + d->byte_offs[r], ns_size, mode, &ns, &key, &kl);
+    if (mode == 0) oc_index_set(x, ns, ns_size, key, kl, 0, fid, rc->foff - OC_HEADER_SIZE, rc->size);
+    else oc_index_set(x, ns, ns_size, key, kl, 0, use_rec_fid ? rc->expire : fid, rc->val_len, rc->meta_len);
+  }
+  *n_put = r;
+  oc_decode_free(d);
+  return ret;
+}
+
+/* compactOneWal's doFilter over every delivered row (compaction.go:299-303): keep[r] = 1 when the index
+ * still points at (src_fid, foff - 7); rows from the first rejected row on are 0. Returns rows visited. */
+uint64_t oc_compact_filter(oc_index* x, const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                           uint32_t ns_size, uint32_t etag_size, uint64_t src_fid, uint8_t* keep, uint64_t n_keep) {
+  oc_decode* d = oc_decode_segment(seg, len, start_off, base_time, ns_size, etag_size, 0);
+  uint64_t r = 0;
+  for (uint64_t i = 0; i < n_keep; ++i) keep[i] = 0;
+  for (; r < d->n_recs; ++r) {
+    const oc_rec* rc = &d->recs[r];
+    if (rc->status != OC_ST_OK) break;
+    const uint8_t *ns, *key;
+    uint64_t kl;
+    rec_ns_key(rc, d->bytes + d->byte_offs[r], ns_size, 0, &ns, &key, &kl);
+    if (r < n_keep) keep[r] = oc_do_filter(x, ns, ns_size, key, kl, src_fid, rc->foff - OC_HEADER_SIZE) ? 0 : 1;
+  }
+  oc_decode_free(d);
+  return r;
+}

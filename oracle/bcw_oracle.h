@@ -167,6 +167,27 @@ void oc_gather_payload_hashes(const uint8_t* seg, uint64_t seg_len, const uint64
                               uint64_t n_frags, const uint32_t* first, const uint32_t* emit, const uint64_t* size,
                               uint64_t n_recs, uint64_t* out);
 
+/* ---- index (index.go:15-19, 81-165; compaction.go:329-348) ---- */
+void oc_murmur3_128(const uint8_t* p, size_t n, uint64_t seed, uint64_t* h1, uint64_t* h2);
+uint64_t oc_murmur3_sum64(const uint8_t* p, size_t n); /* spaolacci/murmur3 v1.1.0 New64().Sum64() */
+typedef struct oc_index oc_index;
+oc_index* oc_index_new(void);
+void oc_index_free(oc_index* x);
+/* op 0: Put, 1: Delete, 2: SoftDelete */
+void oc_index_set(oc_index* x, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, int op, uint64_t fid,
+                  uint64_t off, uint64_t size);
+/* 0: found, 1: ErrKeyNotFound, 2: ErrKeySoftDeleted (value still returned) */
+int oc_index_get(oc_index* x, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, uint64_t* fid,
+                 uint64_t* off, uint64_t* size);
+uint64_t oc_index_live(const oc_index* x);
+int oc_do_filter(oc_index* x, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, uint64_t src_fid,
+                 uint64_t src_off);
+int oc_index_put_segment(oc_index* x, const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                         uint32_t ns_size, uint32_t etag_size, int mode, uint64_t fid, int use_rec_fid,
+                         uint64_t* n_put);
+uint64_t oc_compact_filter(oc_index* x, const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                           uint32_t ns_size, uint32_t etag_size, uint64_t src_fid, uint8_t* keep, uint64_t n_keep);
+
 #ifdef __cplusplus
 }
 #endif

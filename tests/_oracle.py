@@ -81,6 +81,27 @@ lib.oc_decode_payload_hashes.restype = None
 lib.oc_decode_payload_hashes.argtypes = [vp, vp]
 lib.oc_gather_payload_hashes.restype = None
 lib.oc_gather_payload_hashes.argtypes = [vp, C.c_uint64, vp, vp, C.c_uint64, vp, vp, vp, C.c_uint64, vp]
+lib.oc_murmur3_sum64.restype = C.c_uint64
+lib.oc_murmur3_sum64.argtypes = [vp, C.c_size_t]
+lib.oc_murmur3_128.restype = None
+lib.oc_murmur3_128.argtypes = [vp, C.c_size_t, C.c_uint64, _u64p, _u64p]
+lib.oc_index_new.restype = vp
+lib.oc_index_new.argtypes = []
+lib.oc_index_free.argtypes = [vp]
+lib.oc_index_set.restype = None
+lib.oc_index_set.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64]
+lib.oc_index_get.restype = C.c_int
+lib.oc_index_get.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, _u64p, _u64p, _u64p]
+lib.oc_index_live.restype = C.c_uint64
+lib.oc_index_live.argtypes = [vp]
+lib.oc_do_filter.restype = C.c_int
+lib.oc_do_filter.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, C.c_uint64, C.c_uint64]
+lib.oc_index_put_segment.restype = C.c_int
+lib.oc_index_put_segment.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int,
+                                     C.c_uint64, C.c_int, _u64p]
+lib.oc_compact_filter.restype = C.c_uint64
+lib.oc_compact_filter.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, vp,
+                                  C.c_uint64]
 lib.oc_synth_segment.restype = vp
 lib.oc_synth_segment.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
                                  C.c_uint64]
@@ -255,3 +276,54 @@ def compact_append(dst: "Writer", hint: "Writer", dst_fid: int, seg, start_off: 
 
 def meta_app_size_zero(meta: bytes) -> bool:
     return bool(lib.oc_meta_app_size_zero(_ptr(meta), len(meta)))
+
+
+def murmur3_sum64(b: bytes) -> int:
+    return int(lib.oc_murmur3_sum64(_ptr(b), len(b)))
+
+
+def murmur3_128(b: bytes, seed: int = 0):
+    a, c = C.c_uint64(), C.c_uint64()
+    lib.oc_murmur3_128(_ptr(b), len(b), seed, C.byref(a), C.byref(c))
+    return int(a.value), int(c.value)
+
+
+class Index:
+    """oc_index: the reference index's Get/Put/Delete/SoftDelete semantics (index.go:81-165)."""
+    PUT, DELETE, SOFT_DELETE = 0, 1, 2
+
+    def __init__(self):
+        self.h = lib.oc_index_new()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib.oc_index_free(self.h)
+            self.h = None
+
+    def set(self, ns: bytes, key: bytes, op: int, fid: int = 0, off: int = 0, size: int = 0):
+        lib.oc_index_set(self.h, _ptr(ns), len(ns), _ptr(key), len(key), op, fid, off, size)
+
+    def put(self, ns, key, fid, off, size):
+        self.set(ns, key, 0, fid, off, size)
+
+    def get(self, ns: bytes, key: bytes):
+        f, o, s = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        st = lib.oc_index_get(self.h, _ptr(ns), len(ns), _ptr(key), len(key), C.byref(f), C.byref(o), C.byref(s))
+        return int(st), (int(f.value), int(o.value), int(s.value))
+
+    def live(self) -> int:
+        return int(lib.oc_index_live(self.h))
+
+    def put_segment(self, seg, start_off, base_time, ns_size, etag_size, mode, fid, use_rec_fid=False):
+        seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+        n = C.c_uint64()
+        ec = lib.oc_index_put_segment(self.h, _ptr(seg), seg.size, start_off, base_time, ns_size, etag_size, mode, fid,
+                                      int(use_rec_fid), C.byref(n))
+        return int(ec), int(n.value)
+
+    def compact_filter(self, seg, start_off, base_time, ns_size, etag_size, src_fid, n_rows):
+        seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+        keep = np.zeros(max(n_rows, 1), dtype=np.uint8)
+        nv = lib.oc_compact_filter(self.h, _ptr(seg), seg.size, start_off, base_time, ns_size, etag_size, src_fid,
+                                   keep.ctypes.data_as(vp), n_rows)
+        return keep[:n_rows], int(nv)

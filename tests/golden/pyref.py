@@ -211,3 +211,85 @@ def iterate(data: bytes, start_off: int, base_time: int, ns_size: int, etag_size
         recs.append(dict(foff=off, size=len(payload), first_frag=f0, emit_frag=gi, status=st, payload=payload,
                          **{("hint_size" if k == "size" else k): v for k, v in fields.items()}))
         record = bytearray()
+
+
+# ---- index hash: spaolacci/murmur3 v1.1.0 New64().Sum64() (index.go:15-19), independent restatement ----
+_M64 = (1 << 64) - 1
+
+
+def _rotl64(x, r):
+    return ((x << r) | (x >> (64 - r))) & _M64
+
+
+def _fmix64(k):
+    k ^= k >> 33
+    k = (k * 0xff51afd7ed558ccd) & _M64
+    k ^= k >> 33
+    k = (k * 0xc4ceb9fe1a85ec53) & _M64
+    k ^= k >> 33
+    return k
+
+
+def murmur3_x64_128(data: bytes, seed: int = 0):
+    c1, c2 = 0x87c37b91114253d5, 0x4cf5ad432745937f
+    h1 = h2 = seed & _M64
+    n = len(data)
+    nb = n // 16
+    for i in range(nb):
+        k1 = int.from_bytes(data[16 * i:16 * i + 8], "little")
+        k2 = int.from_bytes(data[16 * i + 8:16 * i + 16], "little")
+        k1 = (_rotl64((k1 * c1) & _M64, 31) * c2) & _M64
+        h1 ^= k1
+        h1 = (_rotl64(h1, 27) + h2) & _M64
+        h1 = (h1 * 5 + 0x52dce729) & _M64
+        k2 = (_rotl64((k2 * c2) & _M64, 33) * c1) & _M64
+        h2 ^= k2
+        h2 = (_rotl64(h2, 31) + h1) & _M64
+        h2 = (h2 * 5 + 0x38495ab5) & _M64
+    tail = data[16 * nb:]
+    if len(tail) > 8:
+        k2 = int.from_bytes(tail[8:], "little")
+        h2 ^= (_rotl64((k2 * c2) & _M64, 33) * c1) & _M64
+    if len(tail) > 0:
+        k1 = int.from_bytes(tail[:8], "little")
+        h1 ^= (_rotl64((k1 * c1) & _M64, 31) * c2) & _M64
+    h1 ^= n
+    h2 ^= n
+    h1 = (h1 + h2) & _M64
+    h2 = (h2 + h1) & _M64
+    h1, h2 = _fmix64(h1), _fmix64(h2)
+    h1 = (h1 + h2) & _M64
+    h2 = (h2 + h1) & _M64
+    return h1, h2
+
+
+def murmur3_sum64(data: bytes) -> int:
+    return murmur3_x64_128(data)[0]
+
+
+class PyIndex:
+    """Index semantics (index.go:81-165): MergedKey(ns, key) -> (fid, off, size); Get reports
+    not-found / soft-deleted (off == 0). No eviction (capacity >= keys)."""
+
+    def __init__(self):
+        self.m = {}
+
+    def put(self, ns, key, fid, off, size):
+        self.m[bytes(ns) + bytes(key)] = (fid, off, size)
+
+    def delete(self, ns, key):
+        self.m.pop(bytes(ns) + bytes(key), None)
+
+    def soft_delete(self, ns, key):
+        self.m[bytes(ns) + bytes(key)] = (0, 0, 0)
+
+    def get(self, ns, key):
+        v = self.m.get(bytes(ns) + bytes(key))
+        if v is None:
+            return 1, None
+        return (2 if v[1] == 0 else 0), v
+
+    def do_filter(self, ns, key, src_fid, src_off) -> bool:
+        """compaction.go:329-348 (no user filter): True drops the record."""
+        st, v = self.get(ns, key)
+        return st != 0 or v[0] != src_fid or v[1] != src_off

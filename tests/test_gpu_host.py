@@ -192,55 +192,35 @@ def test_encode_rec_off_capacity_and_zero_length_fulls(ctx):
     assert (roff[300:] == 7).all() and (roff[:300] != 7).all()
 
 
-def _dev_table(torch, cap, dev):
-    cols = {}
-    for name, dt in L.TABLE_COLUMNS:
-        tdt = {"u8": torch.int64, "u4": torch.int32, "u1": torch.uint8}[dt]
-        cols[name] = torch.zeros(max(cap, 1), dtype=tdt, device=dev)
-    ptr_t = {"u8": L.u64p, "u4": L.u32p, "u1": L.u8p}
-    tab = L.RecordTable(cap, *[C.cast(C.c_void_p(cols[n].data_ptr()), ptr_t[dt]) for n, dt in L.TABLE_COLUMNS])
-    return tab, cols
-
-
 def test_encode_async_generation_and_table_checks():
     """bcw_encode_segment_async refuses a decode result that is not the context's latest decode
     (BCW_ENC_ERR_STALE) and a source table smaller than the decode (BCW_ENC_ERR_TABLE)."""
-    torch = pytest.importorskip("torch")
+    import _devmem as D
     from bitcaskdb_amd import Context
-    dev = torch.device("cuda", 0)
     c = Context(0)
-    s = torch.cuda.Stream()
-    c.set_stream(s.cuda_stream)
     data = O.synth(1 << 40, 500, 3)
-    src = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    src = D.upload(data)
     ec, _, _, hint = O.hint_by_wal(data, 3, 40, BASE, 20, 20)
-    hsrc = torch.frombuffer(bytearray(hint), dtype=torch.uint8).to(dev)
-    tab, cols = _dev_table(torch, 600, dev)
-    htab, hcols = _dev_table(torch, 600, dev)
+    hsrc = D.upload(hint)
+    tab, htab, small = D.DevTable(600), D.DevTable(600), D.DevTable(100)
     rsz = C.sizeof(L.DecodeResult)
-    d_res = torch.zeros(rsz, dtype=torch.uint8, device=dev)
-    h_res = torch.zeros(rsz, dtype=torch.uint8, device=dev)
-    e_res = torch.zeros(C.sizeof(L.EncodeResult), dtype=torch.uint8, device=dev)
-    keep = torch.ones(600, dtype=torch.uint8, device=dev)
-    wout = torch.zeros(len(data) * 2, dtype=torch.uint8, device=dev)
-    hout = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
-    roff = torch.zeros(600, dtype=torch.int64, device=dev)
-    vp = C.c_void_p
+    d_res, h_res = D.DevBuf(rsz), D.DevBuf(rsz)
+    e_res = D.DevBuf(C.sizeof(L.EncodeResult))
+    keep = D.DevBuf(600, fill=1)
+    wout, hout, roff = D.DevBuf(len(data) * 2), D.DevBuf(1 << 20), D.DevBuf(600 * 8)
     dp = L.DecodeParams(len(data), BASE, 40, 20, 20, L.MODE_RECORD)
     hp = L.DecodeParams(len(hint), BASE, 40, 20, 0, L.MODE_HINT)
     ep = L.EncodeParams(len(data), BASE, 9, 40, 40, 40, L.ENC_COMPACT, 20, 20)
-    out = L.EncodeOut(C.cast(vp(wout.data_ptr()), L.u8p), wout.numel(), C.cast(vp(hout.data_ptr()), L.u8p),
-                      hout.numel(), C.cast(vp(roff.data_ptr()), L.u64p), 0)
+    out = L.EncodeOut(C.cast(wout.vp(), L.u8p), wout.n, C.cast(hout.vp(), L.u8p), hout.n, C.cast(roff.vp(), L.u64p), 0)
 
     def dec(params, t, r, buf):
-        assert L.lib.bcw_decode_segment_async(c.handle, vp(buf.data_ptr()), C.byref(params), C.byref(t),
-                                              vp(r.data_ptr())) == 0
+        assert L.lib.bcw_decode_segment_async(c.handle, buf.vp(), C.byref(params), C.byref(t.t), r.vp()) == 0
 
     def enc(t, r):
-        assert L.lib.bcw_encode_segment_async(c.handle, vp(src.data_ptr()), C.byref(ep), C.byref(t), vp(r.data_ptr()),
-                                              vp(keep.data_ptr()), C.byref(out), vp(e_res.data_ptr())) == 0
-        torch.cuda.synchronize()
-        return L.EncodeResult.from_buffer_copy(bytes(e_res.cpu().numpy()))
+        assert L.lib.bcw_encode_segment_async(c.handle, src.vp(), C.byref(ep), C.byref(t.t), r.vp(), keep.vp(),
+                                              C.byref(out), e_res.vp()) == 0
+        c.sync()
+        return L.EncodeResult.from_buffer_copy(bytes(e_res.download()))
 
     dec(dp, tab, d_res, src)
     dec(hp, htab, h_res, hsrc)  # replaces the context's fragment table
@@ -251,8 +231,7 @@ def test_encode_async_generation_and_table_checks():
     assert r.err_class == 0 and r.n_written == 500
     rd, rh = O.Writer(BASE, BASE), O.Writer(BASE, BASE)
     O.compact_append(rd, rh, 9, data, 40, BASE, BASE, 20, 20, np.ones(500, np.uint8))
-    assert bytes(wout[:r.wal_need].cpu().numpy()) == rd.data()[40:]
-    small, _ = _dev_table(torch, 100, dev)
+    assert bytes(wout.download(r.wal_need)) == rd.data()[40:]
     dec(dp, small, d_res, src)
     r = enc(small, d_res)
     assert r.err_class == L.ENC_ERR_TABLE and r.n_written == 0 and r.wal_need == 0

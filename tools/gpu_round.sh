@@ -10,7 +10,7 @@ STEPS=${STEPS:-tests,smoke,bench,prof,enc}
 run() { echo "== $1 ($(date +%T))"; }
 if [[ $STEPS == *tests* ]]; then
   run tests
-  timeout -k 10 420 python -m pytest tests -m gpu -x -q > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
+  timeout -k 10 1000 python -u -m pytest ${PYTEST_ARGS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
   tail -3 "$OUT/gpu_tests.log"
 fi
 if [[ $STEPS == *smoke* ]]; then
