@@ -63,6 +63,15 @@ class EncodeResult(C.Structure):
                 ("hint_events", C.c_uint32), ("fits", C.c_uint32), ("_pad", C.c_uint32)]
 
 
+class IndexResult(C.Structure):
+    _fields_ = [("n_in", C.c_uint64), ("n_done", C.c_uint64), ("err_class", C.c_int32), ("_pad", C.c_int32)]
+
+
+class IndexInfo(C.Structure):
+    _fields_ = [("live", C.c_uint64), ("slots_used", C.c_uint64), ("slot_capacity", C.c_uint64),
+                ("arena_used", C.c_uint64), ("arena_capacity", C.c_uint64), ("overflow", C.c_uint64)]
+
+
 # the table's column names, C types and numpy dtypes (one place, used by wal.py and bench.py)
 TABLE_COLUMNS = [("foff", "u8"), ("size", "u8"), ("expire", "u8"), ("aux0", "u8"), ("aux1", "u8"),
                  ("key_len", "u4"), ("val_len", "u4"), ("meta_len", "u4"), ("first_frag", "u4"),
@@ -80,6 +89,9 @@ SB_OK, SB_SHORT, SB_CRC, SB_MAGIC, SB_BLOCKSIZE = 0, 1, 2, 3, 4
 E_CAPACITY = -4
 ENC_COMPACT, ENC_HINT = 0, 1
 ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC, ENC_ERR_TABLE, ENC_ERR_STALE = 0, 1, 2, 3, 4, 5
+IDX_PUT, IDX_DELETE, IDX_SOFT_DELETE = 0, 1, 2
+IDX_FOUND, IDX_NOT_FOUND, IDX_SOFT_DELETED = 0, 1, 2
+IDX_ERR_FULL = 6
 
 
 def _load():
@@ -117,6 +129,22 @@ def _load():
                                                C.POINTER(EncodeOut), vp]),
         "bcw_encode_segment": (C.c_int, [vp, vp, C.POINTER(EncodeParams), vp, C.c_uint64, C.POINTER(EncodeOut),
                                          C.POINTER(EncodeResult)]),
+        "bcw_index_create": (C.c_int, [vp, C.c_uint64, C.c_uint64, C.POINTER(vp)]),
+        "bcw_index_destroy": (C.c_int, [vp]),
+        "bcw_index_reserve": (C.c_int, [vp, C.c_uint64, C.c_uint64]),
+        "bcw_index_stats": (C.c_int, [vp, C.POINTER(IndexInfo)]),
+        "bcw_index_apply": (C.c_int, [vp, C.c_uint64, vp, u64p, u8p, u64p, u64p, u64p]),
+        "bcw_index_get": (C.c_int, [vp, C.c_uint64, vp, u64p, u64p, u64p, u64p, u8p]),
+        "bcw_index_put_decoded_async": (C.c_int, [vp, vp, C.POINTER(DecodeParams), C.POINTER(RecordTable), vp,
+                                                  C.c_uint64, C.c_int, vp]),
+        "bcw_compact_filter_async": (C.c_int, [vp, vp, C.POINTER(DecodeParams), C.POINTER(RecordTable), vp,
+                                               C.c_uint64, vp, vp]),
+        "bcw_index_export": (C.c_int, [vp, vp, C.c_uint64, u64p, u64p, u64p, u64p, C.c_uint64, u64p, u64p]),
+        "bcw_compact_segment": (C.c_int, [vp, vp, vp, C.POINTER(EncodeParams), C.c_uint64, C.POINTER(EncodeOut),
+                                          C.POINTER(EncodeResult), C.POINTER(IndexResult)]),
+        "bcw_index_recover_segment": (C.c_int, [vp, vp, vp, C.POINTER(DecodeParams), C.c_uint64, C.c_int,
+                                                C.POINTER(DecodeResult), C.POINTER(IndexResult)]),
+        "bcw_murmur3_sum64": (C.c_uint64, [vp, C.c_uint64]),
         "bcw_synth_segment": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_int, C.c_uint64, vp, C.c_uint64, u64p, u64p]),
     }

@@ -145,35 +145,6 @@ static inline uint32_t mask_crc(uint32_t c) { return ((c >> 15) | (c << 17)) + 0
 
 using namespace bcw;
 
-struct bcw_ctx {
-  int device = 0;
-  uint64_t id = 0;         // unique per context (high half of every decode generation)
-  uint64_t gen_seq = 0;    // decodes issued on this context
-  uint64_t frag_gen = 0;   // generation of the decode whose fragment table the scratch holds
-  int num_cus = 256;
-  hipStream_t own = nullptr;
-  hipStream_t cur = nullptr;
-  Tables tabs{};
-  Scratch s{};
-  EncScratch es{};
-  // sync encode staging
-  uint8_t* d_keep = nullptr;
-  uint64_t d_keep_cap = 0;
-  void* d_eout = nullptr;
-  uint64_t d_eout_cap = 0;
-  bcw_encode_result* d_eres = nullptr;
-  uint64_t frag_hint = 0;  // capacity requested by a retry
-  // sync-API staging
-  uint8_t* d_seg = nullptr;
-  uint64_t d_seg_cap = 0;
-  void* d_tab_mem = nullptr;
-  uint64_t d_tab_cap = 0;
-  bcw_record_table d_tab{};
-  bcw_decode_result* d_result = nullptr;
-  uint32_t last_start_off = 0;
-  uint64_t last_nfrag_cap = 0;
-  Prof prof;
-};
 
 #define HIPCHK(x)                          \
   do {                                     \
@@ -181,19 +152,6 @@ struct bcw_ctx {
   } while (0)
 
 namespace {
-// Every entry point that touches the device selects the context's device on the calling thread and
-// restores the caller's current device when it returns.
-struct DeviceGuard {
-  int prev = -1;
-  bool ok = false;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    ok = hipSetDevice(dev) == hipSuccess;
-  }
-  ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
 std::atomic<uint64_t> g_ctx_ids{1};
 }  // namespace
 
@@ -331,7 +289,8 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
             hipMalloc(&c->tabs.lds_image, image.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.enc_ops, enc_ops.size() * 4) == hipSuccess &&
             hipMalloc(&c->d_eres, sizeof(bcw_encode_result)) == hipSuccess &&
-            hipMalloc(&c->d_result, sizeof(bcw_decode_result)) == hipSuccess;
+            hipMalloc(&c->d_result, sizeof(bcw_decode_result)) == hipSuccess &&
+            hipMalloc(&c->d_ires, sizeof(bcw_index_result)) == hipSuccess;
   ok = ok && hipMemcpy(c->tabs.slice, slice.data(), slice.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.fwd, fwd.data(), fwd.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.carry, carry.data(), carry.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
@@ -381,6 +340,7 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   (void)hipFree(c->d_seg);
   (void)hipFree(c->d_tab_mem);
   (void)hipFree(c->d_result);
+  (void)hipFree(c->d_ires);
   for (auto& m : c->prof.marks) { (void)hipEventDestroy(m.a); (void)hipEventDestroy(m.b); }
   for (auto e : c->prof.pool) (void)hipEventDestroy(e);
   if (c->own) (void)hipStreamDestroy(c->own);
@@ -692,37 +652,25 @@ int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_
   return launch_encode(L, c->es, c->cur, &c->prof) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 
-int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params* p, const uint8_t* h_keep,
-                       uint64_t n_keep, const bcw_encode_out* h, bcw_encode_result* h_result) {
-  if (!c || !p || !h || !h_result) return BCW_E_INVAL;
-  if (p->src_len && !h_src) return BCW_E_INVAL;
-  DeviceGuard dg(c->device);
-  if (!dg.ok) return BCW_E_HIP;
-  // decode the source (record mode) into the context's table
-  bcw_super_block sb{};
-  bcw_decode_params dp{};
-  dp.seg_len = p->src_len;
-  dp.start_off = p->src_start_off;
-  dp.ns_size = p->ns_size;
-  dp.etag_size = p->etag_size;
-  dp.mode = BCW_MODE_RECORD;
-  dp.base_time = (bcw_load_super_block(h_src, p->src_len, &sb) == BCW_SB_OK) ? sb.base_time : 0;
-  uint64_t cap = std::max<uint64_t>(16, p->src_len / 64 + 16);
-  int rc;
-  bcw_decode_result dres{};
+}  // extern "C"
+
+namespace {
+// Sync-API staging: the source segment into the context's device buffer, decoded into the context's
+// device table (grown until it holds every record), the fragment scratch retried until it fits.
+int sync_decode(bcw_ctx* c, const uint8_t* h_src, const bcw_decode_params& dp, bcw_decode_result& dres) {
+  uint64_t cap = std::max<uint64_t>(16, dp.seg_len / 64 + 16);
+  if (dp.seg_len > c->d_seg_cap) {
+    (void)hipStreamSynchronize(c->cur);
+    (void)hipFree(c->d_seg);
+    c->d_seg = nullptr;
+    c->d_seg_cap = 0;
+    if (hipMalloc(&c->d_seg, dp.seg_len) != hipSuccess) return BCW_E_NOMEM;
+    c->d_seg_cap = dp.seg_len;
+  }
+  if (dp.seg_len) HIPCHK(hipMemcpyAsync(c->d_seg, h_src, dp.seg_len, hipMemcpyHostToDevice, c->cur));
   for (;;) {
-    std::vector<uint8_t> dummy;  // host table not needed: decode into the device table only
-    rc = ensure_dev_table(c, cap, false);
+    int rc = ensure_dev_table(c, cap, dp.mode == BCW_MODE_HINT);
     if (rc != BCW_OK) return rc;
-    if (p->src_len > c->d_seg_cap) {
-      (void)hipStreamSynchronize(c->cur);
-      (void)hipFree(c->d_seg);
-      c->d_seg = nullptr;
-      c->d_seg_cap = 0;
-      if (hipMalloc(&c->d_seg, p->src_len) != hipSuccess) return BCW_E_NOMEM;
-      c->d_seg_cap = p->src_len;
-    }
-    if (p->src_len) HIPCHK(hipMemcpyAsync(c->d_seg, h_src, p->src_len, hipMemcpyHostToDevice, c->cur));
     for (int attempt = 0; attempt < 3; ++attempt) {
       rc = bcw_decode_segment_async(c, c->d_seg, &dp, &c->d_tab, c->d_result);
       if (rc != BCW_OK) return rc;
@@ -732,22 +680,38 @@ int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params
       if (bcw_ctx_reserve_fragments(c, dres.retry_frag_capacity + 64) != BCW_OK) return BCW_E_CAPACITY;
     }
     if (dres.retry_frag_capacity) return BCW_E_NOMEM;
-    if (dres.n_records <= c->d_tab.capacity) break;
+    if (dres.n_records <= c->d_tab.capacity) return BCW_OK;
     cap = dres.n_records + 16;
   }
+}
+
+int ensure_keep(bcw_ctx* c, uint64_t rows) {
+  if (rows <= c->d_keep_cap && c->d_keep) return BCW_OK;
+  (void)hipStreamSynchronize(c->cur);
+  (void)hipFree(c->d_keep);
+  c->d_keep = nullptr;
+  c->d_keep_cap = 0;
+  if (hipMalloc(&c->d_keep, std::max<uint64_t>(rows, 1)) != hipSuccess) return BCW_E_NOMEM;
+  c->d_keep_cap = std::max<uint64_t>(rows, 1);
+  return BCW_OK;
+}
+
+bcw_decode_params src_params(const uint8_t* h_src, const bcw_encode_params* p) {
+  bcw_super_block sb{};
+  bcw_decode_params dp{};
+  dp.seg_len = p->src_len;
+  dp.start_off = p->src_start_off;
+  dp.ns_size = p->ns_size;
+  dp.etag_size = p->etag_size;
+  dp.mode = BCW_MODE_RECORD;
+  dp.base_time = (bcw_load_super_block(h_src, p->src_len, &sb) == BCW_SB_OK) ? sb.base_time : 0;
+  return dp;
+}
+
+// the encode of the context's decoded source with the context's keep mask, outputs copied to the host
+int encode_to_host(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out* h, bcw_encode_result* h_result,
+                   const bcw_decode_result& dres) {
   const uint64_t rows = c->d_tab.capacity;
-  // keep mask (missing entries: dropped)
-  if (rows > c->d_keep_cap) {
-    (void)hipFree(c->d_keep);
-    c->d_keep = nullptr;
-    c->d_keep_cap = 0;
-    if (hipMalloc(&c->d_keep, rows) != hipSuccess) return BCW_E_NOMEM;
-    c->d_keep_cap = rows;
-  }
-  HIPCHK(hipMemsetAsync(c->d_keep, 0, rows, c->cur));
-  const uint64_t nk = std::min(n_keep, rows);
-  if (h_keep && nk) HIPCHK(hipMemcpyAsync(c->d_keep, h_keep, nk, hipMemcpyHostToDevice, c->cur));
-  // device outputs
   const uint64_t need = h->wal_cap + h->hint_cap + rows * 8;
   if (need > c->d_eout_cap) {
     (void)hipStreamSynchronize(c->cur);
@@ -767,7 +731,7 @@ int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params
   d.hint = (uint8_t*)(((uintptr_t)m + 15) & ~(uintptr_t)15);
   d.hint_cap = h->hint_cap;
   if (p->mode == BCW_ENC_HINT && !d.wal) d.wal = d.hint;
-  rc = bcw_encode_segment_async(c, c->d_seg, p, &c->d_tab, c->d_result, c->d_keep, &d, c->d_eres);
+  int rc = bcw_encode_segment_async(c, c->d_seg, p, &c->d_tab, c->d_result, c->d_keep, &d, c->d_eres);
   if (rc != BCW_OK) return rc;
   HIPCHK(hipMemcpyAsync(h_result, c->d_eres, sizeof *h_result, hipMemcpyDeviceToHost, c->cur));
   HIPCHK(hipStreamSynchronize(c->cur));
@@ -780,8 +744,67 @@ int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params
   // rows >= n_in are never written (UINT64_MAX): copy only rows the encode can have written
   const uint64_t nr = std::min(h_result->n_in, rows);
   if (h->rec_off && nr) HIPCHK(hipMemcpyAsync(h->rec_off, d.rec_off, nr * 8, hipMemcpyDeviceToHost, c->cur));
+  HIPCHK(hipStreamSynchronize(c->cur));
   if (h->rec_off)
     for (uint64_t i = nr; i < h->rec_off_cap && i < dres.n_records; ++i) h->rec_off[i] = ~0ull;
+  return BCW_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params* p, const uint8_t* h_keep,
+                       uint64_t n_keep, const bcw_encode_out* h, bcw_encode_result* h_result) {
+  if (!c || !p || !h || !h_result) return BCW_E_INVAL;
+  if (p->src_len && !h_src) return BCW_E_INVAL;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
+  const bcw_decode_params dp = src_params(h_src, p);
+  bcw_decode_result dres{};
+  int rc = sync_decode(c, h_src, dp, dres);
+  if (rc != BCW_OK) return rc;
+  const uint64_t rows = c->d_tab.capacity;
+  rc = ensure_keep(c, rows);  // keep mask (missing entries: dropped)
+  if (rc != BCW_OK) return rc;
+  HIPCHK(hipMemsetAsync(c->d_keep, 0, rows, c->cur));
+  const uint64_t nk = std::min(n_keep, rows);
+  if (h_keep && nk) HIPCHK(hipMemcpyAsync(c->d_keep, h_keep, nk, hipMemcpyHostToDevice, c->cur));
+  return encode_to_host(c, p, h, h_result, dres);
+}
+
+int bcw_compact_segment(bcw_ctx* c, bcw_index* ix, const uint8_t* h_src, const bcw_encode_params* p, uint64_t src_fid,
+                        const bcw_encode_out* h, bcw_encode_result* h_result, bcw_index_result* h_filter) {
+  if (!c || !ix || !p || !h || !h_result || p->mode != BCW_ENC_COMPACT) return BCW_E_INVAL;
+  if (p->src_len && !h_src) return BCW_E_INVAL;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
+  const bcw_decode_params dp = src_params(h_src, p);
+  bcw_decode_result dres{};
+  int rc = sync_decode(c, h_src, dp, dres);
+  if (rc != BCW_OK) return rc;
+  rc = ensure_keep(c, c->d_tab.capacity);
+  if (rc != BCW_OK) return rc;
+  rc = bcw_compact_filter_async(ix, c->d_seg, &dp, &c->d_tab, c->d_result, src_fid, c->d_keep,
+                                h_filter ? c->d_ires : nullptr);
+  if (rc != BCW_OK) return rc;
+  if (h_filter) HIPCHK(hipMemcpyAsync(h_filter, c->d_ires, sizeof *h_filter, hipMemcpyDeviceToHost, c->cur));
+  return encode_to_host(c, p, h, h_result, dres);
+}
+
+int bcw_index_recover_segment(bcw_ctx* c, bcw_index* ix, const uint8_t* h_seg, const bcw_decode_params* p,
+                              uint64_t fid, int use_record_fid, bcw_decode_result* h_dres,
+                              bcw_index_result* h_out) {
+  if (!c || !ix || !p || !h_out) return BCW_E_INVAL;
+  if (p->seg_len && !h_seg) return BCW_E_INVAL;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
+  bcw_decode_result dres{};
+  int rc = sync_decode(c, h_seg, *p, dres);
+  if (rc != BCW_OK) return rc;
+  if (h_dres) *h_dres = dres;
+  rc = bcw_index_put_decoded_async(ix, c->d_seg, p, &c->d_tab, c->d_result, fid, use_record_fid, c->d_ires);
+  if (rc != BCW_OK) return rc;
+  HIPCHK(hipMemcpyAsync(h_out, c->d_ires, sizeof *h_out, hipMemcpyDeviceToHost, c->cur));
   HIPCHK(hipStreamSynchronize(c->cur));
   return BCW_OK;
 }

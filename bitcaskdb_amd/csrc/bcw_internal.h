@@ -158,9 +158,59 @@ size_t enc_sizeof_tile();
 int enc_tile_items();
 int enc_ev_win();
 
+// Every C-ABI entry point that touches the device selects the context's device on the calling thread
+// and restores the caller's current device when it returns.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 // Host-side table builders (bcw_api.cpp).
 void build_slice_tables(uint32_t* t2x256);
 void build_lane_tables(uint32_t* fwd64x8x16, uint32_t* carry8x16, uint32_t* half8x16);
 void build_initc(uint32_t* initc);
 
 }  // namespace bcw
+
+// The context behind the C-ABI handle (bcw.h): one device, one launch stream, constant tables and
+// grow-only scratch. Defined here so every translation unit of libbcw.so can reach its stream,
+// device and the fragment table of its latest decode.
+struct bcw_ctx {
+  int device = 0;
+  uint64_t id = 0;         // unique per context (high half of every decode generation)
+  uint64_t gen_seq = 0;    // decodes issued on this context
+  uint64_t frag_gen = 0;   // generation of the decode whose fragment table the scratch holds
+  int num_cus = 256;
+  hipStream_t own = nullptr;
+  hipStream_t cur = nullptr;
+  bcw::Tables tabs{};
+  bcw::Scratch s{};
+  bcw::EncScratch es{};
+  // sync encode staging
+  uint8_t* d_keep = nullptr;
+  uint64_t d_keep_cap = 0;
+  void* d_eout = nullptr;
+  uint64_t d_eout_cap = 0;
+  bcw_encode_result* d_eres = nullptr;
+  uint64_t frag_hint = 0;  // capacity requested by a retry
+  // sync-API staging
+  uint8_t* d_seg = nullptr;
+  uint64_t d_seg_cap = 0;
+  void* d_tab_mem = nullptr;
+  uint64_t d_tab_cap = 0;
+  bcw_record_table d_tab{};
+  bcw_decode_result* d_result = nullptr;
+  bcw_index_result* d_ires = nullptr;  // sync index calls
+  uint32_t last_start_off = 0;
+  uint64_t last_nfrag_cap = 0;
+  bcw::Prof prof;
+};

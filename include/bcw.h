@@ -301,6 +301,92 @@ int bcw_encode_segment_async(bcw_ctx* ctx, const uint8_t* d_src, const bcw_encod
 int bcw_encode_segment(bcw_ctx* ctx, const uint8_t* h_src, const bcw_encode_params* p, const uint8_t* h_keep,
                        uint64_t n_keep, const bcw_encode_out* h_out, bcw_encode_result* h_result);
 
+/* ---- device index: the bitcaskDB index (index.go) resident in HBM -------------------------------
+ * Observable semantics of Index.Get/Put/Delete/SoftDelete (index.go:81-165): a map from MergedKey(ns, key)
+ * = ns || key (utils.go:133-139) to (fid, off, size), hashed with murmur3 Sum64 (index.go:15-19). Get
+ * reports ErrKeyNotFound, or ErrKeySoftDeleted when off == 0. The reference's sampled approximate-LRU
+ * eviction (random, map.go:395-420) is not restated: the device index keeps every key and grows.
+ * Batches keep the reference's sequential order: the last operation on a key wins. An index is bound to
+ * the context it was created on (its stream and device; the table-driven calls read that context's
+ * fragment table of its latest decode). */
+typedef struct bcw_index bcw_index;
+#define BCW_IDX_PUT 0
+#define BCW_IDX_DELETE 1
+#define BCW_IDX_SOFT_DELETE 2
+#define BCW_IDX_FOUND 0
+#define BCW_IDX_NOT_FOUND 1    /* ErrKeyNotFound */
+#define BCW_IDX_SOFT_DELETED 2 /* ErrKeySoftDeleted (value still reported) */
+#define BCW_IDX_ERR_FULL 6     /* the slot table overflowed (not expected: capacity is managed by the host) */
+
+/* Outcome of a table-driven index call (device struct). err_class: 0, BCW_ENC_ERR_STALE (d_result is not
+ * the context's latest decode), BCW_ENC_ERR_TABLE (table smaller than the decode) or BCW_IDX_ERR_FULL. */
+typedef struct bcw_index_result {
+  uint64_t n_in;   /* rows the iteration delivers: before the first rejected row (record.go:246-263) */
+  uint64_t n_done; /* put: rows applied; filter: rows kept */
+  int32_t err_class;
+  int32_t _pad;
+} bcw_index_result;
+
+typedef struct bcw_index_info {
+  uint64_t live;          /* keys present (Get finds them, soft-deleted included) */
+  uint64_t slots_used;    /* slots claimed (live + deleted keys) */
+  uint64_t slot_capacity;
+  uint64_t arena_used;    /* key arena bytes */
+  uint64_t arena_capacity;
+  uint64_t overflow;      /* != 0: an operation found no slot (index inconsistent) */
+} bcw_index_info;
+
+/* keys / arena_bytes: initial sizing (both grow on demand) */
+int bcw_index_create(bcw_ctx* ctx, uint64_t keys, uint64_t arena_bytes, bcw_index** out);
+int bcw_index_destroy(bcw_index* ix);
+int bcw_index_reserve(bcw_index* ix, uint64_t keys, uint64_t arena_bytes);
+int bcw_index_stats(bcw_index* ix, bcw_index_info* out);
+/* Index.Put / Delete / SoftDelete of n merged keys (host arrays; key i = h_keys[h_key_off[i], h_key_off[i+1]),
+ * h_ops[i] = BCW_IDX_*), applied in order (the Go shim mirrors DBImpl.writeIndex, db_impl.go:433-452).
+ * Synchronous. */
+int bcw_index_apply(bcw_index* ix, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off,
+                    const uint8_t* h_ops, const uint64_t* h_fid, const uint64_t* h_off, const uint64_t* h_size);
+/* Index.Get of n merged keys (host arrays): status BCW_IDX_* and the value per key. Synchronous. */
+int bcw_index_get(bcw_index* ix, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off, uint64_t* h_fid,
+                  uint64_t* h_off, uint64_t* h_size, uint8_t* h_status);
+/* The Put loops that rebuild the index from a decoded WAL (async, on the context stream, after
+ * bcw_decode_segment_async of d_seg on this index's context), for every delivered row in order:
+ *   BCW_MODE_RECORD  recoverFromWal  db_impl.go:305-313  Put(ns, key, fid, foff - 7, size)
+ *   BCW_MODE_HINT    recoverFromWal  db_impl.go:290-299  Put(ns, key, fid, hint.off, hint.size)
+ *                    use_record_fid: onePhase compaction.go:248-251  Put(ns, key, hint.fid, ...)
+ * Callers apply files in ascending fid order (db_impl.go:274-281): later calls override. d_out (device,
+ * may be NULL) receives the outcome. */
+int bcw_index_put_decoded_async(bcw_index* ix, const uint8_t* d_seg, const bcw_decode_params* p,
+                                const bcw_record_table* d_table, const bcw_decode_result* d_result, uint64_t fid,
+                                int use_record_fid, bcw_index_result* d_out);
+/* compactOneWal's doFilter (compaction.go:329-348) on the device, for every delivered row of a decoded
+ * data WAL: d_keep[i] = 1 when Index.Get(ns, key) succeeds and still points at (src_fid, foff - 7)
+ * (compaction.go:302), else 0 (rows not delivered: 0). The user CompactionFilter, when configured, stays a
+ * host callback over the kept rows. d_keep has the table's capacity; it feeds bcw_encode_segment_async
+ * directly (decode -> filter -> encode without leaving HBM). */
+int bcw_compact_filter_async(bcw_index* ix, const uint8_t* d_seg, const bcw_decode_params* p,
+                             const bcw_record_table* d_table, const bcw_decode_result* d_result, uint64_t src_fid,
+                             uint8_t* d_keep, bcw_index_result* d_out);
+/* Every live entry (merged key, fid, off, size), in no particular order, into host arrays (h_key_off has
+ * entries_cap + 1 entries). Returns BCW_E_CAPACITY when too small (*n_out / *key_bytes tell the sizes). */
+int bcw_index_export(bcw_index* ix, uint8_t* h_keys, uint64_t keys_cap, uint64_t* h_key_off, uint64_t* h_fid,
+                     uint64_t* h_off, uint64_t* h_size, uint64_t entries_cap, uint64_t* n_out, uint64_t* key_bytes);
+/* Synchronous compaction of one source WAL with the device filter: decode -> doFilter against the index
+ * -> Record.Encode + WriteRecord + hint append (compaction.go:294-327 with doFilter compaction.go:329-348
+ * and no user CompactionFilter), host in / host out like bcw_encode_segment. h_filter (may be NULL)
+ * receives the filter's outcome (n_done = rows kept). */
+int bcw_compact_segment(bcw_ctx* ctx, bcw_index* ix, const uint8_t* h_src, const bcw_encode_params* p,
+                        uint64_t src_fid, const bcw_encode_out* h_out, bcw_encode_result* h_result,
+                        bcw_index_result* h_filter);
+/* Synchronous recoverFromWal step (db_impl.go:286-313) for one file: decode h_seg (p->mode: BCW_MODE_HINT for a
+ * hint file, BCW_MODE_RECORD for a data WAL) and put every delivered row into the index. h_dres (may be
+ * NULL) receives the decode result: a hint file whose iteration failed is followed, as in the reference,
+ * by the data WAL of the same fid. */
+int bcw_index_recover_segment(bcw_ctx* ctx, bcw_index* ix, const uint8_t* h_seg, const bcw_decode_params* p,
+                              uint64_t fid, int use_record_fid, bcw_decode_result* h_dres, bcw_index_result* h_out);
+/* IndexOperator.Hash (index.go:15-19): murmur3 (spaolacci/murmur3 v1.1.0) New64().Sum64() on the host */
+uint64_t bcw_murmur3_sum64(const uint8_t* p, uint64_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -107,3 +107,14 @@ def test_wal_record_size_and_block_range():
 def test_reserve_fragments_rejects_oversize():
     # no device needed: the call only records a sizing hint (ctx NULL is refused)
     assert L.lib.bcw_ctx_reserve_fragments(None, 10) == -1
+
+
+def test_host_murmur3_matches_oracle():
+    from bitcaskdb_amd import murmur3_sum64
+    rng = random.Random(8)
+    for s in [b"", b"hello", b"hello, world", b"The quick brown fox jumps over the lazy dog."]:
+        assert murmur3_sum64(s) == O.murmur3_sum64(s)
+    assert murmur3_sum64(b"hello") == 0xcbd8a7b341bd9b02
+    for n in range(0, 140):
+        b = bytes(rng.getrandbits(8) for _ in range(n))
+        assert murmur3_sum64(b) == O.murmur3_sum64(b)

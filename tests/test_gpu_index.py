@@ -1,0 +1,198 @@
+"""GPU parity of the device index against the index oracle (oracle/bcw_oracle.c
+oc_index_*, itself pinned by murmur3 known answers and a Python model in test_index_oracle.py):
+Put/Delete/SoftDelete batches with the reference's sequential last-op-wins order, Get, growth, export,
+the recovery Put loops over hint / data WALs, and the device compaction filter feeding the re-encode."""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import cases
+from bitcaskdb_amd import _lib as L
+from bitcaskdb_amd import index as IX
+from bitcaskdb_amd import wal as W
+
+pytestmark = pytest.mark.gpu
+BASE = cases.BASE
+
+
+def _keyset(rng, n, ns=20):
+    out = []
+    for i in range(n):
+        nsb = bytes([65 + i % 5]) * ns
+        k = bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 7, 8, 15, 16, 17, 31, 100, 250])))
+        out.append((nsb, k + b"%d" % i))
+    return out
+
+
+def check_against_oracle(ix, oc, keys):
+    st, fid, off, size = ix.get_many([ns + k for ns, k in keys])
+    for j, (ns, k) in enumerate(keys):
+        ost, (of, oo, osz) = oc.get(ns, k)
+        assert st[j] == ost, (j, st[j], ost)
+        if ost != 1:
+            assert (fid[j], off[j], size[j]) == (of, oo, osz), j
+
+
+def test_index_batches_vs_oracle(ctx):
+    rng = random.Random(1)
+    keys = _keyset(rng, 3000)
+    ix = IX.Index(ctx, keys=1024, arena_bytes=1 << 16)  # small: the batches force growth (rehash)
+    oc = O.Index()
+    for batch in range(12):
+        n = rng.choice([1, 50, 2000, 9000])
+        ops, ks, fids, offs, sizes = [], [], [], [], []
+        for _ in range(n):
+            ns, k = rng.choice(keys)  # duplicates inside a batch: the last op wins
+            op = rng.choice([0, 0, 0, 0, 1, 2])
+            f, o, z = rng.randrange(1, 50), rng.randrange(40, 1 << 40), rng.randrange(5, 1 << 20)
+            ops.append(op)
+            ks.append(ns + k)
+            fids.append(f)
+            offs.append(o)
+            sizes.append(z)
+            oc.set(ns, k, op, f, o, z)
+        ix.apply(ops, ks, fids, offs, sizes)
+        check_against_oracle(ix, oc, keys + _keyset(random.Random(99), 50))
+    s = ix.stats()
+    assert s.live == oc.live() and s.overflow == 0 and s.slot_capacity > 1024
+    exp = ix.export()
+    assert len(exp) == oc.live()
+    for mk, v in exp.items():
+        st, ov = oc.get(mk[:20], mk[20:])
+        assert st != 1 and ov == v
+    # the reference's single-key interface and errors
+    ns, k = keys[0]
+    ix.put(ns, k, 7, 1234, 99)
+    assert ix.get(ns, k) == (7, 1234, 99)
+    ix.soft_delete(ns, k)
+    with pytest.raises(IX.ErrKeySoftDeleted):
+        ix.get(ns, k)
+    ix.delete(ns, k)
+    with pytest.raises(IX.ErrKeyNotFound):
+        ix.get(ns, k)
+    ix.close()
+
+
+def _wal_set(seed, nfiles=3, n=400, nkeys=500, vlens=(10, 300, 5000, 40000)):
+    rng = random.Random(seed)
+    files = {}
+    for fid in range(1, nfiles + 1):
+        payloads = [cases.rec(rng.randrange(0, nkeys), vlen=rng.choice(vlens)) for _ in range(n)]
+        data, _ = cases.wal_of(payloads)
+        ec, _, _, hint = O.hint_by_wal(data, fid, 40, BASE, 20, 20)
+        assert ec == 0
+        files[fid] = (data, hint)
+    return files
+
+
+def test_recover_from_hints_and_wals(ctx):
+    """recoverFromWals (db_impl.go:268-314): ascending fids, hint files preferred; a corrupted hint is
+    followed by its data WAL with the hint's earlier puts kept; the result equals the oracle's index."""
+    files = _wal_set(2)
+    fid2_data, fid2_hint = files[2]
+    bad = bytearray(fid2_hint)
+    bad[len(bad) // 2] ^= 0x21  # CRC failure mid-hint -> fall back to the WAL of fid 2
+    oc = O.Index()
+    for fid in sorted(files):
+        data, hint = files[fid]
+        h = bytes(bad) if fid == 2 else hint
+        ec, _ = oc.put_segment(h, 40, BASE, 20, 0, 1, fid)
+        if ec != 0:
+            assert fid == 2
+            assert oc.put_segment(data, 40, BASE, 20, 20, 0, fid)[0] == 0
+    ix = IX.Index(ctx)
+    IX.recover_from_wals(ix, {fid: (W.load_wal(d, fid), W.load_wal(bytes(bad) if fid == 2 else h, fid))
+                              for fid, (d, h) in files.items()})
+    exp = ix.export()
+    assert len(exp) == oc.live() == ix.stats().live
+    for mk, v in exp.items():
+        st, ov = oc.get(mk[:20], mk[20:])
+        assert st == 0 and ov == v
+
+
+def test_recover_onephase_record_fid(ctx):
+    """onePhase (compaction.go:248-251) puts hint.fid (the compaction output fid), recovery the file fid."""
+    data, _ = cases.wal_of([cases.rec(i, vlen=30) for i in range(100)])
+    ec, _, _, hint = O.hint_by_wal(data, 77, 40, BASE, 20, 20)
+    ix = IX.Index(ctx)
+    dres, ires = ix.recover_segment(hint, L.MODE_HINT, 5, 40, BASE, 20, 0, use_record_fid=True)
+    assert ires.err_class == 0 and ires.n_in == 100 == ires.n_done
+    assert {v[0] for v in ix.export().values()} == {77}
+    dres, ires = ix.recover_segment(hint, L.MODE_HINT, 5, 40, BASE, 20, 0)
+    assert {v[0] for v in ix.export().values()} == {5}
+
+
+def test_compaction_filter_fused(ctx):
+    """the device doFilter (compaction.go:329-348) over the oldest WAL after recovery: keep mask == the
+    oracle's, and the fused decode -> filter -> encode writes the same bytes as oc_compact_append with
+    that mask; soft-deleted and deleted keys are dropped."""
+    files = _wal_set(3, nfiles=3, n=600)
+    ix = IX.Index(ctx)
+    oc = O.Index()
+    for fid in sorted(files):
+        data, hint = files[fid]
+        ix.recover_segment(hint, L.MODE_HINT, fid, 40, BASE, 20, 0)
+        oc.put_segment(hint, 40, BASE, 20, 0, 1, fid)
+    # later writes: soft-delete / delete some keys (DBImpl.writeIndex, db_impl.go:433-452)
+    rng = random.Random(4)
+    ns = cases.sha1("ns")[:20]
+    ops, ks = [], []
+    for i in rng.sample(range(500), 60):
+        op = rng.choice([L.IDX_DELETE, L.IDX_SOFT_DELETE])
+        ops.append(op)
+        ks.append(ns + b"key-%06d" % i)
+        oc.set(ns, b"key-%06d" % i, op)
+    ix.apply(ops, ks)
+    src = files[1][0]
+    keep_ref, nv = oc.compact_filter(src, 40, BASE, 20, 20, 1, 600)
+    assert 0 < int(keep_ref.sum()) < 600
+    dst, hint = W.WalFile(9, BASE), W.WalFile(9, BASE)
+    offs, kept = IX.compact_one_wal_filtered(dst, hint, W.load_wal(src, 1), ix)
+    assert kept == int(keep_ref.sum())
+    rd, rh = O.Writer(BASE, BASE), O.Writer(BASE, BASE)
+    ec, _, nin, roffs = O.compact_append(rd, rh, 9, src, 40, BASE, BASE, 20, 20, keep_ref)
+    assert ec == 0 and bytes(dst.data) == rd.data() and bytes(hint.data) == rh.data()
+    np.testing.assert_array_equal(offs[:nin], roffs[:nin])
+
+
+def test_filter_zero_length_first_drops_live_record(ctx):
+    """a record whose First fragment is zero-length is indexed (Put at write time)
+    at its First header, but the iterator reports the next block -> doFilter drops the live record."""
+    first = cases.rec(0, vlen=0, klen=8)
+    target = 32768 - 7 - 7
+    filler = cases.rec(0, vlen=target - len(first), klen=8)
+    assert len(filler) == target
+    payloads = [filler] + [cases.rec(i, vlen=300, klen=8) for i in range(1, 30)]
+    data, offs = cases.wal_of(payloads)
+    ix, oc = IX.Index(ctx), O.Index()
+    ns = cases.sha1("ns")[:20]
+    keys = [p[p[0]:p[0] + 8] for p in payloads]
+    ix.apply([L.IDX_PUT] * len(payloads), [ns + k for k in keys], [1] * len(payloads), offs,
+             [len(p) for p in payloads])
+    for k, o, p in zip(keys, offs, payloads):
+        oc.put(ns, k, 1, o, len(p))
+    keep_ref, _ = oc.compact_filter(data, 40, BASE, 20, 20, 1, len(payloads))
+    assert keep_ref[1] == 0 and keep_ref.sum() == len(payloads) - 1
+    dst, hint = W.WalFile(9, BASE), W.WalFile(9, BASE)
+    _, kept = IX.compact_one_wal_filtered(dst, hint, W.load_wal(data, 1), ix)
+    assert kept == len(payloads) - 1
+
+
+def test_index_config_b_scale(ctx):
+    """the hint WAL of a 1 GiB config-B segment (~254 k keys) rebuilt into the device index, then the
+    device filter over the data WAL keeps every record (each key's latest copy is in this file)."""
+    data = O.synth(1 << 30, 0, 42)
+    ec, _, n, hint = O.hint_by_wal(data, 1, 40, BASE, 20, 20)
+    assert ec == 0
+    ix = IX.Index(ctx)
+    dres, ires = ix.recover_segment(hint, L.MODE_HINT, 1, 40, BASE, 20, 0)
+    assert ires.err_class == 0 and ires.n_done == n
+    assert ix.stats().live == n
+    dst, hint_w = W.WalFile(2, BASE), W.WalFile(2, BASE)
+    _, kept = IX.compact_one_wal_filtered(dst, hint_w, W.load_wal(data, 1), ix)
+    assert kept == n
+    assert bytes(dst.data)[40:] == data[40:]  # every record kept, same base time: the same bytes
