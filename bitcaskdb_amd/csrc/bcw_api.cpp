@@ -318,7 +318,13 @@ static void free_enc_scratch(EncScratch& e) {
   void* ptrs[] = {e.sz,    e.mflag, e.dsrc, e.da,      e.hda,       e.hsz,  e.dpos,
                   e.hpos,  e.tiles, e.ev,   e.evb,     e.recdesc,   e.recdesc_h, e.emisc};
   for (void* q : ptrs) (void)hipFree(q);
+  hipStream_t aux = e.aux;
+  hipEvent_t evs[3] = {e.ev_scan, e.ev_hscan, e.ev_desc};
   e = EncScratch{};
+  e.aux = aux;  // the auxiliary stream and its events live as long as the context
+  e.ev_scan = evs[0];
+  e.ev_hscan = evs[1];
+  e.ev_desc = evs[2];
 }
 
 int bcw_ctx_destroy(bcw_ctx* c) {
@@ -327,6 +333,11 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   if (c->cur) (void)hipStreamSynchronize(c->cur);
   free_scratch(c->s);
   free_enc_scratch(c->es);
+  if (c->es.aux) (void)hipStreamSynchronize(c->es.aux);
+  if (c->es.ev_scan) (void)hipEventDestroy(c->es.ev_scan);
+  if (c->es.ev_hscan) (void)hipEventDestroy(c->es.ev_hscan);
+  if (c->es.ev_desc) (void)hipEventDestroy(c->es.ev_desc);
+  if (c->es.aux) (void)hipStreamDestroy(c->es.aux);
   (void)hipFree(c->tabs.enc_ops);
   (void)hipFree(c->d_keep);
   (void)hipFree(c->d_eout);
@@ -614,6 +625,11 @@ static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows) {
             hipMalloc(&e.recdesc_h, r * enc_sizeof_recdesc()) == hipSuccess &&
             hipMalloc(&e.emisc, 64 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_enc_scratch(e); return BCW_E_NOMEM; }
+  if (!e.aux && (hipStreamCreateWithFlags(&e.aux, hipStreamNonBlocking) != hipSuccess ||
+                 hipEventCreateWithFlags(&e.ev_scan, hipEventDisableTiming) != hipSuccess ||
+                 hipEventCreateWithFlags(&e.ev_hscan, hipEventDisableTiming) != hipSuccess ||
+                 hipEventCreateWithFlags(&e.ev_desc, hipEventDisableTiming) != hipSuccess))
+    return BCW_E_HIP;
   (void)hipMemsetAsync(e.mflag, 0, r, c->cur);
   e.rows_cap = r;
   return BCW_OK;

@@ -123,14 +123,53 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 }
 
 // ------------------------------------------------------------------------------------------
-// Single-pass header chase with a decoupled look-back over workgroups: every thread chases one block
-// (holding its first kChaseHold headers in registers), the workgroup scans the counts, publishes its
-// aggregate and walks back over earlier workgroups' published values for its fragment base, then the
-// headers are written to the fragment table (blocks with more fragments chase their tail again).
-// Workgroups take tickets in launch order, so a workgroup only ever waits on ones already running.
-// Look-back words: epoch << 40 | flag << 38 | count (flag 1: aggregate, 2: inclusive prefix).
-constexpr int kChaseHold = 16;
+// Single-pass header chase with a decoupled look-back over workgroups: every thread chases one block,
+// the workgroup scans the counts, publishes its aggregate and walks back over earlier workgroups'
+// published values for its fragment base, then chases its block again (the header lines are now
+// cache-resident) writing the fragment table. Workgroups take tickets in launch order, so a workgroup
+// only ever waits on ones already running. Look-back words: epoch << 40 | flag << 38 | count
+// (flag 1: aggregate, 2: inclusive prefix).
+//
+// The chase is the iterator's header loop (wal_iterator.go:45-77: the block's buffer is
+// min(32768, Size - fileOff) bytes, a header is parsed while bufOff + 7 <= bufSize, the data length is
+// clamped to the buffer). It is a dependent chain of header reads; to shorten it, each round issues
+// kSpec header loads at once, at the positions the stride of the last fragment predicts (a run of
+// equal-length records: every 4 KiB-value block after its first two headers), and consumes them while
+// each one lies exactly where the previous header says the next one starts. A wrong guess costs only the
+// wasted loads: the round ends at the first mismatch and the next round starts from the true position.
+constexpr int kSpec = 8;
 constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
+
+// visit(k, start, len, crc, type) for every header of the block; returns the fragment count
+template <typename V>
+__device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg, uint64_t seg_len, uint64_t boff,
+                                                uint32_t bufsize, V&& visit) {
+  uint32_t n = 0, h = 0, s = 0;  // s: predicted distance to the next header (0: no prediction)
+  while (h + kHdr <= bufsize) {
+    uint32_t cr[kSpec], ln[kSpec], ty[kSpec];
+#pragma unroll
+    for (int j = 0; j < kSpec; ++j) {
+      const uint32_t p = h + (uint32_t)j * s;
+      cr[j] = ln[j] = ty[j] = 0;
+      if ((j == 0 || s != 0) && p + kHdr <= bufsize) read_header(seg, seg_len, boff + p, cr[j], ln[j], ty[j]);
+    }
+    // consume the round: header j is valid while it sits where the chain arrives
+    const uint32_t h0 = h, s0 = s;
+#pragma unroll
+    for (int j = 0; j < kSpec; ++j) {
+      if (h + kHdr > bufsize) break;
+      if (j > 0 && (s0 == 0 || h != h0 + (uint32_t)j * s0)) break;
+      const uint32_t start = h + kHdr;
+      uint32_t len = ln[j];
+      if (len > bufsize - start) len = bufsize - start;
+      visit(n, start, len, cr[j], ty[j]);
+      ++n;
+      h = start + len;
+      s = kHdr + len;
+    }
+  }
+  return n;
+}
 
 __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, uint64_t frag_cap, uint32_t b,
                                          uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
@@ -157,43 +196,13 @@ __global__ __launch_bounds__(256) void k_chase(const uint8_t* __restrict__ seg, 
   __syncthreads();
   const uint64_t wg = s_wg;
   const uint64_t b = wg * 256 + tid;
-  // WalIterator refill + header loop (wal_iterator.go:45-77): the block's buffer is
-  // min(32768, Size - fileOff) bytes, a header is parsed while bufOff + 7 <= bufSize, and the data
-  // length is clamped to the buffer
-  uint32_t hs[kChaseHold], hc[kChaseHold], ht[kChaseHold / 4];
-  uint32_t n = 0, h = 0, h_hold = 0, bufsize = 0;
+  uint32_t bufsize = 0;
   uint64_t boff = 0;
   if (b < nblocks) {
     boff = (uint64_t)start_off + b * kBlock;
     bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
   }
-#pragma unroll
-  for (int k = 0; k < kChaseHold / 4; ++k) ht[k] = 0;
-#pragma unroll
-  for (int k = 0; k < kChaseHold; ++k) {
-    hs[k] = 0;
-    hc[k] = 0;
-    if (h + kHdr <= bufsize) {
-      uint32_t crc, len, type;
-      read_header(seg, seg_len, boff + h, crc, len, type);
-      const uint32_t start = h + kHdr;
-      if (len > bufsize - start) len = bufsize - start;
-      hs[k] = start | (len << 16);
-      hc[k] = crc;
-      ht[k >> 2] |= type << (8 * (k & 3));
-      h = start + len;
-      ++n;
-    }
-  }
-  h_hold = h;
-  while (h + kHdr <= bufsize) {  // blocks with more fragments: count the rest
-    uint32_t crc, len, type;
-    read_header(seg, seg_len, boff + h, crc, len, type);
-    const uint32_t start = h + kHdr;
-    if (len > bufsize - start) len = bufsize - start;
-    h = start + len;
-    ++n;
-  }
+  const uint32_t n = chase_block(seg, seg_len, boff, bufsize, [](uint32_t, uint32_t, uint32_t, uint32_t, uint32_t) {});
   uint32_t tot;
   const uint32_t ex = wg256_excl_scan(n, sm4, tot);
   if (tid < 64) {  // wave 0: publish, then look back 64 workgroups per step
@@ -230,20 +239,9 @@ __global__ __launch_bounds__(256) void k_chase(const uint8_t* __restrict__ seg, 
   const uint64_t g0 = s_excl + ex;
   if (b < nblocks) {
     fbase[b] = (uint32_t)(g0 < 0xffffffffull ? g0 : 0xffffffffull);
-#pragma unroll
-    for (int k = 0; k < kChaseHold; ++k)
-      if ((uint32_t)k < n)
-        put_frag(frags, g0 + k, frag_cap, (uint32_t)b, hs[k] & 0xffffu, hs[k] >> 16, hc[k], (ht[k >> 2] >> (8 * (k & 3))) & 0xffu);
-    uint64_t g = g0 + kChaseHold;
-    h = h_hold;
-    while (h + kHdr <= bufsize) {  // the tail of a block with more than kChaseHold fragments
-      uint32_t crc, len, type;
-      read_header(seg, seg_len, boff + h, crc, len, type);
-      const uint32_t start = h + kHdr;
-      if (len > bufsize - start) len = bufsize - start;
-      put_frag(frags, g++, frag_cap, (uint32_t)b, start, len, crc, type);
-      h = start + len;
-    }
+    chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
+      put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type);
+    });
   }
   const uint64_t nwg = (nblocks + 255) / 256;
   if (wg == nwg - 1 && tid == 255) {
@@ -1278,8 +1276,10 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   const uint64_t tail = (p.seg_len - p.start_off) % kBlock;
   const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;
   pr.begin(K_RECORDS, stream, ev);
+  // every resident wave takes work items (runs of blocks holding ~64 fragments): 4 workgroups of 4 waves
+  // per CU (the VGPR / LDS limit), one item per wave at config B
   uint64_t rec_wgs = (nblocks + kRecWaves - 1) / kRecWaves;
-  if (rec_wgs > (uint64_t)num_cus * 2) rec_wgs = (uint64_t)num_cus * 2;
+  if (rec_wgs > (uint64_t)num_cus * 4) rec_wgs = (uint64_t)num_cus * 4;
   k_records<<<(uint32_t)rec_wgs, 64 * kRecWaves, 0, stream>>>(
       d_seg, p.seg_len, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg, s.wgx, nw, t, s.misc, tail_panic,
       gen, d_result);

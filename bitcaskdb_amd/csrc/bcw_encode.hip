@@ -41,7 +41,7 @@ constexpr uint32_t kL = kBlock;           // 32768
 constexpr uint32_t kM = kBlock - kHdr;    // 32761
 constexpr int kTileItems = 4096;          // scan tile: 256 threads x 16 items
 constexpr int kEvThreads = 1024;
-constexpr int kEvWin = 4096;  // records per k_events step
+constexpr int kEvWin = 8192;  // records per k_events window
 constexpr int kEvPer = kEvWin / kEvThreads;
 
 // emisc slots
@@ -296,11 +296,12 @@ struct Ev {
   uint32_t pad;
 };
 
-// One workgroup of kEvThreads, kEvWin = kEvThreads * kEvPer records per window in registers. A round:
-// every thread tests its records after the last event against rho, the wave minima meet in LDS, and
-// the owner of the first hit records the event and advances the scan state. Rounds per window =
-// events in it + 1. (Measured against a barrier-free scanner wave fed by loader waves and against a
-// one-barrier-per-round replay from LDS: both slower)
+// One workgroup of kEvThreads, kEvWin = kEvThreads * kEvPer records per window in registers (the next
+// window's coordinates are loaded while this one is scanned). A round: every thread tests its records
+// after the last event against rho; each wave's first hit (its owner lane publishes {index, a}) goes to
+// LDS; after ONE barrier every thread reads the 16 wave minima and advances the scan state itself
+// (all threads hold the same state, thread 0 records the event). The LDS slots alternate between two
+// buffers so the next round's writes never meet this round's reads. Rounds per window = events + 1.
 __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restrict__ da, uint64_t* __restrict__ emisc,
                                                         int lay, uint64_t q0, Ev* __restrict__ ev,
                                                         uint32_t* __restrict__ evb) {
@@ -309,87 +310,85 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
   const uint64_t AN = X[0];
   const int64_t U = (int64_t)(q0 % kL);
   const uint64_t b0 = q0 / kL;
-  __shared__ int64_t s_ya;
-  __shared__ uint64_t s_kb;
-  __shared__ uint32_t s_rho, s_nev, s_best;
-  __shared__ uint32_t s_wmin[kEvThreads / 64];
-  if (threadIdx.x == 0) {
-    ev[0] = {b0, -U, 0xffffffffu, 0};
-    int64_t ya = -U;
-    uint64_t kb = b0;
-    uint32_t nev = 1;
-    uint32_t rho = (uint32_t)((kL - U) % kM);  // the virtual block ends at y = L - U
-    if (N > 0 && kL - U < (int64_t)kHdr) {    // record 0's header does not fit: pad, event at record 0
-      ev[1] = {b0 + 1, 0, 0u, (uint32_t)(kL - U)};
-      ya = 0;
-      kb = b0 + 1;
-      nev = 2;
-      rho = kL % kM;
-    }
-    s_ya = ya; s_kb = kb; s_rho = rho; s_nev = nev;
+  struct Hit {
+    uint32_t q, pad;
+    uint64_t a;
+  };
+  __shared__ Hit s_hit[2][kEvThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  // scan state, identical in every thread
+  int64_t ya = -U;
+  uint64_t kb = b0;
+  uint32_t nev = 1;
+  uint32_t rho = (uint32_t)((kL - U) % kM);  // the virtual block ends at y = L - U
+  if (tid == 0) ev[0] = {b0, -U, 0xffffffffu, 0};
+  if (N > 0 && kL - U < (int64_t)kHdr) {    // record 0's header does not fit: pad, event at record 0
+    if (tid == 0) ev[1] = {b0 + 1, 0, 0u, (uint32_t)(kL - U)};
+    ya = 0;
+    kb = b0 + 1;
+    nev = 2;
+    rho = kL % kM;
   }
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t an[kEvPer];  // the next window's coordinates, in flight
+#pragma unroll
+  for (int k = 0; k < kEvPer; ++k) {
+    const uint64_t idx = (uint64_t)k * kEvThreads + tid;
+    an[k] = idx < N ? da[idx] : 0;
+  }
+  uint32_t par = 0;
   for (uint64_t base = 0; base < N; base += kEvWin) {
-    if (threadIdx.x == 0) evb[base / kEvWin] = s_nev - 1;
+    if (tid == 0) evb[base / kEvWin] = nev - 1;
     uint64_t a[kEvPer];
     uint32_t r[kEvPer];
 #pragma unroll
     for (int k = 0; k < kEvPer; ++k) {
-      const uint64_t idx = base + (uint64_t)k * kEvThreads + threadIdx.x;
-      a[k] = idx < N ? da[idx] : 0;
+      a[k] = an[k];
       r[k] = (uint32_t)(a[k] % kM);
+      const uint64_t idx = base + kEvWin + (uint64_t)k * kEvThreads + tid;
+      an[k] = idx < N ? da[idx] : 0;
     }
     // record 0 is never tested against the virtual event (its header is in block b0 or it is ev[1])
-    int last = (base == 0) ? 0 : -1;
-    uint32_t rho = s_rho;
+    int32_t last = (base == 0) ? 0 : -1;
     for (;;) {
       uint32_t best = 0xffffffffu;
+      uint64_t abest = 0;
 #pragma unroll
       for (int k = kEvPer - 1; k >= 0; --k) {
-        const uint32_t q = (uint32_t)k * kEvThreads + threadIdx.x;
-        const uint64_t idx = base + q;
-        if (idx < N && (int)q > last) {
+        const uint32_t q = (uint32_t)k * kEvThreads + tid;
+        if (base + q < N && (int32_t)q > last) {
           int32_t d = (int32_t)rho - (int32_t)r[k];
           if (d < 0) d += kM;
-          if (d <= 6) best = q;
+          if (d <= 6) { best = q; abest = a[k]; }
         }
       }
-      for (int d = 32; d >= 1; d >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, d, 64));
-      if (lane == 0) s_wmin[wave] = best;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint32_t m = 0xffffffffu;
-        for (int w = 0; w < kEvThreads / 64; ++w) m = min(m, s_wmin[w]);
-        s_best = m;
-      }
-      __syncthreads();
-      const uint32_t b = s_best;
-      if (b == 0xffffffffu) break;
-      if (threadIdx.x == (b & (kEvThreads - 1))) {  // the owner records the event
-        const int k = (int)(b / kEvThreads);
-        uint64_t ai = a[0];
-        uint32_t ri = r[0];
+      uint32_t m = best;
 #pragma unroll
-        for (int kk = 1; kk < kEvPer; ++kk) if (kk == k) { ai = a[kk]; ri = r[kk]; }
-        int32_t d = (int32_t)s_rho - (int32_t)ri;
-        if (d < 0) d += kM;
-        const int64_t E = (int64_t)ai + d;                         // block end that hits the header
-        const uint64_t m = (uint64_t)(E - s_ya - (int64_t)kL) / kM;  // blocks after the event block
-        const uint64_t kb = s_kb + m + 1;
-        ev[s_nev] = {kb, (int64_t)ai, (uint32_t)(base + b), (uint32_t)d};
-        s_nev = s_nev + 1;
-        s_kb = kb;
-        s_ya = (int64_t)ai;
-        s_rho = (ri + kHdr) % kM;
-      }
+      for (int d = 32; d >= 1; d >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, d, 64));
+      if (best == m && (m == 0xffffffffu ? lane == 0 : true)) s_hit[par][wave] = {m, 0u, abest};
       __syncthreads();
-      rho = s_rho;
-      last = (int)b;
+      uint32_t b = 0xffffffffu;
+      uint64_t ab = 0;
+#pragma unroll
+      for (int w = 0; w < kEvThreads / 64; ++w) {
+        const Hit h = s_hit[par][w];
+        if (h.q < b) { b = h.q; ab = h.a; }
+      }
+      par ^= 1u;
+      if (b == 0xffffffffu) break;
+      const uint32_t rb = (uint32_t)(ab % kM);
+      int32_t d = (int32_t)rho - (int32_t)rb;
+      if (d < 0) d += kM;
+      const int64_t E = (int64_t)ab + d;                            // block end that hits the header
+      const uint64_t mb = (uint64_t)(E - ya - (int64_t)kL) / kM;   // blocks after the event block
+      kb = kb + mb + 1;
+      if (tid == 0) ev[nev] = {kb, (int64_t)ab, (uint32_t)(base + b), (uint32_t)d};
+      ++nev;
+      ya = (int64_t)ab;
+      rho = (rb + kHdr) % kM;
+      last = (int32_t)b;
     }
   }
-  if (threadIdx.x == 0) {
-    const uint32_t nev = s_nev;
+  if (tid == 0) {
     X[1] = nev;
     X[4] = b0;
     X[5] = (uint64_t)U;
@@ -397,8 +396,6 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
       X[2] = b0 - 1;  // no blocks
       X[3] = 40 + q0;
     } else {
-      const int64_t ya = s_ya;
-      const uint64_t kb = s_kb;
       // the block whose end E_k >= A_N first: E_kb = ya + L, E_{kb+m} = ya + L + m M
       const int64_t over = (int64_t)AN - ya - (int64_t)kL;
       const uint64_t m = over > 0 ? ((uint64_t)over + kM - 1) / kM : 0;
@@ -1239,9 +1236,15 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     pr.end(kid, st, ev0);
   };
   if (compact) {
+    // stream st: the layouts (two serial one-workgroup event scans) and the writers; stream aux: the
+    // payload descriptors of the dst records (after the dense scan) and of the hint records (after the
+    // dst offsets), built while the event scans run
     pr.begin(K_ENC_SCAN, st, ev0);
     scan(s.sz, 1, 0, s.da);
     pr.end(K_ENC_SCAN, st, ev0);
+    (void)hipEventRecord(s.ev_scan, st);
+    (void)hipStreamWaitEvent(s.aux, s.ev_scan, 0);
+    k_recdesc_w<PM_DST><<<rgrid, 256, 0, s.aux>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, wd);
     layout(0, s.da, L.p.wal_pos);
     k_recoff<<<rgrid, 256, 0, st>>>(s.da, s.dsrc, s.emisc, 0, evs, s.evb, s.dpos, L.out.rec_off);
     // the hint WAL's layout needs the dst offsets (its records carry them)
@@ -1249,9 +1252,13 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     k_hint_sizes<<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.hsz);
     scan(s.hsz, 0, 1, s.hda);
     pr.end(K_ENC_HINT_LAYOUT, st, ev0);
+    (void)hipEventRecord(s.ev_hscan, st);
+    (void)hipStreamWaitEvent(s.aux, s.ev_hscan, 0);
+    k_recdesc_w<PM_HINT_DST><<<rgrid, 256, 0, s.aux>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag, wh);
+    (void)hipEventRecord(s.ev_desc, s.aux);
     layout(1, s.hda, L.p.hint_pos);
     k_recoff<<<rgrid, 256, 0, st>>>(s.hda, s.dsrc, s.emisc, 1, evs, s.evb, s.hpos, nullptr);
-    // both WALs in one persistent launch: dst records, then hint records
+    (void)hipStreamWaitEvent(st, s.ev_desc, 0);
     W.w[0] = WLay{s.da, s.dpos, wd, L.out.wal, L.p.wal_pos, L.out.wal_cap, 0};
     W.w[1] = WLay{s.hda, s.hpos, wh, L.out.hint, L.p.hint_pos, L.out.hint_cap, 1};
     W.nlay = 1;
@@ -1260,8 +1267,6 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     static const int abl = [] { const char* v = getenv("BCW_ENC_ABL"); return v ? atoi(v) : 0; }();
     static const int hg = [] { const char* v = getenv("BCW_HINT_G"); return v ? atoi(v) : 8; }();
     pr.begin(K_ENC_WRITE, st, ev0);
-    k_recdesc_w<PM_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, wd);
-    k_recdesc_w<PM_HINT_DST><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag, wh);
     // measurement-only ablation (BCW_ENC_ABL: 1 = dst WAL only, 2 = hint WAL only); 0 in the product
     if (abl != 2) k_write<16><<<wgrid(16), kWT, 0, st>>>(W);
     if (abl != 1) {

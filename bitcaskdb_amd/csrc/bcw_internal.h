@@ -133,6 +133,9 @@ struct EncScratch {
   void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc_w -> k_write), dst WAL
   void* recdesc_h = nullptr;  // [rows] the same for the hint WAL
   uint64_t* emisc = nullptr;  // [64] counters
+  // the payload descriptors are built on an auxiliary stream while the serial layout scans run
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_scan = nullptr, ev_hscan = nullptr, ev_desc = nullptr;
 };
 
 struct EncLaunch {

@@ -3,6 +3,7 @@
 #include "../../bitcaskdb_amd/csrc/bcw_api.cpp"
 #include "../../bitcaskdb_amd/csrc/bcw_decode.hip"
 #include "../../bitcaskdb_amd/csrc/bcw_encode.hip"
+#include "../../bitcaskdb_amd/csrc/bcw_index.hip"
 
 #include <cstdio>
 #include <cstdlib>
