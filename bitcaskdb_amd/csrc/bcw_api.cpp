@@ -167,6 +167,7 @@ const char* bcw_strerror(int code) {
     case BCW_E_NOMEM: return "out of memory";
     case BCW_E_CAPACITY: return "output capacity too small";
     case BCW_E_NODEVICE: return "no HIP device";
+    case BCW_E_IO: return "file read / write failed";
     default: return "unknown error";
   }
 }
@@ -379,7 +380,7 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   const uint64_t nb = std::max(nblocks, s.nblocks_cap);
   const uint64_t fc = std::max(frag_cap, s.frag_cap);
   free_scratch(s);
-  const uint64_t nwg = nb / 256 + 2;
+  const uint64_t nwg = nb / 64 + 2;  // k_chase look-back words: one per 64-block workgroup
   bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
             hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
             hipMalloc(&s.pre, (nb + 1) * sizeof(Xf)) == hipSuccess &&

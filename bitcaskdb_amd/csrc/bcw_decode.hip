@@ -123,49 +123,58 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 }
 
 // ------------------------------------------------------------------------------------------
-// Single-pass header chase with a decoupled look-back over workgroups: every thread chases one block,
-// the workgroup scans the counts, publishes its aggregate and walks back over earlier workgroups'
-// published values for its fragment base, then chases its block again (the header lines are now
-// cache-resident) writing the fragment table. Workgroups take tickets in launch order, so a workgroup
-// only ever waits on ones already running. Look-back words: epoch << 40 | flag << 38 | count
-// (flag 1: aggregate, 2: inclusive prefix).
+// Single-pass header chase with a decoupled look-back over workgroups: every lane of a one-wave
+// workgroup chases one block (keeping its first kChaseHold headers in LDS), the wave scans the counts,
+// publishes its aggregate and walks back over earlier workgroups' published values for its fragment
+// base, then writes the fragment table (a block with more headers chases its tail again; the lines are
+// cache-resident by then). Workgroups take tickets in launch order, so a workgroup only ever waits on
+// ones already running. Look-back words: epoch << 40 | flag << 38 | count (flag 1: aggregate,
+// 2: inclusive prefix). One wave per workgroup spreads the blocks over every CU: the chase is a chain
+// of scattered header reads, bound by latency and by each CU's address-processing rate.
 //
 // The chase is the iterator's header loop (wal_iterator.go:45-77: the block's buffer is
 // min(32768, Size - fileOff) bytes, a header is parsed while bufOff + 7 <= bufSize, the data length is
-// clamped to the buffer). It is a dependent chain of header reads; to shorten it, each round issues
-// kSpec header loads at once, at the positions the stride of the last fragment predicts (a run of
-// equal-length records: every 4 KiB-value block after its first two headers), and consumes them while
-// each one lies exactly where the previous header says the next one starts. A wrong guess costs only the
-// wasted loads: the round ends at the first mismatch and the next round starts from the true position.
+// clamped to the buffer), a dependent chain of header reads. To shorten it, once two consecutive Full
+// fragments of the block had the same length (a run of equal-size records, as in every 4 KiB-value
+// block), a round issues kSpec header loads at once at the positions that stride predicts and consumes
+// them while each lies exactly where the chain arrives; the round ends at the first mismatch and the
+// next one starts from the true position. Without that evidence a round reads one header.
 constexpr int kSpec = 8;
+constexpr int kChaseHold = 16;
 constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
 
 // visit(k, start, len, crc, type) for every header of the block; returns the fragment count
 template <typename V>
 __device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg, uint64_t seg_len, uint64_t boff,
                                                 uint32_t bufsize, V&& visit) {
-  uint32_t n = 0, h = 0, s = 0;  // s: predicted distance to the next header (0: no prediction)
+  uint32_t n = 0, h = 0;
+  uint32_t s = 0;      // predicted distance to the next header (0: read one header)
+  uint32_t lfull = 0;  // length of the last Full fragment (+1; 0: none)
   while (h + kHdr <= bufsize) {
     uint32_t cr[kSpec], ln[kSpec], ty[kSpec];
+    read_header(seg, seg_len, boff + h, cr[0], ln[0], ty[0]);
 #pragma unroll
-    for (int j = 0; j < kSpec; ++j) {
+    for (int j = 1; j < kSpec; ++j) {
       const uint32_t p = h + (uint32_t)j * s;
       cr[j] = ln[j] = ty[j] = 0;
-      if ((j == 0 || s != 0) && p + kHdr <= bufsize) read_header(seg, seg_len, boff + p, cr[j], ln[j], ty[j]);
+      if (s != 0 && p + kHdr <= bufsize) read_header(seg, seg_len, boff + p, cr[j], ln[j], ty[j]);
     }
-    // consume the round: header j is valid while it sits where the chain arrives
     const uint32_t h0 = h, s0 = s;
 #pragma unroll
     for (int j = 0; j < kSpec; ++j) {
-      if (h + kHdr > bufsize) break;
-      if (j > 0 && (s0 == 0 || h != h0 + (uint32_t)j * s0)) break;
+      if (j > 0 && (s0 == 0 || h != h0 + (uint32_t)j * s0 || h + kHdr > bufsize)) break;
       const uint32_t start = h + kHdr;
       uint32_t len = ln[j];
       if (len > bufsize - start) len = bufsize - start;
       visit(n, start, len, cr[j], ty[j]);
       ++n;
       h = start + len;
-      s = kHdr + len;
+      if (ty[j] == BCW_RECORD_FULL) {
+        s = (lfull == len + 1) ? kHdr + len : 0;
+        lfull = len + 1;
+      } else {
+        s = 0;
+      }
     }
   }
   return n;
@@ -185,67 +194,74 @@ __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, u
   frags[g] = f;
 }
 
-__global__ __launch_bounds__(256) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
-                                               uint64_t nblocks, uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
-                                               uint64_t frag_cap, uint64_t* __restrict__ lb, uint64_t* __restrict__ misc,
-                                               uint64_t ticket_base, uint64_t epoch) {
-  __shared__ uint32_t sm4[4];
-  __shared__ uint64_t s_wg, s_excl;
-  const uint32_t tid = threadIdx.x;
-  if (tid == 0) s_wg = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_TICKET]), 1ull) - ticket_base;
-  __syncthreads();
-  const uint64_t wg = s_wg;
-  const uint64_t b = wg * 256 + tid;
+__global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
+                                              uint64_t nblocks, uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
+                                              uint64_t frag_cap, uint64_t* __restrict__ lb, uint64_t* __restrict__ misc,
+                                              uint64_t ticket_base, uint64_t epoch) {
+  __shared__ uint32_t s_hold[kChaseHold][3][64];  // {crc, start | len << 16, type} of each lane's headers
+  const uint32_t lane = threadIdx.x;
+  uint64_t wg = 0;
+  if (lane == 0) wg = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_TICKET]), 1ull) - ticket_base;
+  wg = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)wg) |
+       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wg >> 32)) << 32);
+  const uint64_t b = wg * 64 + lane;
   uint32_t bufsize = 0;
   uint64_t boff = 0;
   if (b < nblocks) {
     boff = (uint64_t)start_off + b * kBlock;
     bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
   }
-  const uint32_t n = chase_block(seg, seg_len, boff, bufsize, [](uint32_t, uint32_t, uint32_t, uint32_t, uint32_t) {});
-  uint32_t tot;
-  const uint32_t ex = wg256_excl_scan(n, sm4, tot);
-  if (tid < 64) {  // wave 0: publish, then look back 64 workgroups per step
-    const uint32_t lane = tid;
-    const uint64_t tag = epoch << 40;
-    if (lane == 0)
-      __hip_atomic_store(&lb[wg], tag | ((wg == 0 ? kLbInc : kLbAgg) << 38) | tot, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t excl = 0;
-    for (uint64_t top = wg; top > 0;) {  // predecessors [top - 64, top)
-      const uint64_t q = top - 1 - lane;  // lane 0: the nearest
-      uint64_t v = 0;
-      if (top > lane) {
-        while (((v = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
-          __builtin_amdgcn_s_sleep(1);
-      }
-      const uint64_t inc = __ballot(top > lane && ((v >> 38) & 3u) == kLbInc);
-      const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive prefix
-      uint64_t c = (lane <= stop && top > lane) ? (v & kLbMask) : 0ull;
+  const uint32_t n = chase_block(seg, seg_len, boff, bufsize,
+                                 [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
+                                   if (k < (uint32_t)kChaseHold) {
+                                     s_hold[k][0][lane] = crc;
+                                     s_hold[k][1][lane] = start | (len << 16);
+                                     s_hold[k][2][lane] = type;
+                                   }
+                                 });
+  const uint32_t incl = wave_add_scan(n, lane);
+  const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+  // publish, then look back 64 workgroups per step
+  const uint64_t tag = epoch << 40;
+  if (lane == 0)
+    __hip_atomic_store(&lb[wg], tag | ((wg == 0 ? kLbInc : kLbAgg) << 38) | tot, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t excl = 0;
+  for (uint64_t top = wg; top > 0;) {  // predecessors [top - 64, top)
+    const uint64_t q = top - 1 - lane;  // lane 0: the nearest
+    uint64_t v = 0;
+    if (top > lane) {
+      while (((v = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    const uint64_t inc = __ballot(top > lane && ((v >> 38) & 3u) == kLbInc);
+    const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive prefix
+    uint64_t c = (lane <= stop && top > lane) ? (v & kLbMask) : 0ull;
 #pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) c += (uint64_t)__shfl_xor((long long)c, d, 64);
-      excl += c;
-      if (inc) break;
-      top = top > 64 ? top - 64 : 0;
-    }
-    if (lane == 0) {
-      if (wg != 0)
-        __hip_atomic_store(&lb[wg], tag | (kLbInc << 38) | ((excl + tot) & kLbMask), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      s_excl = excl;
-    }
+    for (int d = 32; d >= 1; d >>= 1) c += (uint64_t)__shfl_xor((long long)c, d, 64);
+    excl += c;
+    if (inc) break;
+    top = top > 64 ? top - 64 : 0;
   }
-  __syncthreads();
-  const uint64_t g0 = s_excl + ex;
+  if (lane == 0 && wg != 0)
+    __hip_atomic_store(&lb[wg], tag | (kLbInc << 38) | ((excl + tot) & kLbMask), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t g0 = excl + incl - n;
   if (b < nblocks) {
     fbase[b] = (uint32_t)(g0 < 0xffffffffull ? g0 : 0xffffffffull);
-    chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
-      put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type);
-    });
+    const uint32_t nh = n < (uint32_t)kChaseHold ? n : (uint32_t)kChaseHold;
+    for (uint32_t k = 0; k < nh; ++k) {
+      const uint32_t sl = s_hold[k][1][lane];
+      put_frag(frags, g0 + k, frag_cap, (uint32_t)b, sl & 0xffffu, sl >> 16, s_hold[k][0][lane], s_hold[k][2][lane]);
+    }
+    if (n > (uint32_t)kChaseHold)  // the tail of a block with more headers than held
+      chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
+        if (k >= (uint32_t)kChaseHold) put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type);
+      });
   }
-  const uint64_t nwg = (nblocks + 255) / 256;
-  if (wg == nwg - 1 && tid == 255) {
-    const uint64_t total = s_excl + tot;
+  const uint64_t nwg = (nblocks + 63) / 64;
+  if (wg == nwg - 1 && lane == 63) {
+    const uint64_t total = excl + tot;
     fbase[nblocks] = (uint32_t)(total < 0xffffffffull ? total : 0xffffffffull);
     misc[M_NFRAGS] = total;
     misc[M_DONE_CRC] = 0;  // k_crc's workgroup completion counter
@@ -1258,9 +1274,9 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   Prof dummy;
   Prof& pr = prof ? *prof : dummy;
   hipEvent_t ev = nullptr;
-  const uint32_t nb_grid = (uint32_t)((nblocks + 255) / 256);
+  const uint32_t nb_grid = (uint32_t)((nblocks + 63) / 64);
   pr.begin(K_CHASE, stream, ev);
-  k_chase<<<nb_grid, 256, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags, s.frag_cap, s.lb,
+  k_chase<<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags, s.frag_cap, s.lb,
                                        s.misc, s.tickets, s.epoch);
   pr.end(K_CHASE, stream, ev);
   s.tickets += nb_grid;

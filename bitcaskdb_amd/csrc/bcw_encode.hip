@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
   const int64_t U = (int64_t)(q0 % kL);
   const uint64_t b0 = q0 / kL;
   struct Hit {
-    uint32_t q, pad;
+    uint32_t q, r;  // window index and residue of the wave's first hit
     uint64_t a;
   };
   __shared__ Hit s_hit[2][kEvThreads / 64];
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
     // record 0 is never tested against the virtual event (its header is in block b0 or it is ev[1])
     int32_t last = (base == 0) ? 0 : -1;
     for (;;) {
-      uint32_t best = 0xffffffffu;
+      uint32_t best = 0xffffffffu, rbest = 0;
       uint64_t abest = 0;
 #pragma unroll
       for (int k = kEvPer - 1; k >= 0; --k) {
@@ -358,24 +358,28 @@ __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restric
         if (base + q < N && (int32_t)q > last) {
           int32_t d = (int32_t)rho - (int32_t)r[k];
           if (d < 0) d += kM;
-          if (d <= 6) { best = q; abest = a[k]; }
+          if (d <= 6) { best = q; abest = a[k]; rbest = r[k]; }
         }
       }
       uint32_t m = best;
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, d, 64));
-      if (best == m && (m == 0xffffffffu ? lane == 0 : true)) s_hit[par][wave] = {m, 0u, abest};
+      if (best == m && (m == 0xffffffffu ? lane == 0 : true)) s_hit[par][wave] = {m, rbest, abest};
       __syncthreads();
-      uint32_t b = 0xffffffffu;
-      uint64_t ab = 0;
+      // lanes 0..15 of every wave read one wave's hit each; the minimum is found with shuffles
+      Hit hh{0xffffffffu, 0u, 0ull};
+      if (lane < (uint32_t)(kEvThreads / 64)) hh = s_hit[par][lane];
+      uint32_t mq = hh.q;
 #pragma unroll
-      for (int w = 0; w < kEvThreads / 64; ++w) {
-        const Hit h = s_hit[par][w];
-        if (h.q < b) { b = h.q; ab = h.a; }
-      }
+      for (int d = 8; d >= 1; d >>= 1) mq = min(mq, (uint32_t)__shfl_xor((int)mq, d, 64));
+      const uint32_t b = __builtin_amdgcn_readfirstlane(mq);
       par ^= 1u;
       if (b == 0xffffffffu) break;
-      const uint32_t rb = (uint32_t)(ab % kM);
+      const uint64_t own = __ballot(lane < (uint32_t)(kEvThreads / 64) && hh.q == b);
+      const uint32_t ol = (uint32_t)__builtin_ctzll(own);
+      const uint32_t rb = __builtin_amdgcn_readlane(hh.r, ol);
+      const uint64_t ab = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)hh.a, ol) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(hh.a >> 32), ol) << 32);
       int32_t d = (int32_t)rho - (int32_t)rb;
       if (d < 0) d += kM;
       const int64_t E = (int64_t)ab + d;                            // block end that hits the header

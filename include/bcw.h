@@ -45,6 +45,7 @@ extern "C" {
 #define BCW_E_NOMEM (-3)      /* device / host allocation failed */
 #define BCW_E_CAPACITY (-4)   /* output table too small: see bcw_decode_result.n_records_total */
 #define BCW_E_NODEVICE (-5)   /* no HIP device */
+#define BCW_E_IO (-6)         /* a pread / pwrite failed or hit end of file */
 
 /* ---- reference constants (wal.go:45-58, record.go:44-48) ---- */
 #define BCW_BLOCK_SIZE 32768u
@@ -386,6 +387,25 @@ int bcw_index_recover_segment(bcw_ctx* ctx, bcw_index* ix, const uint8_t* h_seg,
                               uint64_t fid, int use_record_fid, bcw_decode_result* h_dres, bcw_index_result* h_out);
 /* IndexOperator.Hash (index.go:15-19): murmur3 (spaolacci/murmur3 v1.1.0) New64().Sum64() on the host */
 uint64_t bcw_murmur3_sum64(const uint8_t* p, uint64_t n);
+
+/* ---- host I/O staging: WAL files <-> HBM through pinned slices ---------------------------------------
+ * The reference reads a segment with PreadFull per 32 KiB block (utils.go:32-48, wal_iterator.go:55)
+ * and writes the rewritten WAL through a buffer flushed every >= 1 MiB (WalRewriter
+ * wal_rewriter.go:37-49 -> Wal.Flush wal.go:451-465). A stage owns `nslices` pinned host buffers of
+ * `slice_bytes`; reads pread whole slices (up to `threads` reader threads) while earlier slices are
+ * already copied to the device, writes copy slices back and pwrite each one while the next is in flight.
+ * Copies are queued on hip_stream (a hipStream_t; NULL: the context's stream), so a decode launched on
+ * that stream after bcw_stage_read returns sees the whole segment. */
+typedef struct bcw_stage bcw_stage;
+int bcw_stage_create(bcw_ctx* ctx, uint64_t slice_bytes, uint32_t nslices, bcw_stage** out);
+int bcw_stage_destroy(bcw_stage* st);
+/* len bytes of fd at file_off -> d_dst (device). Returns BCW_E_IO on a read error or a short file. */
+int bcw_stage_read(bcw_stage* st, int fd, uint64_t file_off, uint64_t len, uint8_t* d_dst, void* hip_stream,
+                   uint32_t threads);
+/* len bytes of d_src (device) -> fd at file_off (waits for the work queued on hip_stream before each
+ * slice, then pwrites it). Synchronous: returns once every byte is written. */
+int bcw_stage_write(bcw_stage* st, int fd, uint64_t file_off, const uint8_t* d_src, uint64_t len,
+                    void* hip_stream);
 
 #ifdef __cplusplus
 }
