@@ -1108,6 +1108,9 @@ __device__ __forceinline__ void finalize(uint64_t* __restrict__ misc, uint64_t n
   *res = r;
 }
 
+// ABL: ablation bits for tools/kbench only (0 in the product): 1 no parse, 2 no prefix staging loads,
+// 4 no table stores, 8 no finalize
+template <int ABL = 0>
 __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                  bcw_decode_params p, const Frag* __restrict__ frags,
                                                  const uint32_t* __restrict__ fbase, uint64_t nblocks,
@@ -1206,15 +1209,21 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
       const uint64_t base = a0 & ~15ull;
       const uint32_t sh = (uint32_t)(a0 - base);
       const uint32_t nld = (uint32_t)((sh + want + 15) >> 4);
-      for (uint32_t k = 0; k < nld; ++k) {
-        const uint64_t o = base + 16 * k;
-        *reinterpret_cast<uint4*>(st + 16 * k) = load16_safe(seg, seg_len, (int64_t)o);
-      }
+      if (!(ABL & 2))
+        for (uint32_t k = 0; k < nld; ++k) {
+          const uint64_t o = base + 16 * k;
+          *reinterpret_cast<uint4*>(st + 16 * k) = load16_safe(seg, seg_len, (int64_t)o);
+        }
       RecReader rd{seg, frags, p.start_off, st + sh, (uint32_t)want, src, (uint32_t)g, src, 0, f0.len, a0};
       uint8_t status, hdr, flags, etag_off;
       uint64_t key_len, val_len, meta_len, expire, aux0, aux1;
-      parse_record(p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
-      if (r < tab.capacity) {
+      if (!(ABL & 1)) {
+        parse_record(p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
+      } else {
+        status = hdr = flags = etag_off = 0;
+        key_len = val_len = meta_len = expire = aux0 = aux1 = 0;
+      }
+      if (!(ABL & 4) && r < tab.capacity) {
         tab.foff[r] = foff;
         tab.size[r] = size;
         tab.expire[r] = expire;
@@ -1248,7 +1257,7 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint64_t done = __hip_atomic_fetch_add(&misc[M_DONE_REC], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == gridDim.x - 1u) finalize(misc, nblocks, misc[M_NFRAGS], frag_cap, frags, p.start_off, tail_panic, gen, res);
+    if (!(ABL & 8) && done == gridDim.x - 1u) finalize(misc, nblocks, misc[M_NFRAGS], frag_cap, frags, p.start_off, tail_panic, gen, res);
   }
 }
 
@@ -1296,7 +1305,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   // per CU (the VGPR / LDS limit), one item per wave at config B
   uint64_t rec_wgs = (nblocks + kRecWaves - 1) / kRecWaves;
   if (rec_wgs > (uint64_t)num_cus * 4) rec_wgs = (uint64_t)num_cus * 4;
-  k_records<<<(uint32_t)rec_wgs, 64 * kRecWaves, 0, stream>>>(
+  k_records<0><<<(uint32_t)rec_wgs, 64 * kRecWaves, 0, stream>>>(
       d_seg, p.seg_len, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg, s.wgx, nw, t, s.misc, tail_panic,
       gen, d_result);
   pr.end(K_RECORDS, stream, ev);

@@ -309,6 +309,32 @@ int main(int argc, char** argv) {
     printf("  stamps: first WG start -> scan start %.1f us, scan %.1f us (wall clock %d kHz)\n",
            (m[11] - m[10]) * 1e3 / hz, (m[12] - m[11]) * 1e3 / hz, hz);
   }
+  {  // k_records ablations (after a full pipeline run: its inputs are in place)
+    CK(bcw_decode_segment_async(ctx, d, &p, &t, dres));
+    CK(hipStreamSynchronize(st));
+    const uint64_t nw = (uint64_t)cus * kCrcWaves;
+    auto rrun = [&](auto kern, uint64_t wgs) {
+      return timeit([&] {
+        hipMemsetAsync(&s.misc[M_DONE_REC], 0, 8, st);  // so the last workgroup finalizes every launch
+        kern<<<(uint32_t)wgs, 64 * kRecWaves, 0, st>>>(d, n, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg,
+                                                       s.wgx, nw, t, s.misc, 0u, 0ull, dres);
+      }, reps, st);
+    };
+    const uint64_t g4 = (uint64_t)cus * 4, g2 = (uint64_t)cus * 2, g8 = (uint64_t)cus * 8;
+    printf("k_records: full %.4f  grid 2/CU %.4f  grid 8/CU %.4f | no parse %.4f  no staging %.4f  no stores %.4f  "
+           "no finalize %.4f  skeleton(1|2|4|8) %.4f ms\n",
+           rrun(k_records<0>, g4), rrun(k_records<0>, g2), rrun(k_records<0>, g8), rrun(k_records<1>, g4),
+           rrun(k_records<2>, g4), rrun(k_records<4>, g4), rrun(k_records<8>, g4), rrun(k_records<15>, g4));
+    const float ck = timeit([&] {
+      k_chase<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, s.lb,
+                                                               s.misc, s.tickets, s.epoch);
+      s.tickets += (nblocks + 63) / 64;
+      ++s.epoch;
+    }, reps, st);
+    printf("k_chase alone %.4f ms\n", ck);
+    const float ms0 = timeit([&] { hipMemsetAsync(&s.misc[M_DONE_REC], 0, 8, st); }, reps, st);
+    printf("(k_records rows include an 8-byte memset: %.4f ms alone)\n", ms0);
+  }
   // verify still OK after variants (re-run the real pipeline)
   CK(bcw_decode_segment_async(ctx, d, &p, &t, dres));
   CK(hipMemcpy(&res, dres, sizeof res, hipMemcpyDeviceToHost));
