@@ -10,6 +10,7 @@ from .wal import (Context, Decoded, ErrCorruptedHintRecord, ErrInvalidData, ErrS
                   ErrWalMismatchCRC, ErrWalMismatchMagic, ErrWalUnknownRecordType, HintRecord, Meta, Record,
                   RefPanic, Wal, WalError, WalFile, compact_one_wal, compute_crc32, default_context, iterate_hint,
                   iterate_record, load_wal, new_hint_by_wal)
+from .staging import Stage
 from .index import (ErrKeyNotFound, ErrKeySoftDeleted, Index, compact_one_wal_filtered, merged_key, murmur3_sum64,
                     recover_from_wals)
 
@@ -18,4 +19,4 @@ __all__ = ["Context", "Decoded", "ErrCorruptedHintRecord", "ErrInvalidData", "Er
            "HintRecord", "Meta", "Record", "RefPanic", "Wal", "WalError", "compute_crc32", "default_context",
            "iterate_hint", "iterate_record", "load_wal", "_lib", "WalFile", "compact_one_wal",
            "new_hint_by_wal", "ErrKeyNotFound", "ErrKeySoftDeleted", "Index", "compact_one_wal_filtered",
-           "merged_key", "murmur3_sum64", "recover_from_wals"]
+           "merged_key", "murmur3_sum64", "recover_from_wals", "Stage"]

@@ -87,6 +87,7 @@ ST_OK, ST_INVALID, ST_PANIC, ST_UNSUPPORTED = 0, 1, 2, 3
 ERR_NONE, ERR_CRC, ERR_TYPE, ERR_PANIC = 0, 1, 2, 3
 SB_OK, SB_SHORT, SB_CRC, SB_MAGIC, SB_BLOCKSIZE = 0, 1, 2, 3, 4
 E_CAPACITY = -4
+E_IO = -6
 ENC_COMPACT, ENC_HINT = 0, 1
 ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC, ENC_ERR_TABLE, ENC_ERR_STALE = 0, 1, 2, 3, 4, 5
 IDX_PUT, IDX_DELETE, IDX_SOFT_DELETE = 0, 1, 2
@@ -145,6 +146,10 @@ def _load():
         "bcw_index_recover_segment": (C.c_int, [vp, vp, vp, C.POINTER(DecodeParams), C.c_uint64, C.c_int,
                                                 C.POINTER(DecodeResult), C.POINTER(IndexResult)]),
         "bcw_murmur3_sum64": (C.c_uint64, [vp, C.c_uint64]),
+        "bcw_stage_create": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.POINTER(vp)]),
+        "bcw_stage_destroy": (C.c_int, [vp]),
+        "bcw_stage_read": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint64, vp, vp, C.c_uint32]),
+        "bcw_stage_write": (C.c_int, [vp, C.c_int, C.c_uint64, vp, C.c_uint64, vp]),
         "bcw_synth_segment": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_int, C.c_uint64, vp, C.c_uint64, u64p, u64p]),
     }

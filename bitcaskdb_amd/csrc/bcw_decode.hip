@@ -497,11 +497,11 @@ __device__ void scan_wg_aggregates(Xf* __restrict__ wgx, uint64_t n, uint64_t* _
 // the init 0xFFFFFFFF contributes A_{8L}(~0) at ge, the XOR-out is folded into ~unmask). So the
 // CRC check becomes a zero test of a linear functional, and windows can be computed by separate
 // lanes and combined with fixed shift operators:
-//   * head pass: lane i processes the first window of fragment i (prefix masking); if C == 1 it
-//     also holds the J word and tests zero directly, otherwise its end state seeds the second
-//     window's chain.
-//   * body passes: the remaining windows of consecutive fragments, one per lane, consecutive
-//     windows of a fragment on consecutive lanes. Lane l maps its end state into a common frame
+//   * a wave appends its fragments (64 at a time, the next group's descriptors prefetched) to a ring
+//     with their window counts; every pass then takes the next 64 windows of consecutive fragments,
+//     one per lane, consecutive windows of a fragment on consecutive lanes (a fragment's first window
+//     has the bytes before its data masked off, its last window holds the J word). Lane l maps its end
+//     state into a common frame
 //     with F_l = A_{8*128*(63-l)} (lane-replicated nibble tables), a segmented XOR scan combines
 //     the fragment's windows, and the lane holding the last window tests the total for zero.
 //     A fragment continuing past lane 63 carries its state to the next pass, where it seeds lane 0's chain.
@@ -678,14 +678,15 @@ __device__ __forceinline__ FragGeo frag_geo(uint32_t start_off, uint32_t blk, ui
 // one body-pass lane: which window, where, how to seed and finish it
 struct BodyDesc {
   uint32_t woff;    // window offset relative to the wave's base (start of its first block - 128)
-  uint32_t J;
-  uint32_t seed;    // first body window: head-window end state; else 0
+  uint32_t J;       // last window: the J word (the init contribution and the stored CRC)
   uint32_t fi;      // fragment index relative to the wave's first fragment
   uint32_t meta;    // hi (last window: data end within the window) | cfb << 8 | last << 17 | active << 18
+                    // | lo << 19 (first window: bytes before the data)
   __device__ __forceinline__ uint32_t hi() const { return meta & 0xffu; }
-  __device__ __forceinline__ uint32_t cfb() const { return (meta >> 8) & 0x1ffu; }  // body window index
+  __device__ __forceinline__ uint32_t cfb() const { return (meta >> 8) & 0x1ffu; }  // window index in the fragment
   __device__ __forceinline__ bool last() const { return (meta >> 17) & 1u; }
   __device__ __forceinline__ bool active() const { return (meta >> 18) & 1u; }
+  __device__ __forceinline__ uint32_t lo() const { return (meta >> 19) & 0x7fu; }
 };
 
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
@@ -728,10 +729,10 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint32_t lo = lane & 31u;
   const uint32_t lb = lo * 4u;  // lane slot in a slice-table row
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of multi-window fragments: first body chunk
-  uint32_t* r_cend = r_cpre + kRing;                 //   chunk end
-  uint4* r_ent = reinterpret_cast<uint4*>(r_cend + kRing);  // {window end (GE) - wbase, C | last hi << 16, J, V1},
-                                                             // {fragment index, cpre, -, -}
+  uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of fragments: first window (wave-relative)
+  uint32_t* r_cend = r_cpre + kRing;                 //   end of its windows
+  uint4* r_ent = reinterpret_cast<uint4*>(r_cend + kRing);  // {window end (GE) - wbase, C | last hi << 16,
+                                                             //  stored crc, len}, {fragment index, cpre, lo, -}
   const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
   const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
   const uint64_t b0 = nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
@@ -743,66 +744,49 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint32_t nwin = (nfr + 63u) / 64u;
 
   uint32_t r_head = 0, r_tail = 0;  // absolute ring positions (wave-uniform)
-  uint32_t cbase = 0;               // body chunks appended so far
-  uint32_t kwin = 0;                // next fragment window to load
+  uint32_t cbase = 0;               // windows appended so far
+  uint32_t kwin = 0;                // next group of 64 fragments to append
+  Frag pf{};                        // the next group's fragment descriptor (loaded one group ahead)
+  if (lane < nfr) pf = frags[f0 + lane];
 
-  // Fragment window kwin (64 fragments): head pass for every fragment (first window; C == 1
-  // fragments are finished here), then the fragments with body windows are appended to the ring.
-  // w: a dead 32-word buffer (the pipeline buffer about to be refilled).
-  auto load_win = [&](uint32_t (&w)[32]) {
+  // Group kwin (64 fragments, one per lane): every fragment is appended to the ring with its C windows
+  // (GE tiling, see above); the group after it is prefetched. No window is loaded here: the first window
+  // of a fragment is an ordinary pass window with the bytes before the data masked off.
+  auto load_win = [&]() {
     const uint32_t fi = kwin * 64u + lane;
     ++kwin;
-    uint32_t cb = 0, s = 0, e = 0, J = 0, blk = 0;
-    FragGeo geo{0, 0, 1};
     const bool valid = fi < nfr;
+    const Frag f = pf;
+    if (fi + 64u < nfr) pf = frags[f0 + fi + 64u];
+    FragGeo geo{0, 0, 0};
+    uint32_t e = 0;
     if (valid) {
-      const Frag f = frags[f0 + fi];
-      s = f.start;
       e = (uint32_t)f.start + f.len;
-      blk = f.blk;
-      geo = frag_geo(start_off, blk, s, e);
-      cb = geo.C - 1u;
-      const uint32_t crc = rotl32(f.crc - 0xa282ead8u, 15);
-      J = ~crc ^ tabs.initc[f.len];
+      geo = frag_geo(start_off, f.blk, f.start, e);
     }
-    uint32_t V = 0;
-    const int64_t wst = geo.GE - 128 * (int64_t)geo.C;
-    const bool inb = __all(!valid || (wst >= 0 && (uint64_t)wst + 128 <= seg_len));
-    if (valid) {
-      load_window(seg, seg_len, wst, inb, w);
-      const int32_t lo8 = 8 * (int32_t)(geo.gs - wst);  // 8 * lo, lo in [0,128)
-#pragma unroll
-      for (int k2 = 0; k2 < 32; ++k2) {
-        int32_t sh = lo8 - 32 * k2;
-        sh = sh < 0 ? 0 : (sh > 32 ? 32 : sh);
-        w[k2] &= (uint32_t)(0xffffffffffffffffull << sh);
-      }
-      if (geo.C == 1u) fix_last(w, (uint32_t)(geo.gs + (int64_t)(e - s) - wst), J);
-      V = crc_window(s_slice, s_half, lb, 0u, w);
-      if (geo.C == 1u) frags[f0 + fi].ok = (V == 0u) ? 1 : 0;
-    }
-    // append fragments with body windows to the ring
-    const bool multi = valid && cb > 0u;
-    const uint64_t mm = __ballot(multi);
-    const uint32_t below = lane == 0 ? 0u : (uint32_t)__builtin_popcountll(mm & (~0ull >> (64 - lane)));
+    const uint32_t cb = geo.C;
+    const uint64_t vm = __ballot(valid);
+    const uint32_t below = lane == 0 ? 0u : (uint32_t)__builtin_popcountll(vm & (~0ull >> (64 - lane)));
     const uint32_t incl = wave_add_scan(cb, lane);
     const uint32_t tot = __shfl(incl, 63, 64);
-    if (multi) {
+    if (valid) {
       const uint32_t a = (r_tail + below) & (kRing - 1);
-      const int64_t ge = geo.gs + (int64_t)(e - s);
+      const int64_t ge = geo.gs + (int64_t)(e - f.start);
+      const uint32_t lo = (uint32_t)(geo.gs - (geo.GE - 128 * (int64_t)geo.C));  // bytes before the data
       r_cpre[a] = cbase + incl - cb;
       r_cend[a] = cbase + incl;
-      r_ent[2 * a] = make_uint4((uint32_t)(geo.GE - wbase), geo.C | ((uint32_t)(ge - (geo.GE - 128)) << 16), J, V);
-      r_ent[2 * a + 1] = make_uint4(fi, cbase + incl - cb, 0u, 0u);
+      r_ent[2 * a] = make_uint4((uint32_t)(geo.GE - wbase), geo.C | ((uint32_t)(ge - (geo.GE - 128)) << 16), f.crc,
+                                f.len);
+      r_ent[2 * a + 1] = make_uint4(fi, cbase + incl - cb, lo, 0u);
     }
-    r_tail += (uint32_t)__builtin_popcountll(mm);
+    r_tail += (uint32_t)__builtin_popcountll(vm);
     cbase += __builtin_amdgcn_readfirstlane(tot);
     wave_sync();
   };
 
   // make the ring hold every fragment owning a chunk of [pass, pass+64): drop entries ending at or
   // before `pass` (chunk ends increase along the ring, so the dead entries are a ballot prefix)
-  auto advance = [&](uint32_t pass, uint32_t (&scratch)[32]) {
+  auto advance = [&](uint32_t pass) {
     auto evict = [&]() {
       for (;;) {
         const uint32_t a = r_head + lane;
@@ -814,7 +798,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     };
     evict();
     while (kwin < nwin && cbase < pass + 64u) {
-      load_win(scratch);
+      load_win();
       evict();
     }
   };
@@ -843,11 +827,13 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     const uint4 e0 = r_ent[2 * slot], e1 = r_ent[2 * slot + 1];
     const uint32_t chl = e0.y;
     const uint32_t cfb = j - e1.y;
-    const uint32_t c = (chl & 0xffffu) - 2u - cfb;  // windows from the end (0 = last)
+    const uint32_t c = (chl & 0xffffu) - 1u - cfb;  // windows from the end (0 = last)
     d.woff = e0.x - 128u * (c + 1u);
-    d.meta = (c == 0u ? (chl >> 16) : 0u) | (cfb << 8) | ((c == 0u ? 1u : 0u) << 17) | (1u << 18);
-    d.J = e0.z;
-    d.seed = cfb == 0u ? e0.w : 0u;
+    d.meta = (c == 0u ? (chl >> 16) : 0u) | (cfb << 8) | ((c == 0u ? 1u : 0u) << 17) | (1u << 18) |
+             ((cfb == 0u ? e1.z : 0u) << 19);
+    // J = ~unmask(stored) ^ A_{8L}(~0) (see above); the init-contribution load is two passes ahead of its use
+    d.J = 0;
+    if (c == 0u) d.J = ~rotl32(e0.z - 0xa282ead8u, 15) ^ tabs.initc[e0.w];
     d.fi = e1.x;
     return d;
   };
@@ -870,9 +856,18 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     uint32_t v = 0;
     if ((ABL & 32) && !(ABL & 64)) quad_windows_transpose(w, lane);
     if (d.active()) {
+      if (d.cfb() == 0u) {  // first window: zero the bytes before the data (the previous header / fragment)
+        const int32_t lo8 = 8 * (int32_t)d.lo();
+#pragma unroll
+        for (int k2 = 0; k2 < 32; ++k2) {
+          int32_t sh = lo8 - 32 * k2;
+          sh = sh < 0 ? 0 : (sh > 32 ? 32 : sh);
+          w[k2] &= (uint32_t)(0xffffffffffffffffull << sh);
+        }
+      }
       if (d.last()) fix_last(w, d.hi(), d.J);
       // a fragment continuing from the previous pass: its state so far seeds lane 0's chain
-      const uint32_t seed = (lane == 0u && d.cfb() > 0u) ? carry : d.seed;
+      const uint32_t seed = (lane == 0u && d.cfb() > 0u) ? carry : 0u;
       if (!(ABL & 1)) {
         v = crc_window(s_slice, s_half, lb, seed, w);
       } else {
@@ -902,7 +897,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   };
   // One copy of the loop body (instruction-cache footprint). At the top of an iteration wx holds pass
   // p (chained now), wy the loads of pass p+64 in flight, dz the descriptors of pass p+128. After
-  // the chain: advance the ring (wx is the head-pass scratch), take wy into wx, issue pass p+128's
+  // the chain: advance the ring, take wy into wx, issue pass p+128's
   // loads, then describe pass p+192 -- descriptor work is off the load-to-load critical path.
   // The first three iterations only fill the pipeline (p < 0).
   uint32_t wx[32], wy[32];
@@ -916,7 +911,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     }
     p += 64;
     if (p >= 0 && (uint64_t)p >= cbase) break;
-    advance((uint32_t)(p + 128), wx);
+    advance((uint32_t)(p + 128));
 #pragma unroll
     for (int k2 = 0; k2 < 32; ++k2) wx[k2] = wy[k2];
     dx = dy;
@@ -1301,10 +1296,10 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   const uint64_t tail = (p.seg_len - p.start_off) % kBlock;
   const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;
   pr.begin(K_RECORDS, stream, ev);
-  // every resident wave takes work items (runs of blocks holding ~64 fragments): 4 workgroups of 4 waves
-  // per CU (the VGPR / LDS limit), one item per wave at config B
+  // 2 workgroups of 4 waves per CU take the work items (runs of blocks holding ~64 fragments); measured
+  // with tools/kbench: 4 per CU (every resident wave one item) 14 % slower, 8 per CU 50 % slower
   uint64_t rec_wgs = (nblocks + kRecWaves - 1) / kRecWaves;
-  if (rec_wgs > (uint64_t)num_cus * 4) rec_wgs = (uint64_t)num_cus * 4;
+  if (rec_wgs > (uint64_t)num_cus * 2) rec_wgs = (uint64_t)num_cus * 2;
   k_records<0><<<(uint32_t)rec_wgs, 64 * kRecWaves, 0, stream>>>(
       d_seg, p.seg_len, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg, s.wgx, nw, t, s.misc, tail_panic,
       gen, d_result);

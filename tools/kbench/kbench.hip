@@ -337,6 +337,7 @@ int main(int argc, char** argv) {
   }
   // verify still OK after variants (re-run the real pipeline)
   CK(bcw_decode_segment_async(ctx, d, &p, &t, dres));
+  CK(hipStreamSynchronize(st));
   CK(hipMemcpy(&res, dres, sizeof res, hipMemcpyDeviceToHost));
   printf("recheck: n_records=%lu err=%d bad=%d\n", res.n_records, res.err_class, res.first_bad_record);
   return 0;
