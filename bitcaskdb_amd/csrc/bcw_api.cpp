@@ -271,6 +271,17 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
   build_initc(initc.data());
   std::vector<uint32_t> enc_ops(kEncOpsWords);
   build_enc_ops(enc_ops.data());
+  std::vector<uint32_t> pow2(15 * 128);
+  {
+    uint32_t t0[256], img[32], sq[32];
+    byte_table(t0);
+    shift_basis(t0, 1, img);  // A_8, then repeated squaring: A_{8*2^(k+1)} = A_{8*2^k} o A_{8*2^k}
+    for (int k = 0; k < 15; ++k) {
+      nibble_image(img, pow2.data() + k * 128);
+      for (int i = 0; i < 32; ++i) sq[i] = apply_basis(img, img[i]);
+      memcpy(img, sq, sizeof img);
+    }
+  }
   std::vector<uint32_t> image(kLdsImage);
   for (int e = 0; e < 256; ++e)
     for (int r = 0; r < 32; ++r) {
@@ -289,6 +300,7 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
             hipMalloc(&c->tabs.initc, initc.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.lds_image, image.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.enc_ops, enc_ops.size() * 4) == hipSuccess &&
+            hipMalloc(&c->tabs.pow2, pow2.size() * 4) == hipSuccess &&
             hipMalloc(&c->d_eres, sizeof(bcw_encode_result)) == hipSuccess &&
             hipMalloc(&c->d_result, sizeof(bcw_decode_result)) == hipSuccess &&
             hipMalloc(&c->d_ires, sizeof(bcw_index_result)) == hipSuccess;
@@ -298,7 +310,8 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
        hipMemcpy(c->tabs.half, half.data(), half.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.initc, initc.data(), initc.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.lds_image, image.data(), image.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemcpy(c->tabs.enc_ops, enc_ops.data(), enc_ops.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+       hipMemcpy(c->tabs.enc_ops, enc_ops.data(), enc_ops.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(c->tabs.pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
   if (!ok) { bcw_ctx_destroy(c); return BCW_E_NOMEM; }
   *out = c;
   return BCW_OK;
@@ -340,6 +353,7 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   if (c->es.ev_desc) (void)hipEventDestroy(c->es.ev_desc);
   if (c->es.aux) (void)hipStreamDestroy(c->es.aux);
   (void)hipFree(c->tabs.enc_ops);
+  (void)hipFree(c->tabs.pow2);
   (void)hipFree(c->d_keep);
   (void)hipFree(c->d_eout);
   (void)hipFree(c->d_eres);
@@ -456,7 +470,8 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
   DeviceGuard dg(c->device);
   if (!dg.ok) return BCW_E_HIP;
   const uint64_t n = std::min(c->s.frag_cap, d_frags->capacity);
-  return launch_export_frags(c->s, *d_frags, c->last_start_off, c->cur, n) == hipSuccess ? BCW_OK : BCW_E_HIP;
+  return launch_export_frags(c->s, *d_frags, c->last_start_off, c->cur, n, c->tabs.initc) == hipSuccess ? BCW_OK
+                                                                                                  : BCW_E_HIP;
 }
 
 static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_records", "k_enc_prep", "k_enc_scan", "k_events",
@@ -523,7 +538,7 @@ int bcw_decode_fragments(bcw_ctx* c, const bcw_frag_table* h, uint64_t* n_total)
   d.stored_crc = (uint32_t*)m; m += n * 4;
   d.type = m; m += n;
   d.crc_ok = m;
-  bool ok = launch_export_frags(c->s, d, c->last_start_off, c->cur, n) == hipSuccess;
+  bool ok = launch_export_frags(c->s, d, c->last_start_off, c->cur, n, c->tabs.initc) == hipSuccess;
   auto cp = [&](void* dst, const void* src, size_t esz) {
     return !dst || hipMemcpyAsync(dst, src, n * esz, hipMemcpyDeviceToHost, c->cur) == hipSuccess;
   };

@@ -14,6 +14,7 @@
 #include <cstdint>
 
 #include "bcw_internal.h"
+#include "bcw_parse.h"
 
 namespace bcw {
 
@@ -180,14 +181,16 @@ __device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg,
   return n;
 }
 
+// the fragment table entry; the stored CRC is kept as the check word J (see Frag)
 __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, uint64_t frag_cap, uint32_t b,
-                                         uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
+                                         uint32_t start, uint32_t len, uint32_t crc, uint32_t type,
+                                         const uint32_t* __restrict__ initc) {
   if (g >= frag_cap) return;
   Frag f;
   f.blk = b;
   f.start = (uint16_t)start;
   f.len = (uint16_t)len;
-  f.crc = crc;
+  f.chk = ~rotl32(crc - 0xa282ead8u, 15) ^ initc[len];
   f.type = (uint8_t)type;
   f.ok = 0;
   f.pad = 0;
@@ -197,7 +200,7 @@ __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, u
 __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
                                               uint64_t nblocks, uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
                                               uint64_t frag_cap, uint64_t* __restrict__ lb, uint64_t* __restrict__ misc,
-                                              uint64_t ticket_base, uint64_t epoch) {
+                                              uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc) {
   __shared__ uint32_t s_hold[kChaseHold][3][64];  // {crc, start | len << 16, type} of each lane's headers
   const uint32_t lane = threadIdx.x;
   uint64_t wg = 0;
@@ -252,11 +255,12 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     const uint32_t nh = n < (uint32_t)kChaseHold ? n : (uint32_t)kChaseHold;
     for (uint32_t k = 0; k < nh; ++k) {
       const uint32_t sl = s_hold[k][1][lane];
-      put_frag(frags, g0 + k, frag_cap, (uint32_t)b, sl & 0xffffu, sl >> 16, s_hold[k][0][lane], s_hold[k][2][lane]);
+      put_frag(frags, g0 + k, frag_cap, (uint32_t)b, sl & 0xffffu, sl >> 16, s_hold[k][0][lane], s_hold[k][2][lane],
+               initc);
     }
     if (n > (uint32_t)kChaseHold)  // the tail of a block with more headers than held
       chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
-        if (k >= (uint32_t)kChaseHold) put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type);
+        if (k >= (uint32_t)kChaseHold) put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, initc);
       });
   }
   const uint64_t nwg = (nblocks + 63) / 64;
@@ -732,7 +736,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of fragments: first window (wave-relative)
   uint32_t* r_cend = r_cpre + kRing;                 //   end of its windows
   uint4* r_ent = reinterpret_cast<uint4*>(r_cend + kRing);  // {window end (GE) - wbase, C | last hi << 16,
-                                                             //  stored crc, len}, {fragment index, cpre, lo, -}
+                                                             //  J, len}, {fragment index, cpre, lo, -}
   const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
   const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
   const uint64_t b0 = nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
@@ -775,7 +779,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       const uint32_t lo = (uint32_t)(geo.gs - (geo.GE - 128 * (int64_t)geo.C));  // bytes before the data
       r_cpre[a] = cbase + incl - cb;
       r_cend[a] = cbase + incl;
-      r_ent[2 * a] = make_uint4((uint32_t)(geo.GE - wbase), geo.C | ((uint32_t)(ge - (geo.GE - 128)) << 16), f.crc,
+      r_ent[2 * a] = make_uint4((uint32_t)(geo.GE - wbase), geo.C | ((uint32_t)(ge - (geo.GE - 128)) << 16), f.chk,
                                 f.len);
       r_ent[2 * a + 1] = make_uint4(fi, cbase + incl - cb, lo, 0u);
     }
@@ -831,9 +835,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     d.woff = e0.x - 128u * (c + 1u);
     d.meta = (c == 0u ? (chl >> 16) : 0u) | (cfb << 8) | ((c == 0u ? 1u : 0u) << 17) | (1u << 18) |
              ((cfb == 0u ? e1.z : 0u) << 19);
-    // J = ~unmask(stored) ^ A_{8L}(~0) (see above); the init-contribution load is two passes ahead of its use
-    d.J = 0;
-    if (c == 0u) d.J = ~rotl32(e0.z - 0xa282ead8u, 15) ^ tabs.initc[e0.w];
+    d.J = c == 0u ? e0.z : 0u;  // J = ~unmask(stored) ^ A_{8L}(~0) (see above), from the fragment table
     d.fi = e1.x;
     return d;
   };
@@ -968,26 +970,6 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
 // k_records: record emission (one wave per run of blocks, fragments in chunks of 64 lanes) and
 // RecordFromBytes (record.go:140-239) / HintRecord.Decode (hint.go:50-84) per record, one lane each.
 
-// Go encoding/binary.Uvarint over a byte accessor; DecodeUvarint maps errors to (0,0).
-template <typename RD>
-__device__ __forceinline__ uint64_t uvarint(RD& rd, uint64_t pos, uint64_t len, uint32_t& used) {
-  uint64_t x = 0;
-  uint32_t s = 0;
-  for (uint32_t i = 0; pos + i < len; ++i) {
-    if (i == 10) { used = 0; return 0; }
-    const uint32_t b = rd(pos + i);
-    if (b < 0x80u) {
-      if (i == 9 && b > 1u) { used = 0; return 0; }
-      used = i + 1;
-      return x | ((uint64_t)b << s);
-    }
-    x |= (uint64_t)(b & 0x7fu) << s;
-    s += 7;
-  }
-  used = 0;
-  return 0;
-}
-
 constexpr int kRecWaves = 4;
 constexpr uint32_t kStage = 128;      // staged record-prefix bytes per lane
 constexpr uint32_t kStageArea = 144;  // 9 x 16 B aligned loads
@@ -1021,61 +1003,6 @@ struct RecReader {
     return seg[caddr + (pos - cbeg)];
   }
 };
-
-__device__ __forceinline__ void parse_record(const bcw_decode_params& p, RecReader& rd, uint64_t len, uint8_t& status,
-                                             uint8_t& hdr, uint8_t& flags, uint8_t& etag_off, uint64_t& key_len,
-                                             uint64_t& val_len, uint64_t& meta_len, uint64_t& expire, uint64_t& aux0,
-                                             uint64_t& aux1) {
-  uint32_t used;
-  status = BCW_ST_OK;
-  hdr = flags = etag_off = 0;
-  key_len = val_len = meta_len = expire = aux0 = aux1 = 0;
-  if (p.mode == BCW_MODE_RECORD) {
-    // RecordFromBytes, record.go:140-239
-    const uint64_t min_hdr = 1ull + p.ns_size + 1ull + 3ull;
-    if (len < min_hdr) { status = BCW_ST_INVALID; return; }
-    const uint64_t header = rd(0);
-    uint64_t o = 1 + p.ns_size;
-    const uint32_t flag = rd(o);
-    ++o;
-    key_len = uvarint(rd, o, len, used); o += used;
-    val_len = uvarint(rd, o, len, used); o += used;
-    meta_len = uvarint(rd, o, len, used); o += used;
-    const uint64_t etag_len = (flag & 1u) ? 0 : p.etag_size;
-    uint64_t expire_size = 0;
-    hdr = (uint8_t)header; flags = (uint8_t)flag; etag_off = (uint8_t)o;
-    if ((flag & 2u) == 0) {
-      if (o + etag_len > len) { status = BCW_ST_PANIC; return; }  // data[offset+etagLen:] (record.go:186)
-      expire = uvarint(rd, o + etag_len, len, used);
-      expire_size = used;
-      expire += p.base_time;
-    }
-    const int64_t cur_hdr = (int64_t)o + (int64_t)etag_len + (int64_t)expire_size;
-    const int64_t cur_total = cur_hdr + (int64_t)(key_len + val_len + meta_len);
-    if ((uint64_t)cur_hdr != header || cur_total != (int64_t)len) { status = BCW_ST_INVALID; return; }
-    const uint64_t s1 = key_len + val_len;
-    const uint64_t s2 = s1 + meta_len;
-    const bool wrapped = (s1 < key_len) || (s2 < s1);
-    if ((int64_t)key_len < 0 || (int64_t)val_len < 0 || (int64_t)meta_len < 0 || wrapped) status = BCW_ST_PANIC;
-    else if (key_len > 0xffffffffull || val_len > 0xffffffffull || meta_len > 0xffffffffull || len > 0xffffffffull)
-      status = BCW_ST_UNSUPPORTED;
-  } else {
-    // HintRecord.Decode, hint.go:50-84
-    if (len < (uint64_t)p.ns_size + 5ull) { status = BCW_ST_INVALID; return; }
-    int64_t o = p.ns_size;
-    key_len = uvarint(rd, (uint64_t)o, len, used);
-    o += used;
-    const int64_t key_off = o;
-    o = (int64_t)((uint64_t)o + key_len);
-    hdr = (uint8_t)key_off;
-    if (o < 0 || o > (int64_t)len) { status = BCW_ST_PANIC; return; }
-    expire = uvarint(rd, (uint64_t)o, len, used); o += used;  // fid
-    aux0 = uvarint(rd, (uint64_t)o, len, used); o += used;    // off
-    aux1 = uvarint(rd, (uint64_t)o, len, used); o += used;    // size
-    if (o != (int64_t)len) status = BCW_ST_INVALID;
-    else if ((int64_t)key_len < 0) status = BCW_ST_PANIC;
-  }
-}
 
 __device__ __forceinline__ void finalize(uint64_t* __restrict__ misc, uint64_t nblocks, uint64_t frag_total,
                            uint64_t frag_cap, const Frag* __restrict__ frags, uint32_t start_off, uint32_t tail_panic,
@@ -1257,14 +1184,15 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
 }
 
 __global__ void k_export_frags(const Frag* __restrict__ frags, const uint64_t* __restrict__ misc, uint64_t cap,
-                               uint32_t start_off, bcw_frag_table out) {
+                               uint32_t start_off, bcw_frag_table out, const uint32_t* __restrict__ initc) {
   const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t n = misc[M_NFRAGS];
   if (g >= n || g >= cap || g >= out.capacity) return;
   const Frag f = frags[g];
   out.data_off[g] = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
   out.len[g] = f.len;
-  out.stored_crc[g] = f.crc;
+  const uint32_t u = ~(f.chk ^ initc[f.len]);  // unmask(stored), from J
+  out.stored_crc[g] = ((u >> 15) | (u << 17)) + 0xa282ead8u;
   out.type[g] = f.type;
   out.crc_ok[g] = f.ok;
 }
@@ -1281,7 +1209,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   const uint32_t nb_grid = (uint32_t)((nblocks + 63) / 64);
   pr.begin(K_CHASE, stream, ev);
   k_chase<<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags, s.frag_cap, s.lb,
-                                       s.misc, s.tickets, s.epoch);
+                                       s.misc, s.tickets, s.epoch, tabs.initc);
   pr.end(K_CHASE, stream, ev);
   s.tickets += nb_grid;
   if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse
@@ -1308,9 +1236,10 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
 }
 
 hipError_t launch_export_frags(const Scratch& s, const bcw_frag_table& out, uint32_t start_off, hipStream_t stream,
-                               uint64_t n) {
+                               uint64_t n, const uint32_t* initc) {
   if (n == 0) return hipSuccess;
-  k_export_frags<<<(uint32_t)((n + 255) / 256), 256, 0, stream>>>(s.frags, s.misc, s.frag_cap, start_off, out);
+  k_export_frags<<<(uint32_t)((n + 255) / 256), 256, 0, stream>>>(s.frags, s.misc, s.frag_cap, start_off, out,
+                                                                    initc);
   return hipGetLastError();
 }
 

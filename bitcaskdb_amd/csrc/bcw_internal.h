@@ -18,7 +18,8 @@ struct Frag {
   uint32_t blk;    // block index within the segment
   uint16_t start;  // block-relative offset of the data (header + 7)
   uint16_t len;    // data length after the clamp of wal_iterator.go:75
-  uint32_t crc;    // stored masked CRC (header bytes [0,4))
+  uint32_t chk;    // check word J = ~unmask(stored CRC) ^ A_{8 len}(0xFFFFFFFF) (bcw_decode.hip, k_crc): the
+                   // fragment's data passes ComputeCRC32 iff its raw CRC-32C equals this (stored CRC recoverable)
   uint8_t type;    // header byte 6
   uint8_t ok;      // CRC verified
   uint16_t pad;
@@ -47,6 +48,7 @@ struct Tables {
   uint32_t* initc;   // [kBlock+1] A_{8L}(0xFFFFFFFF)
   uint32_t* lds_image;  // k_crc's LDS table image, laid out exactly as in LDS (see kLdsImage)
   uint32_t* enc_ops;    // [kEncOpsWords] encode shift operators (nibble images, see build_enc_ops)
+  uint32_t* pow2;       // [15][8][16] A_{8 * 2^k} (nibble images), k < 15: shifts by any distance < 32 KiB
 };
 constexpr int kEncWrOps = 2 * 16 * 128;              // k_write's operators follow k_pack's
 constexpr int kEncOpsWords = kEncWrOps + 56 * 128;
@@ -114,7 +116,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
                          bcw_decode_result* d_result, const Tables& tabs, Scratch& s, uint64_t nblocks,
                          uint64_t gen, hipStream_t stream, int num_cus, Prof* prof);
 hipError_t launch_export_frags(const Scratch& s, const bcw_frag_table& out, uint32_t start_off, hipStream_t stream,
-                               uint64_t n);
+                               uint64_t n, const uint32_t* initc);
 
 // Encode scratch (grow-only, per context). rows: source table rows.
 struct EncScratch {

@@ -388,6 +388,38 @@ int bcw_index_recover_segment(bcw_ctx* ctx, bcw_index* ix, const uint8_t* h_seg,
 /* IndexOperator.Hash (index.go:15-19): murmur3 (spaolacci/murmur3 v1.1.0) New64().Sum64() on the host */
 uint64_t bcw_murmur3_sum64(const uint8_t* p, uint64_t n);
 
+/* ---- batched point reads (Get / GetV2's record fetch, db_impl.go:567-631) -----------------------------
+ * For each request (offset, size) -- an index value -- Wal.ReadRecord (wal.go:556-573: WalRecordSize,
+ * one read of the record's physical span) + WalParseRecord (wal.go:121-173) + RecordFromBytes
+ * (record.go:140-239) against a WAL image resident in HBM. rd_status per request: */
+#define BCW_RD_OK 0
+#define BCW_RD_BEYOND 1     /* errors.New("read beyond file size") (wal.go:562-564) */
+#define BCW_RD_CORRUPTED 2  /* ErrWalCorruptedData: a fragment length beyond the buffer */
+#define BCW_RD_CRC 3        /* ErrWalMismatchCRC (verifyChecksum) */
+#define BCW_RD_SIZE 4       /* ErrWalMismatchSize */
+#define BCW_RD_TYPE 5       /* ErrWalUnknownRecordType */
+#define BCW_RD_INCOMPLETE 6 /* ErrWalIncompleteRecord */
+#define BCW_RD_PANIC 7      /* the reference panics (size 0: the header slice of an empty buffer) */
+
+typedef struct bcw_read_params {
+  uint64_t seg_len;   /* the WAL image's size (Wal.size) */
+  uint64_t base_time; /* wal.BaseTime() for RecordFromBytes */
+  uint32_t ns_size;
+  uint32_t etag_size;
+  uint32_t verify;    /* ReadOptions.VerifyChecksum */
+  uint32_t _pad;
+} bcw_read_params;
+
+/* Async, device-resident: request i reads d_size[i] payload bytes into d_payload + d_pay_off[i]; d_table
+ * (may be NULL) receives RecordFromBytes' fields and status (foff = offset + 7) when rd_status == OK. */
+int bcw_read_records_async(bcw_ctx* ctx, const uint8_t* d_seg, const bcw_read_params* p, uint64_t n,
+                           const uint64_t* d_off, const uint64_t* d_size, const uint64_t* d_pay_off,
+                           uint8_t* d_payload, uint8_t* d_rd_status, const bcw_record_table* d_table);
+/* Synchronous, host in / host out: payloads concatenated in request order into h_payload (sum of sizes). */
+int bcw_read_records(bcw_ctx* ctx, const uint8_t* h_seg, const bcw_read_params* p, uint64_t n,
+                     const uint64_t* h_off, const uint64_t* h_size, uint8_t* h_payload, uint8_t* h_rd_status,
+                     const bcw_record_table* h_table);
+
 /* ---- host I/O staging: WAL files <-> HBM through pinned slices ---------------------------------------
  * The reference reads a segment with PreadFull per 32 KiB block (utils.go:32-48, wal_iterator.go:55)
  * and writes the rewritten WAL through a buffer flushed every >= 1 MiB (WalRewriter

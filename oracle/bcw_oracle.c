@@ -1008,3 +1008,35 @@ uint64_t oc_compact_filter(oc_index* x, const uint8_t* seg, uint64_t len, uint32
   oc_decode_free(d);
   return r;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* point reads: Wal.ReadRecord (wal.go:556-573) = WalRecordSize + one PreadFull of the record's */
+/* physical span + WalParseRecord (wal.go:121-173) over that single buffer                     */
+/* ------------------------------------------------------------------------------------------ */
+/* returns OC_RD_*; payload (size bytes) into out when OC_RD_OK */
+int oc_read_record(const uint8_t* seg, uint64_t seg_len, uint64_t offset, uint64_t size, int verify, uint8_t* out) {
+  uint64_t rs = oc_wal_record_size(offset, size);
+  if (offset + rs > seg_len) return OC_RD_BEYOND;   /* "read beyond file size" (wal.go:562-564) */
+  const uint8_t* buf = seg + offset;                /* buffer := make([]byte, recordSize); PreadFull */
+  uint64_t blk_size = rs, blk_off = 0, got = 0;     /* WalParseRecord(size, 0, [][]byte{buffer}, ...) */
+  for (;;) {
+    if (blk_off + OC_HEADER_SIZE > blk_size) return OC_RD_PANIC; /* header := blks[i][blkOff:blkOff+7] */
+    const uint8_t* h = buf + blk_off;
+    blk_off += OC_HEADER_SIZE;
+    uint32_t crc = get_u32(h);
+    uint16_t l16;
+    memcpy(&l16, h + 4, 2);
+    uint64_t length = l16;
+    uint8_t type = h[6];
+    if (length > blk_size - blk_off) return OC_RD_CORRUPTED;  /* ErrWalCorruptedData */
+    const uint8_t* data = buf + blk_off;
+    blk_off += length;
+    if (verify && oc_compute_crc32(data, (size_t)length) != crc) return OC_RD_CRC;
+    /* record = append(record, data...): the capacity is `size`, appending beyond it just grows */
+    if (got + length <= size) memcpy(out + got, data, (size_t)length);
+    got += length;
+    if (type == OC_FULL || type == OC_LAST) return got != size ? OC_RD_SIZE : OC_RD_OK;
+    if (type != OC_FIRST && type != OC_MIDDLE) return OC_RD_TYPE;
+    if (blk_size - blk_off <= OC_HEADER_SIZE) return OC_RD_INCOMPLETE; /* break; i++ ends the block loop */
+  }
+}

@@ -188,6 +188,11 @@ int oc_index_put_segment(oc_index* x, const uint8_t* seg, uint64_t len, uint32_t
 uint64_t oc_compact_filter(oc_index* x, const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
                            uint32_t ns_size, uint32_t etag_size, uint64_t src_fid, uint8_t* keep, uint64_t n_keep);
 
+/* ---- point reads: Wal.ReadRecord + WalParseRecord (wal.go:556-573, 121-173) ---- */
+enum { OC_RD_OK = 0, OC_RD_BEYOND = 1, OC_RD_CORRUPTED = 2, OC_RD_CRC = 3, OC_RD_SIZE = 4, OC_RD_TYPE = 5,
+       OC_RD_INCOMPLETE = 6, OC_RD_PANIC = 7 };
+int oc_read_record(const uint8_t* seg, uint64_t seg_len, uint64_t offset, uint64_t size, int verify, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif
