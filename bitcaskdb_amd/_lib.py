@@ -63,6 +63,11 @@ class EncodeResult(C.Structure):
                 ("hint_events", C.c_uint32), ("fits", C.c_uint32), ("_pad", C.c_uint32)]
 
 
+class ReadParams(C.Structure):
+    _fields_ = [("seg_len", C.c_uint64), ("base_time", C.c_uint64), ("ns_size", C.c_uint32),
+                ("etag_size", C.c_uint32), ("verify", C.c_uint32), ("_pad", C.c_uint32)]
+
+
 class IndexResult(C.Structure):
     _fields_ = [("n_in", C.c_uint64), ("n_done", C.c_uint64), ("err_class", C.c_int32), ("_pad", C.c_int32)]
 
@@ -93,6 +98,7 @@ ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC, ENC_ERR_TABLE, ENC_ERR
 IDX_PUT, IDX_DELETE, IDX_SOFT_DELETE = 0, 1, 2
 IDX_FOUND, IDX_NOT_FOUND, IDX_SOFT_DELETED = 0, 1, 2
 IDX_ERR_FULL = 6
+RD_OK, RD_BEYOND, RD_CORRUPTED, RD_CRC, RD_SIZE, RD_TYPE, RD_INCOMPLETE, RD_PANIC = range(8)
 
 
 def _load():
@@ -146,6 +152,10 @@ def _load():
         "bcw_index_recover_segment": (C.c_int, [vp, vp, vp, C.POINTER(DecodeParams), C.c_uint64, C.c_int,
                                                 C.POINTER(DecodeResult), C.POINTER(IndexResult)]),
         "bcw_murmur3_sum64": (C.c_uint64, [vp, C.c_uint64]),
+        "bcw_read_records_async": (C.c_int, [vp, vp, C.POINTER(ReadParams), C.c_uint64, vp, vp, vp, vp, vp,
+                                             C.POINTER(RecordTable)]),
+        "bcw_read_records": (C.c_int, [vp, vp, C.POINTER(ReadParams), C.c_uint64, u64p, u64p, vp, u8p,
+                                       C.POINTER(RecordTable)]),
         "bcw_stage_create": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.POINTER(vp)]),
         "bcw_stage_destroy": (C.c_int, [vp]),
         "bcw_stage_read": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint64, vp, vp, C.c_uint32]),

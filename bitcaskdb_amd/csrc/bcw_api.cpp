@@ -90,27 +90,30 @@ static void nibble_image(const uint32_t* img, uint32_t* t) {
     for (uint32_t n = 0; n < 16; ++n) t[i * 16 + n] = apply_basis(img, n << (4 * i));
 }
 
-// encode shift operators (nibble images, 128 words each):
-//   k_pack:  [m] = A_{8*128*m}, [16 + m] = A_{8*2048*m} (m < 16)
-//   k_write (from kEncWrOps): [n] = A_{8*16*n}, [16 + n] = A_{8*256*n} (n < 16), [32 + n] = A_{8*4096*n}
-//            (n < 8), [40 + t] = A_{8t}^-1 (t < 16)
+// encode shift operators (nibble images, 128 words each; layout in bcw_internal.h): A_{8*16*n},
+// A_{8*256*n}, A_{8*4096*n} (k_write's lane chains), A_{8t}^-1 (t < 16), and A_{8*2^k} / A_{8*2^k}^-1 for
+// shifts by arbitrary distances (the CRC combine of re-encoded records)
 static void build_enc_ops(uint32_t* ops) {
   uint32_t t0[256];
   byte_table(t0);
-  uint32_t img[32], inv[32];
-  for (int h = 0; h < 2; ++h)
-    for (int m = 0; m < 16; ++m) {
-      shift_basis(t0, (uint64_t)(h ? 2048 : 128) * m, img);
-      nibble_image(img, ops + (h * 16 + m) * 128);
-    }
-  uint32_t* w = ops + kEncWrOps;
-  for (int n = 0; n < 16; ++n) { shift_basis(t0, 16ull * n, img); nibble_image(img, w + n * 128); }
-  for (int n = 0; n < 16; ++n) { shift_basis(t0, 256ull * n, img); nibble_image(img, w + (16 + n) * 128); }
-  for (int n = 0; n < 8; ++n) { shift_basis(t0, 4096ull * n, img); nibble_image(img, w + (32 + n) * 128); }
+  uint32_t img[32], inv[32], sq[32];
+  for (int n = 0; n < 16; ++n) { shift_basis(t0, 16ull * n, img); nibble_image(img, ops + n * 128); }
+  for (int n = 0; n < 16; ++n) { shift_basis(t0, 256ull * n, img); nibble_image(img, ops + (16 + n) * 128); }
+  for (int n = 0; n < 8; ++n) { shift_basis(t0, 4096ull * n, img); nibble_image(img, ops + (32 + n) * 128); }
   for (int t = 0; t < 16; ++t) {
     shift_basis(t0, (uint64_t)t, img);
     invert_basis(img, inv);
-    nibble_image(inv, w + (40 + t) * 128);
+    nibble_image(inv, ops + (kOpInv + t) * 128);
+  }
+  shift_basis(t0, 1, img);  // A_8, then repeated squaring
+  for (int k = 0; k < 32; ++k) {
+    nibble_image(img, ops + (kOpPow2 + k) * 128);
+    if (k < 15) {
+      invert_basis(img, inv);
+      nibble_image(inv, ops + (kOpPow2Inv + k) * 128);
+    }
+    for (int i = 0; i < 32; ++i) sq[i] = apply_basis(img, img[i]);
+    memcpy(img, sq, sizeof img);
   }
 }
 

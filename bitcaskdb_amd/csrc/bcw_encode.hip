@@ -9,6 +9,7 @@
 //   k_enc_prep      per source row: keep / Encode errors / re-encoded payload size     record.go:57-138
 //   k_tile_*        3-phase scan: dense list of written records, y-coordinates a_j
 //   k_events        the writer's layout recurrence as an event scan (one workgroup)    wal.go:505-549
+//   k_ev_fix        event blocks / y-coordinates (a scan over the events), layout end
 //   k_recoff        per record: the file offset WriteRecord returns                     wal.go:514-516
 //   (compaction) k_hint_sizes + scan + k_events + k_recoff for the hint WAL            hint.go:32-48
 //   k_recdesc_w     per record: payload as literal prefix | source range | literal suffix
@@ -26,9 +27,9 @@
 // bytes), else at E_k with a continuation header. Between events every block start is congruent
 // mod M, so with rho = (next block end) mod M, record i is an event iff (rho - a_i) mod M <= 6,
 // and after it rho = (a_i + 7) mod M. That is a scan with a 15-bit state that is the identity on
-// all but rare records (~7/M of them): k_events runs it over 4096 records per step with a
-// workgroup-wide minimum, and every other quantity (record offsets, and from them fragment types,
-// lengths and pads) follows in parallel from the event list.
+// all but rare records (~7/M of them): k_events finds each next event through per-residue lists
+// (7 candidate residues) over windows of 16384 records, and every other quantity (event blocks,
+// record offsets, and from them fragment types, lengths and pads) follows in parallel from the event list.
 #include <algorithm>
 #include <cstdlib>
 
@@ -41,8 +42,10 @@ constexpr uint32_t kL = kBlock;           // 32768
 constexpr uint32_t kM = kBlock - kHdr;    // 32761
 constexpr int kTileItems = 4096;          // scan tile: 256 threads x 16 items
 constexpr int kEvThreads = 1024;
-constexpr int kEvWin = 8192;  // records per k_events window
+constexpr int kEvWin = 16384;          // records per k_events window (14-bit window index)
+constexpr int kEvShift = 14;
 constexpr int kEvPer = kEvWin / kEvThreads;
+constexpr uint32_t kEvTab = 32768;     // residue table entries (>= M)
 
 // emisc slots
 enum {
@@ -65,6 +68,21 @@ __device__ __forceinline__ uint32_t uvput(uint8_t* p, uint64_t v) {
   while (v >= 0x80) { p[n++] = (uint8_t)(v | 0x80); v >>= 7; }
   p[n++] = (uint8_t)v;
   return n;
+}
+
+// a shift operator (nibble images: 8 x 16 words) applied to x
+__device__ __forceinline__ uint32_t op_apply_s(const uint32_t* __restrict__ op, uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r ^= op[i * 16 + ((x >> (4 * i)) & 15u)];
+  return r;
+}
+// A_{8m}(x) (m zero bytes appended to a raw CRC-32C state) from the power-of-two operators p2[k] =
+// A_{8*2^k} (or their inverses: A_{8m}^-1), one operator per set bit of m
+__device__ __forceinline__ uint32_t shift_by(const uint32_t* __restrict__ p2, uint32_t x, uint64_t m) {
+  for (int k = 0; m != 0 && x != 0; ++k, m >>= 1)
+    if (m & 1u) x = op_apply_s(p2 + k * 128, x);
+  return x;
 }
 
 // ---- source payload access: the record's bytes are the data of fragments [f0, f1] ----
@@ -296,109 +314,159 @@ struct Ev {
   uint32_t pad;
 };
 
-// One workgroup of kEvThreads, kEvWin = kEvThreads * kEvPer records per window in registers (the next
-// window's coordinates are loaded while this one is scanned). A round: every thread tests its records
-// after the last event against rho; each wave's first hit (its owner lane publishes {index, a}) goes to
-// LDS; after ONE barrier every thread reads the 16 wave minima and advances the scan state itself
-// (all threads hold the same state, thread 0 records the event). The LDS slots alternate between two
-// buffers so the next round's writes never meet this round's reads. Rounds per window = events + 1.
+// One workgroup. Window w holds records [w*kEvWin, (w+1)*kEvWin). All threads first enter the window's
+// records into per-residue lists in LDS: head[r] = (w + 1) << 14 | q through an atomic exchange, whose
+// old value (when it belongs to this window) becomes link[q] -- so entries of earlier windows read as
+// absent and the table is never cleared. Wave 0 then runs the scan: the next event after the last one
+// is the first record q > last whose residue r_q = a_q mod M lies in {rho, rho-1, ..., rho-6}; lanes
+// 0..6 walk one residue's list each (about 1.25 entries on average, in arbitrary order, so a list is
+// walked to its end), a wave minimum picks the event and the lane gives the pad d = (rho - r_q) mod M.
+// A round costs a few LDS round trips instead of a workgroup-wide search; the next window's
+// coordinates are loaded during the scan. The event blocks and y-coordinates (blk, ya) follow in
+// k_ev_fix.
 __global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restrict__ da, uint64_t* __restrict__ emisc,
                                                         int lay, uint64_t q0, Ev* __restrict__ ev,
                                                         uint32_t* __restrict__ evb) {
   const uint64_t N = emisc[X_NDENSE];
   uint64_t* X = emisc + X_LAY + lay * kLayStride;
-  const uint64_t AN = X[0];
   const int64_t U = (int64_t)(q0 % kL);
   const uint64_t b0 = q0 / kL;
-  struct Hit {
-    uint32_t q, r;  // window index and residue of the wave's first hit
-    uint64_t a;
-  };
-  __shared__ Hit s_hit[2][kEvThreads / 64];
+  __shared__ uint32_t s_head[kEvTab];
+  __shared__ uint16_t s_link[kEvWin];
+  constexpr uint16_t kNil = 0xffffu;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  // scan state, identical in every thread
-  int64_t ya = -U;
-  uint64_t kb = b0;
-  uint32_t nev = 1;
+  for (uint32_t i = tid; i < kEvTab; i += kEvThreads) s_head[i] = 0;
+  // scan state (wave 0; wave-uniform)
   uint32_t rho = (uint32_t)((kL - U) % kM);  // the virtual block ends at y = L - U
+  uint32_t nev = 1;
+  int32_t last = 0;  // record 0 is never tested against the virtual event
   if (tid == 0) ev[0] = {b0, -U, 0xffffffffu, 0};
-  if (N > 0 && kL - U < (int64_t)kHdr) {    // record 0's header does not fit: pad, event at record 0
-    if (tid == 0) ev[1] = {b0 + 1, 0, 0u, (uint32_t)(kL - U)};
-    ya = 0;
-    kb = b0 + 1;
+  if (N > 0 && kL - U < (int64_t)kHdr) {  // record 0's header does not fit: pad, event at record 0
+    if (tid == 0) ev[1] = {0, 0, 0u, (uint32_t)(kL - U)};
     nev = 2;
-    rho = kL % kM;
+    rho = kHdr;  // (r_0 + 7) mod M with a_0 = 0
   }
-  uint64_t an[kEvPer];  // the next window's coordinates, in flight
+  // coordinates of windows w, w+1, w+2 (loads two windows ahead of the insert)
+  uint64_t a0[kEvPer], a1[kEvPer], a2[kEvPer];
 #pragma unroll
   for (int k = 0; k < kEvPer; ++k) {
     const uint64_t idx = (uint64_t)k * kEvThreads + tid;
-    an[k] = idx < N ? da[idx] : 0;
+    a0[k] = idx < N ? da[idx] : 0;
+    a1[k] = idx + kEvWin < N ? da[idx + kEvWin] : 0;
   }
-  uint32_t par = 0;
-  for (uint64_t base = 0; base < N; base += kEvWin) {
-    if (tid == 0) evb[base / kEvWin] = nev - 1;
-    uint64_t a[kEvPer];
-    uint32_t r[kEvPer];
+  __syncthreads();
+  const uint64_t nwin = (N + kEvWin - 1) / kEvWin;
+  for (uint64_t w = 0; w < nwin; ++w) {
+    const uint64_t base = w * kEvWin;
+    const uint32_t tag = (uint32_t)(w + 1);
 #pragma unroll
     for (int k = 0; k < kEvPer; ++k) {
-      a[k] = an[k];
-      r[k] = (uint32_t)(a[k] % kM);
-      const uint64_t idx = base + kEvWin + (uint64_t)k * kEvThreads + tid;
-      an[k] = idx < N ? da[idx] : 0;
+      const uint32_t q = (uint32_t)k * kEvThreads + tid;
+      const uint64_t idx = base + 2 * kEvWin + q;
+      a2[k] = idx < N ? da[idx] : 0;
     }
-    // record 0 is never tested against the virtual event (its header is in block b0 or it is ev[1])
-    int32_t last = (base == 0) ? 0 : -1;
-    for (;;) {
-      uint32_t best = 0xffffffffu, rbest = 0;
-      uint64_t abest = 0;
 #pragma unroll
-      for (int k = kEvPer - 1; k >= 0; --k) {
-        const uint32_t q = (uint32_t)k * kEvThreads + tid;
-        if (base + q < N && (int32_t)q > last) {
-          int32_t d = (int32_t)rho - (int32_t)r[k];
-          if (d < 0) d += kM;
-          if (d <= 6) { best = q; abest = a[k]; rbest = r[k]; }
-        }
+    for (int k = 0; k < kEvPer; ++k) {
+      const uint32_t q = (uint32_t)k * kEvThreads + tid;
+      if (base + q < N) {
+        const uint32_t r = (uint32_t)(a0[k] % kM);
+        const uint32_t old = atomicExch(&s_head[r], (tag << kEvShift) | q);
+        s_link[q] = (old >> kEvShift) == tag ? (uint16_t)(old & (uint32_t)(kEvWin - 1)) : kNil;
       }
-      uint32_t m = best;
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, d, 64));
-      if (best == m && (m == 0xffffffffu ? lane == 0 : true)) s_hit[par][wave] = {m, rbest, abest};
-      __syncthreads();
-      // lanes 0..15 of every wave read one wave's hit each; the minimum is found with shuffles
-      Hit hh{0xffffffffu, 0u, 0ull};
-      if (lane < (uint32_t)(kEvThreads / 64)) hh = s_hit[par][lane];
-      uint32_t mq = hh.q;
-#pragma unroll
-      for (int d = 8; d >= 1; d >>= 1) mq = min(mq, (uint32_t)__shfl_xor((int)mq, d, 64));
-      const uint32_t b = __builtin_amdgcn_readfirstlane(mq);
-      par ^= 1u;
-      if (b == 0xffffffffu) break;
-      const uint64_t own = __ballot(lane < (uint32_t)(kEvThreads / 64) && hh.q == b);
-      const uint32_t ol = (uint32_t)__builtin_ctzll(own);
-      const uint32_t rb = __builtin_amdgcn_readlane(hh.r, ol);
-      const uint64_t ab = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)hh.a, ol) |
-                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(hh.a >> 32), ol) << 32);
-      int32_t d = (int32_t)rho - (int32_t)rb;
-      if (d < 0) d += kM;
-      const int64_t E = (int64_t)ab + d;                            // block end that hits the header
-      const uint64_t mb = (uint64_t)(E - ya - (int64_t)kL) / kM;   // blocks after the event block
-      kb = kb + mb + 1;
-      if (tid == 0) ev[nev] = {kb, (int64_t)ab, (uint32_t)(base + b), (uint32_t)d};
-      ++nev;
-      ya = (int64_t)ab;
-      rho = (rb + kHdr) % kM;
-      last = (int32_t)b;
+      a0[k] = a1[k];
+      a1[k] = a2[k];
     }
+    __syncthreads();
+    if (wave == 0) {
+      if (lane == 0) evb[w] = nev - 1;
+      for (;;) {
+        uint32_t cand = 0xffffffffu;
+        if (lane < kHdr) {
+          const uint32_t v = rho >= lane ? rho - lane : rho + kM - lane;
+          const uint32_t t = s_head[v];
+          if ((t >> kEvShift) == tag) {
+            uint32_t q = t & (uint32_t)(kEvWin - 1);
+            for (;;) {
+              if ((int32_t)q > last) cand = min(cand, (q << 3) | lane);
+              const uint16_t nx = s_link[q];
+              if (nx == kNil) break;
+              q = nx;
+            }
+          }
+        }
+#pragma unroll
+        for (int s2 = 4; s2 >= 1; s2 >>= 1) cand = min(cand, (uint32_t)__shfl_xor((int)cand, s2, 64));
+        const uint32_t best = __builtin_amdgcn_readfirstlane(cand);
+        if (best == 0xffffffffu) break;
+        const uint32_t q = best >> 3, d = best & 7u;
+        const uint32_t r = rho >= d ? rho - d : rho + kM - d;  // r_q
+        if (lane == 0) ev[nev] = {0, 0, (uint32_t)(base + q), d};
+        ++nev;
+        rho = (r + kHdr) % kM;
+        last = (int32_t)q;
+      }
+      last = -1;
+    }
+    __syncthreads();
   }
   if (tid == 0) {
     X[1] = nev;
     X[4] = b0;
     X[5] = (uint64_t)U;
+  }
+}
+
+// Event blocks and y-coordinates: ev[g].ya = a_rec, the block it starts is kb_g = kb_{g-1} + m_g + 1 with
+// m_g = (E_g - ya_{g-1} - L) / M blocks between (E_g = a_rec + pad: the block end that hit the header),
+// an inclusive scan over the events; then the layout's end (X[2], X[3]). One workgroup.
+__global__ __launch_bounds__(1024) void k_ev_fix(const uint64_t* __restrict__ da, uint64_t* __restrict__ emisc,
+                                                 int lay, Ev* __restrict__ ev) {
+  const uint64_t N = emisc[X_NDENSE];
+  uint64_t* X = emisc + X_LAY + lay * kLayStride;
+  const uint64_t AN = X[0], nev = X[1], b0 = X[4];
+  const int64_t U = (int64_t)X[5];
+  __shared__ uint32_t s_w[16];
+  __shared__ uint64_t s_tot;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint64_t kb = b0;
+  for (uint64_t g0 = 1; g0 < nev; g0 += 1024) {
+    const uint64_t g = g0 + tid;
+    uint32_t steps = 0;
+    int64_t ya = 0;
+    if (g < nev) {
+      const Ev e = ev[g];
+      ya = (int64_t)da[e.rec];
+      const int64_t yp = g == 1 ? -U : (int64_t)da[ev[g - 1].rec];
+      const int64_t E = ya + (int64_t)e.pad;
+      steps = (uint32_t)((uint64_t)(E - yp - (int64_t)kL) / kM + 1);
+    }
+    uint32_t incl = steps;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
+      if (lane >= (uint32_t)d) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+    for (uint32_t k = 0; k < 16; ++k) {
+      if (k < wave) wb += s_w[k];
+      tot += s_w[k];
+    }
+    if (g < nev) {
+      ev[g].blk = kb + wb + incl;
+      ev[g].ya = ya;
+    }
+    if (tid == 0) s_tot = tot;
+    __syncthreads();
+    kb += s_tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int64_t ya = nev > 1 ? (int64_t)da[ev[nev - 1].rec] : -U;
     if (N == 0) {
       X[2] = b0 - 1;  // no blocks
-      X[3] = 40 + q0;
+      X[3] = 40 + b0 * kL + (uint64_t)U;
     } else {
       // the block whose end E_k >= A_N first: E_kb = ya + L, E_{kb+m} = ya + L + m M
       const int64_t over = (int64_t)AN - ya - (int64_t)kL;
@@ -523,15 +591,27 @@ __device__ __forceinline__ uint64_t src_at(uint64_t d0, uint32_t l0, uint32_t st
 // longest source piece: key+value+meta of a record, the key of a hint) | materialised suffix bytes.
 // Records whose prefix + suffix exceed kWLit bytes (NsSize/EtagSize beyond ~60) are marked
 // `general` and written by k_write_general instead.
-constexpr int kWLit = 96;
+//
+// CRC combine (dst WAL records): the source fragments were CRC-verified by the decode, so each one's
+// check word chk = ~unmask(stored) ^ A_{8n}(~0) is the raw CRC-32C R (init 0, no final inversion) of
+// its data. With the source range running to the end of the source payload src (no suffix), the
+// re-encoded payload is pre | src[h, n) (h = mid_off) and by linearity of R
+//     R(pre | src[h, n)) = A_{8(n-h)}(R(pre) ^ R(src[0, h))) ^ R(src),
+// R(src) = the source fragments' check words chained with shifts. R(pre) ^ R(src[0, h)) is the raw
+// CRC of the two header strings right-aligned and XOR-ed (zero when the header is unchanged). The
+// record's CRC (rcrc) is thus known before a byte of it is copied, and k_write only computes the
+// CRC of the shorter piece of a record that the dst layout splits in two (the other piece follows
+// from rcrc); `regular` bit 1 marks such records.
+constexpr int kWLit = 92;
 struct RecDescW {
   uint64_t d0;       // file offset of the data of the source payload's first fragment
   uint32_t l0;       // its length
   uint32_t f0, f1;   // source fragments
   uint32_t mid_off;  // source payload offset of the source range
   uint32_t mid_len;
-  uint8_t npre, nsuf, regular, general;
+  uint8_t npre, nsuf, regular, general;  // regular: bit 0 closed-form source addressing, bit 1 rcrc valid
   uint8_t lit[kWLit];  // prefix bytes, then suffix bytes
+  uint32_t rcrc;       // raw CRC-32C of the whole re-encoded payload (regular bit 1)
 };
 static_assert(sizeof(RecDescW) == 128, "RecDescW layout");
 
@@ -547,7 +627,14 @@ template <int PM>
 __global__ __launch_bounds__(256) void k_recdesc_w(EncDev e, const uint64_t* __restrict__ emisc,
                                                     const uint32_t* __restrict__ dsrc, const uint64_t* __restrict__ dst_da,
                                                     const uint64_t* __restrict__ dpos, const uint8_t* __restrict__ mflag,
-                                                    RecDescW* __restrict__ rd) {
+                                                    const uint32_t* __restrict__ ops, RecDescW* __restrict__ rd) {
+  __shared__ uint32_t t0[256];
+  if (PM == PM_DST) {
+    uint32_t c = threadIdx.x;
+    for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    t0[threadIdx.x] = c;
+    __syncthreads();
+  }
   const uint64_t j = blockIdx.x * 256ull + threadIdx.x;
   if (j >= emisc[X_NDENSE]) return;
   const uint64_t row = dsrc[j];
@@ -599,6 +686,29 @@ __global__ __launch_bounds__(256) void k_recdesc_w(EncDev e, const uint64_t* __r
       }
     }
   }
+  d.rcrc = 0;
+  if (PM == PM_DST && !d.general && nsuf == 0 && m < p.n && (uint64_t)d.mid_off + ml == e.t.size[row]) {
+    // R(pre) ^ R(src[0, h)): both header strings right-aligned to hl bytes, XOR-ed, one CRC pass
+    const uint32_t h = d.mid_off, hl = npre > h ? npre : h;
+    uint32_t x = 0;
+    for (uint32_t b = 0; b < hl; ++b) {
+      uint32_t z = b + npre >= hl ? d.lit[b + npre - hl] : 0u;
+      if (b + h >= hl) {
+        const uint64_t zz = b + h - hl;
+        uint64_t run;
+        z ^= reg ? e.seg[src_at(d.d0, d.l0, e.start_off, zz, run)] : src_byte(e.seg, e.frags, e.start_off, sr, zz);
+      }
+      x = (x >> 8) ^ t0[(x ^ z) & 0xffu];
+    }
+    const uint32_t* p2 = ops + kOpPow2 * 128;
+    uint32_t cs = 0;  // R(src): the source fragments' check words, chained
+    for (uint32_t f = sr.f0; f <= sr.f1; ++f) {
+      const Frag F = e.frags[f];
+      cs = shift_by(p2, cs, F.len) ^ F.chk;
+    }
+    d.rcrc = shift_by(p2, x, ml) ^ cs;
+    d.regular |= 2;
+  }
   uint4* dst = reinterpret_cast<uint4*>(rd + j);
   const uint4* s = reinterpret_cast<const uint4*>(&d);
 #pragma unroll
@@ -648,11 +758,19 @@ struct WArgs {
   WLay w[2];              // dst WAL and hint WAL of a compaction (nlay = 2), or the hint WAL
   uint32_t nlay;
   const uint64_t* emisc;
-  const uint32_t* wops;   // enc_ops + kEncWrOps
+  const uint32_t* wops;   // enc_ops (layout in bcw_internal.h)
   const uint32_t* initc;  // A_{8L}(0xFFFFFFFF)
 };
 
 __device__ __forceinline__ uint64_t blk_end(uint64_t P) { return P + kL - (P - 40) % kL; }
+
+// the records k_wcopy writes (the others go to k_write): regular source, rcrc valid, not general, at
+// most two dst fragments
+__device__ __forceinline__ bool wcopy_item(uint32_t h1w, uint64_t P, uint64_t len) {
+  if (((h1w >> 16) & 3u) != 3u || (h1w >> 24) != 0) return false;  // regular source, rcrc, not general
+  const uint64_t x1 = blk_end(P) - (P + kHdr);
+  return len <= x1 || len - x1 <= kM;
+}
 
 // file offset just past a record whose first header is at P, with a payload of len > 0 bytes
 __device__ __forceinline__ uint64_t rec_end(uint64_t P, uint64_t len) {
@@ -661,13 +779,6 @@ __device__ __forceinline__ uint64_t rec_end(uint64_t P, uint64_t len) {
   const uint64_t rem = len - (be - ds);
   const uint64_t q = (rem - 1) / kM;  // whole continuation blocks before the last fragment
   return be + q * kL + kHdr + (rem - q * kM);
-}
-
-__device__ __forceinline__ uint32_t op_apply_s(const uint32_t* __restrict__ op, uint32_t x) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r ^= op[i * 16 + ((x >> (4 * i)) & 15u)];
-  return r;
 }
 
 __device__ __forceinline__ uint32_t sel_byte(uint4 v, uint32_t b) {
@@ -790,6 +901,7 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
   __shared__ uint32_t t8[8 * 256];
   __shared__ uint32_t sop[40 * kWopStride];  // A_{8*16*n}, A_{8*256*n} (n < 16), A_{8*4096*n} (n < 8)
   __shared__ uint32_t sinv[16 * 128];        // A_{8t}^-1
+  __shared__ uint32_t sp2[2][15 * 128];      // A_{8*2^k}, A_{8*2^k}^-1 (k < 15): the CRC combine
   __shared__ uint32_t s_lit[kWT / kG][kWLitWords];
   const uint32_t tid = threadIdx.x, lane = tid & 63, gl = tid & (kG - 1), gb = lane & ~(uint32_t)(kG - 1);
   for (uint32_t i = tid; i < 256; i += kWT) {
@@ -798,7 +910,11 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
     t8[i] = c;
   }
   for (uint32_t i = tid; i < 40 * 128; i += kWT) sop[(i >> 7) * kWopStride + (i & 127u)] = A.wops[i];
-  for (uint32_t i = tid; i < 16 * 128; i += kWT) sinv[i] = A.wops[40 * 128 + i];
+  for (uint32_t i = tid; i < 16 * 128; i += kWT) sinv[i] = A.wops[kOpInv * 128 + i];
+  for (uint32_t i = tid; i < 15 * 128; i += kWT) {
+    sp2[0][i] = A.wops[kOpPow2 * 128 + i];
+    sp2[1][i] = A.wops[kOpPow2Inv * 128 + i];
+  }
   for (uint32_t i = tid; i < (kWT / kG) * kWLitWords; i += kWT) (&s_lit[0][0])[i] = 0;
   __syncthreads();
   for (uint32_t i = tid; i < 256; i += kWT) {
@@ -853,6 +969,7 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
     const uint64_t P = pc.fp;
     const uint64_t aj = pc.a0;
     const uint64_t len = pc.a1 - aj - kHdr;
+    if (li == 0 && wcopy_item(h1w, P, len)) continue;  // k_wcopy
     WRec R;
     R.d0 = (uint64_t)gw(qc.x, 0) | ((uint64_t)gw(qc.y, 0) << 32);
     R.l0 = gw(qc.z, 0);
@@ -862,7 +979,8 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
     R.npre = (int32_t)(h1w & 0xffu);
     R.zA = R.npre;
     R.zB = (int64_t)R.npre + gw(qc.z, 1);
-    R.regular = ((h1w >> 16) & 0xffu) != 0;
+    R.regular = ((h1w >> 16) & 1u) != 0;
+    const uint32_t rcrc = gw(qc.w, 7);
     // stage the literal bytes in LDS (group-private; the previous record's reads are done: LDS
     // executes a wave's operations in order)
     if (gl >= 2 && gl < 8) {
@@ -882,6 +1000,14 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
       if (prev + gl < P) out[prev + gl - pos] = 0;
     }
 
+    // CRC combine (see RecDescW): a record in one dst fragment takes rcrc; one split in two computes the
+    // shorter piece's CRC and derives the other's, R(data) = A_{8y}(R(First)) ^ R(Last) (y = |Last|)
+    const uint64_t x1 = blk_end(P) - (P + kHdr);  // room in the first block
+    const uint32_t nfr = len <= x1 ? 1u : (len - x1 <= kM ? 2u : 3u);
+    const bool comb = ((h1w >> 17) & 1u) != 0 && nfr <= 2;
+    const bool direct_first = len - x1 >= x1;  // (two pieces) the First is the shorter one
+    uint32_t a_first = 0;
+    uint64_t h_first = 0;
     uint64_t hp = P, x0 = 0;
     for (bool first = true;; first = false) {  // (a zero-length First leaves x0 at 0)
       const uint64_t be = blk_end(hp), ds = hp + kHdr;
@@ -891,6 +1017,7 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
       const uint32_t type = first ? (last ? BCW_RECORD_FULL : BCW_RECORD_FIRST)
                                   : (last ? BCW_RECORD_LAST : BCW_RECORD_MIDDLE);
       const uint32_t ic = A.initc[flen];  // in flight during the pass
+      const bool crc_on = !comb || (nfr == 2 && first == direct_first);
       uint32_t acc = 0;
       if (flen) {
         const uint64_t as = obase + (ds - pos), ae = as + flen;  // output addresses of the data
@@ -977,7 +1104,7 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
             } else {
               for (int32_t b = b0; b < b1; ++b) d[b] = (uint8_t)sel_byte(v, (uint32_t)b);
             }
-            c = op_apply_s(hop, c) ^ crc_step16(t8, 0u, v);
+            if (crc_on) c = op_apply_s(hop, c) ^ crc_step16(t8, 0u, v);
           }
           zb += kStep * kWRounds;
         }
@@ -1034,11 +1161,12 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
             } else {
               for (int32_t b = b0; b < b1; ++b) d[b] = (uint8_t)sel_byte(v, (uint32_t)b);
             }
-            c = op_apply_s(hop, c) ^ crc_step16(t8, 0u, v);
+            if (crc_on) c = op_apply_s(hop, c) ^ crc_step16(t8, 0u, v);
           }
           zb += kStep * kWRounds;
         }
         }
+        if (crc_on) {
         // shift each lane's chain to the end of the fragment's last unit (d < kG units follow it)
         if (gl < nunits) {
           const uint32_t dn = (nunits - 1 - gl) & (kG - 1);
@@ -1049,14 +1177,32 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
         for (int m = 1; m < kG; m <<= 1) c ^= __shfl_xor(c, m, 64);
         const uint32_t t = (uint32_t)(((ul + 1) << 4) - ae);
         acc = t ? op_apply_s(sinv + t * 128, c) : c;
+        }
       }
-      if (gl < kHdr) {
-        const uint32_t crc = ~(acc ^ ic);
-        const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
-        const uint32_t by = gl < 4 ? (masked >> (8 * gl)) : gl == 4 ? (uint32_t)flen
-                          : gl == 5 ? (uint32_t)(flen >> 8) : type;
-        out[hp - pos + gl] = (uint8_t)by;
+      auto put_header = [&](uint64_t h, uint32_t r, uint32_t icv, uint64_t fl, uint32_t ty) {
+        if (gl < kHdr) {
+          const uint32_t crc = ~(r ^ icv);
+          const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
+          const uint32_t by = gl < 4 ? (masked >> (8 * gl)) : gl == 4 ? (uint32_t)fl : gl == 5 ? (uint32_t)(fl >> 8) : ty;
+          out[h - pos + gl] = (uint8_t)by;
+        }
+      };
+      bool put = true;
+      if (comb) {
+        if (nfr == 1) {
+          acc = rcrc;
+        } else if (first) {
+          if (direct_first) a_first = acc;
+          else put = false;  // derived from the Last piece below
+          h_first = hp;
+        } else if (direct_first) {
+          acc = rcrc ^ shift_by(sp2[0], a_first, flen);
+        } else {
+          const uint32_t af = shift_by(sp2[1], rcrc ^ acc, flen);  // A_{8y}^-1
+          put_header(h_first, af, A.initc[x1], x1, BCW_RECORD_FIRST);
+        }
       }
+      if (put) put_header(hp, acc, ic, flen, type);
       x0 += flen;
       if (last) break;
       hp = be;
@@ -1124,6 +1270,208 @@ __global__ __launch_bounds__(256) void k_write_general(WArgs WA, uint32_t li, co
     h[6] = (uint8_t)type;
     if (last) break;
     hp = be;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_wcopy: the dst WAL records whose CRC follows from rcrc (RecDescW `regular` bits 0 and 1) and that
+// the dst layout puts in at most two fragments -- nearly every record of a compaction (k_write takes
+// the others). One wave per record: the literal prefix is written with byte stores, the source range
+// as runs (one per source fragment) of 16 B units aligned to the output, each from two aligned source
+// loads funnel-shifted. A record split in two computes the raw CRC of its shorter piece (lane chunks,
+// bytewise, shifted to the piece end and XOR-ed over the wave) and derives the other piece's from
+// rcrc: R(data) = A_{8y}(R(First)) ^ R(Last).
+constexpr int kCT = 256;
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+  return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
+}
+constexpr int kCU = 2;  // units per lane in flight (8 waves per SIMD: the wave count hides the latency)
+
+
+// copy m bytes from src to dst (global pointers, any alignment), one wave
+__device__ __forceinline__ void copy_run(uint8_t* dst, const uint8_t* src, uint64_t m, const uint8_t* seg,
+                                         uint64_t seg_len, uint32_t lane) {
+  if (m == 0) return;
+  const uint64_t da = uni64((uint64_t)(uintptr_t)dst), de = da + uni64(m);
+  const uint64_t u0 = da >> 4, nu = ((de - 1) >> 4) - u0 + 1;
+  const uint64_t delta = uni64((uint64_t)(uintptr_t)src) - da;  // modular
+  const uint64_t send = uni64((uint64_t)(uintptr_t)seg + seg_len);
+  for (uint64_t k0 = 0; k0 < nu; k0 += 64 * kCU) {
+    uint4 v[kCU];
+    uint32_t kind[kCU];  // 0 none, 1 full unit, 2 partial
+#pragma unroll
+    for (int q = 0; q < kCU; ++q) {
+      const uint64_t k = k0 + (uint64_t)q * 64 + lane;
+      kind[q] = 0;
+      v[q] = make_uint4(0, 0, 0, 0);
+      if (k < nu) {
+        const uint64_t ua = (u0 + k) << 4;
+        const uint64_t sa = ua + delta;
+        if (ua >= da && ua + 16 <= de && (sa & ~15ull) + 32 <= send) {
+          const uint4* w = reinterpret_cast<const uint4*>((uintptr_t)(sa & ~15ull));
+          v[q] = shift16(w[0], w[1], (uint32_t)(sa & 15u));
+          kind[q] = 1;
+        } else {
+          kind[q] = 2;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kCU; ++q) {
+      if (kind[q] == 0) continue;
+      const uint64_t ua = (u0 + k0 + (uint64_t)q * 64 + lane) << 4;
+      uint8_t* d = reinterpret_cast<uint8_t*>((uintptr_t)ua);
+      if (kind[q] == 1) {
+        __builtin_nontemporal_store(v[q].x, reinterpret_cast<uint32_t*>(d));
+        __builtin_nontemporal_store(v[q].y, reinterpret_cast<uint32_t*>(d) + 1);
+        __builtin_nontemporal_store(v[q].z, reinterpret_cast<uint32_t*>(d) + 2);
+        __builtin_nontemporal_store(v[q].w, reinterpret_cast<uint32_t*>(d) + 3);
+      } else {
+        const uint64_t lo = ua > da ? ua : da, hi = ua + 16 < de ? ua + 16 : de;
+        for (uint64_t b = lo; b < hi; ++b)
+          *reinterpret_cast<uint8_t*>((uintptr_t)b) = *reinterpret_cast<const uint8_t*>((uintptr_t)(b + delta));
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kCT) void k_wcopy(WArgs A) {
+  __shared__ uint32_t t0[256];
+  __shared__ uint32_t sp2[2][15 * 128];  // A_{8*2^k}, A_{8*2^k}^-1
+  __shared__ uint32_t s_desc[kCT / 64][32];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  {
+    uint32_t c = tid;
+    for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    t0[tid] = c;
+  }
+  for (uint32_t i = tid; i < 15 * 128; i += kCT) {
+    sp2[0][i] = A.wops[kOpPow2 * 128 + i];
+    sp2[1][i] = A.wops[kOpPow2Inv * 128 + i];
+  }
+  __syncthreads();
+  const WLay& W = A.w[0];
+  if (!lay_ok(A.emisc, W)) return;
+  const EncDev& e = A.e;
+  const uint64_t N = A.emisc[X_NDENSE];
+  uint32_t* sd = s_desc[wave];
+  const uint8_t* lit = reinterpret_cast<const uint8_t*>(sd) + 32;
+  uint8_t* const out = W.out;
+  const uint64_t pos = W.pos;
+  const uint64_t nw = (uint64_t)gridDim.x * (kCT / 64);
+  // the next record's descriptor word (lanes 0..31), header offset and y-coordinates, one record ahead
+  uint32_t ndw = 0;
+  uint64_t nP = 0, na0 = 0, na1 = 0;
+  auto fetch = [&](uint64_t jj) {
+    if (jj >= N) return;
+    ndw = lane < 32 ? reinterpret_cast<const uint32_t*>(static_cast<const RecDescW*>(W.rd) + jj)[lane] : 0u;
+    nP = W.fpos[jj];
+    na0 = W.da[jj];
+    na1 = W.da[jj + 1];
+  };
+  fetch((uint64_t)blockIdx.x * (kCT / 64) + wave);
+  for (uint64_t j = (uint64_t)blockIdx.x * (kCT / 64) + wave; j < N; j += nw) {
+    const uint32_t dw = ndw;
+    const uint64_t P = uni64(nP), aj = uni64(na0), len = uni64(na1) - aj - kHdr;
+    fetch(j + nw);
+    const uint32_t h1w = uni((uint32_t)__shfl((int)dw, 7, 64));
+    if (!wcopy_item(h1w, P, len)) continue;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 32) sd[lane] = dw;  // the previous record's reads are done (LDS keeps a wave's order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t d0 = uni64((uint64_t)sd[0] | ((uint64_t)sd[1] << 32));
+    const uint32_t l0 = uni(sd[2]), mid_off = uni(sd[5]), npre = h1w & 0xffu, rcrc = uni(sd[31]);
+    // zero pad before a record that starts a block (wal.go:509-512)
+    if ((P - 40) % kL == 0) {
+      const uint64_t prev = j == 0 ? pos : rec_end(W.fpos[j - 1], aj - W.da[j - 1] - kHdr);
+      if (prev + lane < P) out[prev + lane - pos] = 0;
+    }
+    const uint64_t be = blk_end(P), x1 = be - (P + kHdr);
+    const uint32_t nfr = len <= x1 ? 1u : 2u;
+    uint32_t cr0 = rcrc, cr1 = 0;
+    if (nfr == 2) {
+      // the shorter piece's raw CRC: lane chunks of [pa, pb) (whole 16 B units of the payload, loaded
+      // up to kPU at a time), each chunk's CRC shifted to pb
+      const bool df = len - x1 >= x1;
+      const uint64_t pa = df ? 0 : x1, pb = df ? x1 : len;
+      const uint64_t c = (((pb - pa + 63) / 64) + 15) & ~15ull;
+      const uint64_t a0 = pa + lane * c, a1 = a0 + c < pb ? a0 + c : pb;
+      uint32_t x = 0;
+      constexpr int kPU = 4;
+      for (uint64_t zb = a0; zb < a1; zb += 16 * kPU) {
+        uint4 u[kPU];
+#pragma unroll
+        for (int q = 0; q < kPU; ++q) {
+          const uint64_t z = zb + 16 * q;
+          u[q] = make_uint4(0, 0, 0, 0);
+          if (z >= a1) continue;
+          uint64_t run = 0;
+          const uint64_t S = z >= npre ? src_at(d0, l0, e.start_off, mid_off + (z - npre), run) : 0;
+          if (z >= npre && run >= 16 && S + 16 <= e.src_len) {
+            __builtin_memcpy(&u[q], e.seg + S, 16);
+          } else {
+            uint32_t wv[4] = {0, 0, 0, 0};
+            for (uint32_t b = 0; b < 16 && z + b < a1; ++b) {
+              const uint64_t zz = z + b;
+              uint32_t by;
+              if (zz < npre) {
+                by = lit[zz];
+              } else {
+                uint64_t r2;
+                by = e.seg[src_at(d0, l0, e.start_off, mid_off + (zz - npre), r2)];
+              }
+#pragma unroll
+              for (int k = 0; k < 4; ++k)
+                if ((b >> 2) == (uint32_t)k) wv[k] |= by << (8 * (b & 3));
+            }
+            u[q] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < kPU; ++q) {
+          const uint64_t z = zb + 16 * q;
+          const uint32_t nb = z >= a1 ? 0u : (a1 - z < 16 ? (uint32_t)(a1 - z) : 16u);
+          const uint32_t wq[4] = {u[q].x, u[q].y, u[q].z, u[q].w};
+          for (uint32_t b = 0; b < nb; ++b) x = (x >> 8) ^ t0[(x ^ (wq[b >> 2] >> (8 * (b & 3)))) & 0xffu];
+        }
+      }
+      x = a0 < a1 ? shift_by(sp2[0], x, pb - a1) : 0u;
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) x ^= (uint32_t)__shfl_xor((int)x, m, 64);
+      const uint64_t y = len - x1;
+      if (df) {
+        cr0 = x;
+        cr1 = rcrc ^ shift_by(sp2[0], x, y);
+      } else {
+        cr1 = x;
+        cr0 = shift_by(sp2[1], rcrc ^ x, y);  // A_{8y}^-1
+      }
+    }
+    for (uint32_t k = 0; k < nfr; ++k) {
+      const uint64_t hp = k == 0 ? P : be, x0 = k == 0 ? 0 : x1;
+      const uint64_t fl = nfr == 1 ? len : (k == 0 ? x1 : len - x1);
+      const uint32_t type = nfr == 1 ? BCW_RECORD_FULL : (k == 0 ? BCW_RECORD_FIRST : BCW_RECORD_LAST);
+      if (lane < kHdr) {
+        const uint32_t crc = ~((k == 0 ? cr0 : cr1) ^ A.initc[fl]);
+        const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
+        const uint32_t by = lane < 4 ? (masked >> (8 * lane)) : lane == 4 ? (uint32_t)fl
+                          : lane == 5 ? (uint32_t)(fl >> 8) : type;
+        out[hp - pos + lane] = (uint8_t)by;
+      }
+      const uint64_t dd = hp + kHdr - pos;  // out index of the fragment's data
+      const uint64_t ze = x0 + fl, le = ze < npre ? ze : npre;
+      for (uint64_t z = x0 + lane; z < le; z += 64) out[dd + (z - x0)] = lit[z];
+      for (uint64_t z = x0 > npre ? x0 : npre; z < ze;) {
+        uint64_t run;
+        const uint64_t S = src_at(d0, l0, e.start_off, mid_off + (z - npre), run);
+        const uint64_t m = run < ze - z ? run : ze - z;
+        copy_run(out + dd + (z - x0), e.seg + S, m, e.seg, e.src_len, lane);
+        z += m;
+      }
+    }
   }
 }
 
@@ -1216,7 +1564,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
   WArgs W{};
   W.e = e;
   W.emisc = s.emisc;
-  W.wops = L.crc_ops + kEncWrOps;
+  W.wops = L.crc_ops;
   W.initc = L.initc;
   const uint32_t rgrid = (uint32_t)((rows + 255) / 256) + 1;
   RecDescW* wd = static_cast<RecDescW*>(s.recdesc);
@@ -1237,6 +1585,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     const int kid = lay == 1 ? K_ENC_EVENTS_HINT : K_ENC_EVENTS;
     pr.begin(kid, st, ev0);
     k_events<<<1, kEvThreads, 0, st>>>(da, s.emisc, lay, pos - 40, evs, s.evb);
+    k_ev_fix<<<1, 1024, 0, st>>>(da, s.emisc, lay, evs);
     pr.end(kid, st, ev0);
   };
   if (compact) {
@@ -1248,7 +1597,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     pr.end(K_ENC_SCAN, st, ev0);
     (void)hipEventRecord(s.ev_scan, st);
     (void)hipStreamWaitEvent(s.aux, s.ev_scan, 0);
-    k_recdesc_w<PM_DST><<<rgrid, 256, 0, s.aux>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, wd);
+    k_recdesc_w<PM_DST><<<rgrid, 256, 0, s.aux>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, L.crc_ops, wd);
     layout(0, s.da, L.p.wal_pos);
     k_recoff<<<rgrid, 256, 0, st>>>(s.da, s.dsrc, s.emisc, 0, evs, s.evb, s.dpos, L.out.rec_off);
     // the hint WAL's layout needs the dst offsets (its records carry them)
@@ -1258,7 +1607,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     pr.end(K_ENC_HINT_LAYOUT, st, ev0);
     (void)hipEventRecord(s.ev_hscan, st);
     (void)hipStreamWaitEvent(s.aux, s.ev_hscan, 0);
-    k_recdesc_w<PM_HINT_DST><<<rgrid, 256, 0, s.aux>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag, wh);
+    k_recdesc_w<PM_HINT_DST><<<rgrid, 256, 0, s.aux>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag, L.crc_ops, wh);
     (void)hipEventRecord(s.ev_desc, s.aux);
     layout(1, s.hda, L.p.hint_pos);
     k_recoff<<<rgrid, 256, 0, st>>>(s.hda, s.dsrc, s.emisc, 1, evs, s.evb, s.hpos, nullptr);
@@ -1272,7 +1621,11 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     static const int hg = [] { const char* v = getenv("BCW_HINT_G"); return v ? atoi(v) : 8; }();
     pr.begin(K_ENC_WRITE, st, ev0);
     // measurement-only ablation (BCW_ENC_ABL: 1 = dst WAL only, 2 = hint WAL only); 0 in the product
-    if (abl != 2) k_write<16><<<wgrid(16), kWT, 0, st>>>(W);
+    if (abl != 2) {
+      k_wcopy<<<(uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, (uint64_t)L.num_cus * 8)), kCT, 0,
+                st>>>(W);
+      k_write<16><<<wgrid(16), kWT, 0, st>>>(W);
+    }
     if (abl != 1) {
       if (hg == 16) k_write<16><<<wgrid(16), kWT, 0, st>>>(H);
       else k_write<8><<<wgrid(8), kWT, 0, st>>>(H);
@@ -1290,7 +1643,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     W.w[1] = W.w[0];
     W.nlay = 1;
     pr.begin(K_ENC_WRITE, st, ev0);
-    k_recdesc_w<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, wd);
+    k_recdesc_w<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, L.crc_ops, wd);
     k_write<8><<<wgrid(8), kWT, 0, st>>>(W);
     k_write_general<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr, s.mflag);
     pr.end(K_ENC_WRITE, st, ev0);

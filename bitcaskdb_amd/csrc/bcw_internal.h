@@ -50,8 +50,10 @@ struct Tables {
   uint32_t* enc_ops;    // [kEncOpsWords] encode shift operators (nibble images, see build_enc_ops)
   uint32_t* pow2;       // [15][8][16] A_{8 * 2^k} (nibble images), k < 15: shifts by any distance < 32 KiB
 };
-constexpr int kEncWrOps = 2 * 16 * 128;              // k_write's operators follow k_pack's
-constexpr int kEncOpsWords = kEncWrOps + 56 * 128;
+// enc_ops layout (operators of 128 words): [n] A_{8*16*n}, [16 + n] A_{8*256*n} (n < 16), [32 + n]
+// A_{8*4096*n} (n < 8), [40 + t] A_{8t}^-1 (t < 16), [56 + k] A_{8*2^k} (k < 32), [88 + k] A_{8*2^k}^-1 (k < 15)
+constexpr int kOpInv = 40, kOpPow2 = 56, kOpPow2Inv = 88;
+constexpr int kEncOpsWords = 103 * 128;
 
 // k_crc LDS table image (dwords): slice-by-2 tables as 256-B rows {T1[e] x32, T0[e] x32} (lane l
 // reads bank l % 32), lane operators transposed to [8][16][64 lanes], then the carry and half operators.

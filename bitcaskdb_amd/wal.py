@@ -37,6 +37,21 @@ class ErrWalUnknownRecordType(WalError):
         super().__init__(msg)
 
 
+class ErrWalMismatchSize(WalError):
+    def __init__(self, msg="size mismatch, corrupted data"):
+        super().__init__(msg)
+
+
+class ErrWalCorruptedData(WalError):
+    def __init__(self, msg="corrupted data"):
+        super().__init__(msg)
+
+
+class ErrWalIncompleteRecord(WalError):
+    def __init__(self, msg="incomplete record"):
+        super().__init__(msg)
+
+
 class ErrWalMismatchMagic(WalError):
     def __init__(self, msg="magic number mismatch"):
         super().__init__(msg)
@@ -167,6 +182,32 @@ class Context:
                 raise RuntimeError(f"bcw_encode_segment: {L.lib.bcw_strerror(rc).decode()}")
             break
         return res, bytes(wal[:int(res.wal_need)]), bytes(hint[:int(res.hint_need)]), offs[:int(res.n_in)].copy()
+
+    # synchronous batched point reads (Wal.ReadRecord + WalParseRecord + RecordFromBytes per request)
+    def read_records(self, seg, offsets, sizes, base_time: int, ns_size: int, etag_size: int, verify: bool = True):
+        """Returns (payload bytes per request, rd_status per request, record table dict)."""
+        seg = np.ascontiguousarray(np.frombuffer(seg, dtype=np.uint8) if not isinstance(seg, np.ndarray) else seg,
+                                   dtype=np.uint8)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+        n = int(offs.size)
+        if sizes.size != n:
+            raise ValueError("offsets and sizes differ in length")
+        p = L.ReadParams(int(seg.size), base_time, ns_size, etag_size, 1 if verify else 0, 0)
+        pay = np.zeros(max(int(sizes.sum()), 1), dtype=np.uint8)
+        st = np.zeros(max(n, 1), dtype=np.uint8)
+        cols = {name: np.zeros(max(n, 1), dtype=dt) for name, dt in L.TABLE_COLUMNS}
+        tab = L.RecordTable(n, *[cols[name].ctypes.data_as(getattr(L, "u8p" if dt == "u1" else
+                                                                   ("u32p" if dt == "u4" else "u64p")))
+                                 for name, dt in L.TABLE_COLUMNS])
+        rc = L.lib.bcw_read_records(self._h, seg.ctypes.data_as(C.c_void_p) if seg.size else None, C.byref(p), n,
+                                    offs.ctypes.data_as(L.u64p), sizes.ctypes.data_as(L.u64p),
+                                    pay.ctypes.data_as(C.c_void_p), st.ctypes.data_as(L.u8p), C.byref(tab))
+        if rc != 0:
+            raise RuntimeError(f"bcw_read_records: {L.lib.bcw_strerror(rc).decode()}")
+        ends = np.concatenate([[0], np.cumsum(sizes, dtype=np.uint64)]) if n else np.zeros(1, np.uint64)
+        payloads = [bytes(pay[int(ends[i]):int(ends[i + 1])]) for i in range(n)]
+        return payloads, st[:n].copy(), {k: v[:n].copy() for k, v in cols.items()}
 
     def fragments(self, capacity: int):
         cols = {name: np.zeros(max(capacity, 1), dtype=dt) for name, dt in L.FRAG_COLUMNS}
@@ -357,6 +398,39 @@ def iterate_hint(hint: Wal, cb, ns_size: int = 20, ctx: Context | None = None):
     err = _frag_error(dec.result)
     if err is not None:
         raise err
+
+
+_RD_ERRORS = {
+    L.RD_BEYOND: lambda: WalError("read beyond file size"),
+    L.RD_CORRUPTED: lambda: ErrWalCorruptedData(),
+    L.RD_CRC: lambda: ErrWalMismatchCRC(),
+    L.RD_SIZE: lambda: ErrWalMismatchSize(),
+    L.RD_TYPE: lambda: ErrWalUnknownRecordType(),
+    L.RD_INCOMPLETE: lambda: ErrWalIncompleteRecord(),
+    L.RD_PANIC: lambda: RefPanic("slice bounds out of range (zero-size read)"),
+}
+
+
+def read_records(wal: Wal, offsets, sizes, verify: bool = True, ns_size: int = 20, etag_size: int = 20,
+                 ctx: Context | None = None) -> list:
+    """The record fetch of DBImpl.Get / GetV2 (db_impl.go:567-631) for many index values at once:
+    Wal.ReadRecord(off, size, verifyChecksum) (wal.go:556-573) then RecordFromBytes (record.go:140-239).
+    One entry per request: a Record, or the exception the reference returns for it (not raised)."""
+    ctx = ctx or default_context()
+    pays, st, t = ctx.read_records(wal.data, offsets, sizes, wal.base_time, ns_size, etag_size, verify)
+    view = Decoded(result=L.DecodeResult(), table=t, seg=wal.data, mode=L.MODE_RECORD, ns_size=ns_size,
+                   etag_size=etag_size)
+    out = []
+    for i, payload in enumerate(pays):
+        if st[i] != L.RD_OK:
+            out.append(_RD_ERRORS[int(st[i])]())
+        elif t["status"][i] == L.ST_INVALID:
+            out.append(ErrInvalidData())
+        elif t["status"][i] == L.ST_PANIC:
+            out.append(RefPanic("slice bounds out of range"))
+        else:
+            out.append(_record_of(view, i, payload))
+    return out
 
 
 # ---- write side: compaction re-encode and hint rebuild ----

@@ -102,6 +102,10 @@ lib.oc_index_put_segment.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64,
 lib.oc_compact_filter.restype = C.c_uint64
 lib.oc_compact_filter.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, vp,
                                   C.c_uint64]
+lib.oc_read_record.restype = C.c_int
+lib.oc_read_record.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, vp]
+lib.oc_record_parse.restype = None
+lib.oc_record_parse.argtypes = [vp, C.c_size_t, C.c_size_t, C.c_uint64, C.c_uint32, C.c_uint32, vp]
 lib.oc_synth_segment.restype = vp
 lib.oc_synth_segment.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
                                  C.c_uint64]
@@ -231,6 +235,22 @@ def wal_block_index_range(offset: int, size: int):
     a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
     lib.oc_wal_block_index_range(offset, size, C.byref(a), C.byref(b), C.byref(c))
     return int(a.value), int(b.value), int(c.value)
+
+
+def read_record(seg, offset: int, size: int, verify: bool = True):
+    """Wal.ReadRecord (wal.go:556-573) -> (OC_RD_* status, payload bytes when OK)."""
+    seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+    out = np.zeros(max(size, 1), dtype=np.uint8)
+    st = int(lib.oc_read_record(_ptr(seg), seg.size, offset, size, int(verify), out.ctypes.data_as(vp)))
+    return st, (bytes(out[:size]) if st == 0 else None)
+
+
+def record_parse(payload: bytes, base_time: int, ns_size: int, etag_size: int):
+    """RecordFromBytes (record.go:140-239) -> one REC_DT row."""
+    r = np.zeros(1, dtype=REC_DT)
+    lib.oc_record_parse(_ptr(payload), len(payload), len(payload), base_time, ns_size, etag_size,
+                        r.ctypes.data_as(vp))
+    return r[0]
 
 
 def decode_fast(seg, start_off, base_time, ns_size, etag_size):
