@@ -760,6 +760,7 @@ struct WArgs {
   const uint64_t* emisc;
   const uint32_t* wops;   // enc_ops (layout in bcw_internal.h)
   const uint32_t* initc;  // A_{8L}(0xFFFFFFFF)
+  uint32_t abl;           // measurement-only ablations of k_wcopy (BCW_ENC_ABL bits 4/8/16); 0 in the product
 };
 
 __device__ __forceinline__ uint64_t blk_end(uint64_t P) { return P + kL - (P - 40) % kL; }
@@ -1289,48 +1290,49 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
 constexpr int kCU = 2;  // units per lane in flight (8 waves per SIMD: the wave count hides the latency)
 
 
-// copy m bytes from src to dst (global pointers, any alignment), one wave
+// copy m bytes from src to dst (global pointers, any alignment), one wave. Every unit (16 B aligned to
+// the output) takes its source bytes from two aligned 16 B loads; partial units at the run's ends
+// store only their bytes, from registers.
 __device__ __forceinline__ void copy_run(uint8_t* dst, const uint8_t* src, uint64_t m, const uint8_t* seg,
                                          uint64_t seg_len, uint32_t lane) {
   if (m == 0) return;
   const uint64_t da = uni64((uint64_t)(uintptr_t)dst), de = da + uni64(m);
   const uint64_t u0 = da >> 4, nu = ((de - 1) >> 4) - u0 + 1;
   const uint64_t delta = uni64((uint64_t)(uintptr_t)src) - da;  // modular
-  const uint64_t send = uni64((uint64_t)(uintptr_t)seg + seg_len);
+  const uint64_t sbeg = uni64((uint64_t)(uintptr_t)seg), send = sbeg + uni64(seg_len);
   for (uint64_t k0 = 0; k0 < nu; k0 += 64 * kCU) {
     uint4 v[kCU];
-    uint32_t kind[kCU];  // 0 none, 1 full unit, 2 partial
+    bool ok[kCU];
 #pragma unroll
     for (int q = 0; q < kCU; ++q) {
       const uint64_t k = k0 + (uint64_t)q * 64 + lane;
-      kind[q] = 0;
+      const uint64_t ua = (u0 + k) << 4;
+      const uint64_t sa = ua + delta, sw = sa & ~15ull;
       v[q] = make_uint4(0, 0, 0, 0);
-      if (k < nu) {
-        const uint64_t ua = (u0 + k) << 4;
-        const uint64_t sa = ua + delta;
-        if (ua >= da && ua + 16 <= de && (sa & ~15ull) + 32 <= send) {
-          const uint4* w = reinterpret_cast<const uint4*>((uintptr_t)(sa & ~15ull));
-          v[q] = shift16(w[0], w[1], (uint32_t)(sa & 15u));
-          kind[q] = 1;
-        } else {
-          kind[q] = 2;
-        }
+      ok[q] = k < nu && sw >= sbeg && sw + 32 <= send;
+      if (ok[q]) {
+        const uint4* w = reinterpret_cast<const uint4*>((uintptr_t)sw);
+        v[q] = shift16(w[0], w[1], (uint32_t)(sa & 15u));
       }
     }
 #pragma unroll
     for (int q = 0; q < kCU; ++q) {
-      if (kind[q] == 0) continue;
-      const uint64_t ua = (u0 + k0 + (uint64_t)q * 64 + lane) << 4;
+      const uint64_t k = k0 + (uint64_t)q * 64 + lane;
+      if (k >= nu) continue;
+      const uint64_t ua = (u0 + k) << 4;
       uint8_t* d = reinterpret_cast<uint8_t*>((uintptr_t)ua);
-      if (kind[q] == 1) {
+      if (ok[q] && ua >= da && ua + 16 <= de) {
         __builtin_nontemporal_store(v[q].x, reinterpret_cast<uint32_t*>(d));
         __builtin_nontemporal_store(v[q].y, reinterpret_cast<uint32_t*>(d) + 1);
         __builtin_nontemporal_store(v[q].z, reinterpret_cast<uint32_t*>(d) + 2);
         __builtin_nontemporal_store(v[q].w, reinterpret_cast<uint32_t*>(d) + 3);
       } else {
-        const uint64_t lo = ua > da ? ua : da, hi = ua + 16 < de ? ua + 16 : de;
-        for (uint64_t b = lo; b < hi; ++b)
-          *reinterpret_cast<uint8_t*>((uintptr_t)b) = *reinterpret_cast<const uint8_t*>((uintptr_t)(b + delta));
+        const uint32_t b0 = ua < da ? (uint32_t)(da - ua) : 0u, b1 = ua + 16 > de ? (uint32_t)(de - ua) : 16u;
+        if (ok[q]) {
+          for (uint32_t b = b0; b < b1; ++b) d[b] = (uint8_t)sel_byte(v[q], b);
+        } else {  // the source window touches the segment's ends: bytewise
+          for (uint32_t b = b0; b < b1; ++b) d[b] = *reinterpret_cast<const uint8_t*>((uintptr_t)(ua + b + delta));
+        }
       }
     }
   }
@@ -1392,7 +1394,7 @@ __global__ __launch_bounds__(kCT) void k_wcopy(WArgs A) {
     const uint64_t be = blk_end(P), x1 = be - (P + kHdr);
     const uint32_t nfr = len <= x1 ? 1u : 2u;
     uint32_t cr0 = rcrc, cr1 = 0;
-    if (nfr == 2) {
+    if (nfr == 2 && !(A.abl & 16)) {
       // the shorter piece's raw CRC: lane chunks of [pa, pb) (whole 16 B units of the payload, loaded
       // up to kPU at a time), each chunk's CRC shifted to pb
       const bool df = len - x1 >= x1;
@@ -1454,7 +1456,7 @@ __global__ __launch_bounds__(kCT) void k_wcopy(WArgs A) {
       const uint64_t hp = k == 0 ? P : be, x0 = k == 0 ? 0 : x1;
       const uint64_t fl = nfr == 1 ? len : (k == 0 ? x1 : len - x1);
       const uint32_t type = nfr == 1 ? BCW_RECORD_FULL : (k == 0 ? BCW_RECORD_FIRST : BCW_RECORD_LAST);
-      if (lane < kHdr) {
+      if (lane < kHdr && !(A.abl & 8)) {
         const uint32_t crc = ~((k == 0 ? cr0 : cr1) ^ A.initc[fl]);
         const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
         const uint32_t by = lane < 4 ? (masked >> (8 * lane)) : lane == 4 ? (uint32_t)fl
@@ -1463,7 +1465,9 @@ __global__ __launch_bounds__(kCT) void k_wcopy(WArgs A) {
       }
       const uint64_t dd = hp + kHdr - pos;  // out index of the fragment's data
       const uint64_t ze = x0 + fl, le = ze < npre ? ze : npre;
-      for (uint64_t z = x0 + lane; z < le; z += 64) out[dd + (z - x0)] = lit[z];
+      if (!(A.abl & 8))
+        for (uint64_t z = x0 + lane; z < le; z += 64) out[dd + (z - x0)] = lit[z];
+      if (!(A.abl & 4))
       for (uint64_t z = x0 > npre ? x0 : npre; z < ze;) {
         uint64_t run;
         const uint64_t S = src_at(d0, l0, e.start_off, mid_off + (z - npre), run);
@@ -1566,6 +1570,8 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
   W.emisc = s.emisc;
   W.wops = L.crc_ops;
   W.initc = L.initc;
+  static const int abl_env = [] { const char* v = getenv("BCW_ENC_ABL"); return v ? atoi(v) : 0; }();
+  W.abl = (uint32_t)abl_env;
   const uint32_t rgrid = (uint32_t)((rows + 255) / 256) + 1;
   RecDescW* wd = static_cast<RecDescW*>(s.recdesc);
   RecDescW* wh = static_cast<RecDescW*>(s.recdesc_h);
@@ -1617,7 +1623,7 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     W.nlay = 1;
     WArgs H = W;
     H.w[0] = W.w[1];
-    static const int abl = [] { const char* v = getenv("BCW_ENC_ABL"); return v ? atoi(v) : 0; }();
+    const int abl = abl_env & 3;
     static const int hg = [] { const char* v = getenv("BCW_HINT_G"); return v ? atoi(v) : 8; }();
     pr.begin(K_ENC_WRITE, st, ev0);
     // measurement-only ablation (BCW_ENC_ABL: 1 = dst WAL only, 2 = hint WAL only); 0 in the product
