@@ -333,7 +333,8 @@ static void free_scratch(Scratch& s) {
 
 static void free_enc_scratch(EncScratch& e) {
   void* ptrs[] = {e.sz,    e.mflag, e.dsrc, e.da,      e.hda,       e.hsz,  e.dpos,
-                  e.hpos,  e.tiles, e.ev,   e.evb,     e.recdesc,   e.recdesc_h, e.emisc};
+                  e.hpos,  e.tiles, e.ev,   e.evb,     e.recdesc,   e.recdesc_h, e.emisc, e.evt,
+                  e.hnl,   e.evw};
   for (void* q : ptrs) (void)hipFree(q);
   hipStream_t aux = e.aux;
   hipEvent_t evs[3] = {e.ev_scan, e.ev_hscan, e.ev_desc};
@@ -640,6 +641,8 @@ static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows) {
             hipMalloc(&e.dpos, r * 8) == hipSuccess && hipMalloc(&e.hpos, r * 8) == hipSuccess &&
             hipMalloc(&e.tiles, ntiles * enc_sizeof_tile()) == hipSuccess &&
             hipMalloc(&e.ev, (r + 2) * enc_sizeof_ev()) == hipSuccess && hipMalloc(&e.evb, nwin * 4) == hipSuccess &&
+            hipMalloc(&e.evt, nwin * 32768 * 8) == hipSuccess && hipMalloc(&e.hnl, r * 2) == hipSuccess &&
+            hipMalloc(&e.evw, nwin * 12) == hipSuccess &&
             hipMalloc(&e.recdesc, r * enc_sizeof_recdesc()) == hipSuccess &&
             hipMalloc(&e.recdesc_h, r * enc_sizeof_recdesc()) == hipSuccess &&
             hipMalloc(&e.emisc, 64 * sizeof(uint64_t)) == hipSuccess;

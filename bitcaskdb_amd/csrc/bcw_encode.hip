@@ -8,10 +8,9 @@
 // Pipeline (one HIP stream, no host synchronisation; DESIGN.md "Encode"):
 //   k_enc_prep      per source row: keep / Encode errors / re-encoded payload size     record.go:57-138
 //   k_tile_*        3-phase scan: dense list of written records, y-coordinates a_j
-//   k_events        the writer's layout recurrence as an event scan (one workgroup)    wal.go:505-549
-//   k_ev_fix        event blocks / y-coordinates (a scan over the events), layout end
+//   k_ev_win/walk/emit/fix  the writer's layout recurrence as an event scan              wal.go:505-549
 //   k_recoff        per record: the file offset WriteRecord returns                     wal.go:514-516
-//   (compaction) k_hint_sizes + scan + k_events + k_recoff for the hint WAL            hint.go:32-48
+//   (compaction) k_hint_sizes + scan + event scan + k_recoff for the hint WAL           hint.go:32-48
 //   k_recdesc_w     per record: payload as literal prefix | source range | literal suffix
 //   k_write         one persistent launch over every record of both WALs: fragments in closed form,
 //                   16 B units copied and folded into each fragment's CRC-32C (utils.go:24-29)
@@ -27,9 +26,10 @@
 // bytes), else at E_k with a continuation header. Between events every block start is congruent
 // mod M, so with rho = (next block end) mod M, record i is an event iff (rho - a_i) mod M <= 6,
 // and after it rho = (a_i + 7) mod M. That is a scan with a 15-bit state that is the identity on
-// all but rare records (~7/M of them): k_events finds each next event through per-residue lists
-// (7 candidate residues) over windows of 16384 records, and every other quantity (event blocks,
-// record offsets, and from them fragment types, lengths and pads) follows in parallel from the event list.
+// all but rare records (~7/M of them). The scan runs in parallel over windows of 16384 records
+// (per-window next-event chains and state tables, one sequential table read per window, see k_ev_win),
+// and every other quantity (event blocks, record offsets, and from them fragment types, lengths and
+// pads) follows in parallel from the event list.
 #include <algorithm>
 #include <cstdlib>
 
@@ -41,10 +41,8 @@ namespace enc {
 constexpr uint32_t kL = kBlock;           // 32768
 constexpr uint32_t kM = kBlock - kHdr;    // 32761
 constexpr int kTileItems = 4096;          // scan tile: 256 threads x 16 items
-constexpr int kEvThreads = 1024;
-constexpr int kEvWin = 16384;          // records per k_events window (14-bit window index)
+constexpr int kEvWin = 16384;          // records per event-scan window (14-bit record index in a window)
 constexpr int kEvShift = 14;
-constexpr int kEvPer = kEvWin / kEvThreads;
 constexpr uint32_t kEvTab = 32768;     // residue table entries (>= M)
 
 // emisc slots
@@ -314,105 +312,210 @@ struct Ev {
   uint32_t pad;
 };
 
-// One workgroup. Window w holds records [w*kEvWin, (w+1)*kEvWin). All threads first enter the window's
-// records into per-residue lists in LDS: head[r] = (w + 1) << 14 | q through an atomic exchange, whose
-// old value (when it belongs to this window) becomes link[q] -- so entries of earlier windows read as
-// absent and the table is never cleared. Wave 0 then runs the scan: the next event after the last one
-// is the first record q > last whose residue r_q = a_q mod M lies in {rho, rho-1, ..., rho-6}; lanes
-// 0..6 walk one residue's list each (about 1.25 entries on average, in arbitrary order, so a list is
-// walked to its end), a wave minimum picks the event and the lane gives the pad d = (rho - r_q) mod M.
-// A round costs a few LDS round trips instead of a workgroup-wide search; the next window's
-// coordinates are loaded during the scan. The event blocks and y-coordinates (blk, ya) follow in
-// k_ev_fix.
-__global__ __launch_bounds__(kEvThreads) void k_events(const uint64_t* __restrict__ da, uint64_t* __restrict__ emisc,
-                                                        int lay, uint64_t q0, Ev* __restrict__ ev,
-                                                        uint32_t* __restrict__ evb) {
+// The scan in parallel. Records are cut into windows of kEvWin. For record q, let hn(q) be the next
+// event if q is one: the first q' > q with r_q' in {r_q + 1, ..., r_q + 7} (mod M). Within a window the
+// events after any event are the hn-chain from it, so:
+//   k_ev_win   one workgroup per window: per-residue lists in LDS (atomic exchange; link = old head),
+//              hn inside the window by walking 7 lists, then pointer jumping gives every record's
+//              chain end in the window and chain length; finally, for every state rho, the window's
+//              first event q (the first record with r_q in {rho - 6, ..., rho}) and what its chain
+//              leaves behind: T_w[rho] = q | events << 16 | r_last << 32 (q = 0xffff: no event, rho
+//              passes through unchanged). Window 0 also resolves the writer's start (record 0 excluded,
+//              or the forced event at record 0 when its header does not fit the first block).
+//   k_ev_walk  one thread: rho through the windows, one T read per window: each window's first event,
+//              its entry state and the events before it.
+//   k_ev_emit  one thread per window: the window's events along its hn-chain (record, pad).
+//   k_ev_fix   event blocks / y-coordinates, the layout end.
+constexpr uint16_t kNone16 = 0xffffu;
+constexpr uint64_t kTNone = 0xffffull;
+constexpr int kEvPer = kEvWin / 1024;
+
+__global__ __launch_bounds__(1024) void k_ev_win(const uint64_t* __restrict__ da, uint64_t* __restrict__ emisc,
+                                                 int lay, uint64_t q0, uint64_t* __restrict__ evt,
+                                                 uint16_t* __restrict__ hnl) {
+  const uint64_t N = emisc[X_NDENSE];
+  const uint64_t w = blockIdx.x, base = w * kEvWin;
+  if (base >= N) return;
+  const uint32_t nq = (uint32_t)(N - base < (uint64_t)kEvWin ? N - base : (uint64_t)kEvWin);
+  __shared__ uint32_t s_a[kEvTab];  // list heads; then F[32768] (u16), P[16384] (u16), C[16384] (u16)
+  __shared__ uint16_t s_b[kEvWin];  // list links; then the residue of every record
+  uint16_t* F = reinterpret_cast<uint16_t*>(s_a);
+  uint16_t* Pp = F + kEvTab;
+  uint16_t* Cc = Pp + kEvWin;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  for (uint32_t i = tid; i < kEvTab; i += 1024) s_a[i] = 0xffffffffu;
+  uint32_t r[kEvPer];
+#pragma unroll
+  for (int k = 0; k < kEvPer; ++k) {
+    const uint32_t q = (uint32_t)k * 1024 + tid;
+    r[k] = q < nq ? (uint32_t)(da[base + q] % kM) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kEvPer; ++k) {
+    const uint32_t q = (uint32_t)k * 1024 + tid;
+    if (q < nq) {
+      const uint32_t old = atomicExch(&s_a[r[k]], q);
+      s_b[q] = old == 0xffffffffu ? kNone16 : (uint16_t)old;
+    }
+  }
+  __syncthreads();
+  // min q' > after in the list of residue v (lists are in arbitrary order: walked to the end)
+  auto walk = [&](uint32_t v, int32_t after) -> uint32_t {
+    uint32_t best = kNone16;
+    uint32_t t = s_a[v];
+    while (t != 0xffffffffu) {
+      if ((int32_t)t > after && t < best) best = t;
+      const uint16_t nx = s_b[t];
+      t = nx == kNone16 ? 0xffffffffu : nx;
+    }
+    return best;
+  };
+  uint16_t fv[kEvTab / 1024];
+#pragma unroll
+  for (int k = 0; k < (int)(kEvTab / 1024); ++k) {
+    const uint32_t v = (uint32_t)k * 1024 + tid;
+    fv[k] = v < kM ? (uint16_t)walk(v, -1) : kNone16;
+  }
+  uint16_t hn[kEvPer];
+#pragma unroll
+  for (int k = 0; k < kEvPer; ++k) {
+    const uint32_t q = (uint32_t)k * 1024 + tid;
+    uint32_t b = kNone16;
+    if (q < nq)
+      for (uint32_t d = 1; d <= kHdr; ++d) {
+        const uint32_t v = r[k] + d >= kM ? r[k] + d - kM : r[k] + d;
+        b = min(b, walk(v, (int32_t)q));
+      }
+    hn[k] = (uint16_t)b;
+  }
+  // window 0: the first event after the writer's start position q0
+  uint32_t qs = kNone16;
+  if (w == 0 && tid < 64) {
+    const int64_t U = (int64_t)(q0 % kL);
+    if (kL - U < (int64_t)kHdr) {
+      qs = 0;  // record 0's header does not fit: pad, event at record 0
+    } else {
+      const uint32_t rho0 = (uint32_t)((kL - U) % kM);
+      uint32_t c = kNone16;
+      if (lane < kHdr) c = walk(rho0 >= lane ? rho0 - lane : rho0 + kM - lane, 0);  // record 0 never tested
+#pragma unroll
+      for (int s2 = 4; s2 >= 1; s2 >>= 1) c = min(c, (uint32_t)__shfl_xor((int)c, s2, 64));
+      qs = c;
+    }
+  }
+  __syncthreads();  // every list read is done: the LDS is reused
+#pragma unroll
+  for (int k = 0; k < (int)(kEvTab / 1024); ++k) F[(uint32_t)k * 1024 + tid] = fv[k];
+#pragma unroll
+  for (int k = 0; k < kEvPer; ++k) {
+    const uint32_t q = (uint32_t)k * 1024 + tid;
+    if (q < nq) {
+      Pp[q] = hn[k] == kNone16 ? (uint16_t)q : hn[k];
+      Cc[q] = hn[k] == kNone16 ? 0 : 1;
+      s_b[q] = (uint16_t)r[k];
+      hnl[base + q] = hn[k];
+    }
+  }
+  __syncthreads();
+  // pointer jumping: P -> the chain's last record in the window, C -> hops to it
+  for (int round = 0; round < kEvShift; ++round) {
+    uint16_t np[kEvPer], nc[kEvPer];
+#pragma unroll
+    for (int k = 0; k < kEvPer; ++k) {
+      const uint32_t q = (uint32_t)k * 1024 + tid;
+      np[k] = 0;
+      nc[k] = 0;
+      if (q < nq) {
+        const uint32_t pq = Pp[q];
+        np[k] = Pp[pq];
+        nc[k] = (uint16_t)(Cc[q] + Cc[pq]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kEvPer; ++k) {
+      const uint32_t q = (uint32_t)k * 1024 + tid;
+      if (q < nq) {
+        Pp[q] = np[k];
+        Cc[q] = nc[k];
+      }
+    }
+    __syncthreads();
+  }
+  auto entry = [&](uint32_t q) -> uint64_t {
+    return q == kNone16 ? kTNone
+                        : ((uint64_t)q | ((uint64_t)(Cc[q] + 1u) << 16) | ((uint64_t)s_b[Pp[q]] << 32));
+  };
+  uint64_t* T = evt + w * kEvTab;
+#pragma unroll 4
+  for (int k = 0; k < (int)(kEvTab / 1024); ++k) {
+    const uint32_t rho = (uint32_t)k * 1024 + tid;
+    uint64_t ent = kTNone;
+    if (rho < kM) {
+      uint32_t q = kNone16;
+      for (uint32_t d = 0; d < kHdr; ++d) q = min(q, (uint32_t)F[rho >= d ? rho - d : rho + kM - d]);
+      ent = entry(q);
+    }
+    T[rho] = ent;
+  }
+  if (w == 0 && tid == 0) emisc[X_LAY + lay * kLayStride + 6] = entry(qs);
+}
+
+// one thread: the state through the windows (ev[0] = the writer's start; evw[w] = {first event of window
+// w (0xffffffff: none), state entering it, events before it})
+__global__ void k_ev_walk(uint64_t* __restrict__ emisc, int lay, uint64_t q0, const uint64_t* __restrict__ evt,
+                          uint32_t* __restrict__ evw, Ev* __restrict__ ev) {
+  if (threadIdx.x != 0) return;
   const uint64_t N = emisc[X_NDENSE];
   uint64_t* X = emisc + X_LAY + lay * kLayStride;
   const int64_t U = (int64_t)(q0 % kL);
   const uint64_t b0 = q0 / kL;
-  __shared__ uint32_t s_head[kEvTab];
-  __shared__ uint16_t s_link[kEvWin];
-  constexpr uint16_t kNil = 0xffffu;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  for (uint32_t i = tid; i < kEvTab; i += kEvThreads) s_head[i] = 0;
-  // scan state (wave 0; wave-uniform)
-  uint32_t rho = (uint32_t)((kL - U) % kM);  // the virtual block ends at y = L - U
-  uint32_t nev = 1;
-  int32_t last = 0;  // record 0 is never tested against the virtual event
-  if (tid == 0) ev[0] = {b0, -U, 0xffffffffu, 0};
-  if (N > 0 && kL - U < (int64_t)kHdr) {  // record 0's header does not fit: pad, event at record 0
-    if (tid == 0) ev[1] = {0, 0, 0u, (uint32_t)(kL - U)};
-    nev = 2;
-    rho = kHdr;  // (r_0 + 7) mod M with a_0 = 0
-  }
-  // coordinates of windows w, w+1, w+2 (loads two windows ahead of the insert)
-  uint64_t a0[kEvPer], a1[kEvPer], a2[kEvPer];
-#pragma unroll
-  for (int k = 0; k < kEvPer; ++k) {
-    const uint64_t idx = (uint64_t)k * kEvThreads + tid;
-    a0[k] = idx < N ? da[idx] : 0;
-    a1[k] = idx + kEvWin < N ? da[idx + kEvWin] : 0;
-  }
-  __syncthreads();
+  ev[0] = {b0, -U, 0xffffffffu, 0};
   const uint64_t nwin = (N + kEvWin - 1) / kEvWin;
+  uint32_t rho = (uint32_t)((kL - U) % kM);
+  uint64_t total = 0;
   for (uint64_t w = 0; w < nwin; ++w) {
-    const uint64_t base = w * kEvWin;
-    const uint32_t tag = (uint32_t)(w + 1);
-#pragma unroll
-    for (int k = 0; k < kEvPer; ++k) {
-      const uint32_t q = (uint32_t)k * kEvThreads + tid;
-      const uint64_t idx = base + 2 * kEvWin + q;
-      a2[k] = idx < N ? da[idx] : 0;
+    const uint64_t ent = w == 0 ? X[6] : evt[w * kEvTab + rho];
+    const uint32_t q = (uint32_t)(ent & 0xffffu);
+    evw[3 * w + 2] = (uint32_t)total;
+    if (q == kNone16) {
+      evw[3 * w] = 0xffffffffu;
+      continue;
     }
-#pragma unroll
-    for (int k = 0; k < kEvPer; ++k) {
-      const uint32_t q = (uint32_t)k * kEvThreads + tid;
-      if (base + q < N) {
-        const uint32_t r = (uint32_t)(a0[k] % kM);
-        const uint32_t old = atomicExch(&s_head[r], (tag << kEvShift) | q);
-        s_link[q] = (old >> kEvShift) == tag ? (uint16_t)(old & (uint32_t)(kEvWin - 1)) : kNil;
-      }
-      a0[k] = a1[k];
-      a1[k] = a2[k];
-    }
-    __syncthreads();
-    if (wave == 0) {
-      if (lane == 0) evb[w] = nev - 1;
-      for (;;) {
-        uint32_t cand = 0xffffffffu;
-        if (lane < kHdr) {
-          const uint32_t v = rho >= lane ? rho - lane : rho + kM - lane;
-          const uint32_t t = s_head[v];
-          if ((t >> kEvShift) == tag) {
-            uint32_t q = t & (uint32_t)(kEvWin - 1);
-            for (;;) {
-              if ((int32_t)q > last) cand = min(cand, (q << 3) | lane);
-              const uint16_t nx = s_link[q];
-              if (nx == kNil) break;
-              q = nx;
-            }
-          }
-        }
-#pragma unroll
-        for (int s2 = 4; s2 >= 1; s2 >>= 1) cand = min(cand, (uint32_t)__shfl_xor((int)cand, s2, 64));
-        const uint32_t best = __builtin_amdgcn_readfirstlane(cand);
-        if (best == 0xffffffffu) break;
-        const uint32_t q = best >> 3, d = best & 7u;
-        const uint32_t r = rho >= d ? rho - d : rho + kM - d;  // r_q
-        if (lane == 0) ev[nev] = {0, 0, (uint32_t)(base + q), d};
-        ++nev;
-        rho = (r + kHdr) % kM;
-        last = (int32_t)q;
-      }
-      last = -1;
-    }
-    __syncthreads();
+    evw[3 * w] = q;
+    evw[3 * w + 1] = rho;
+    total += (ent >> 16) & 0xffffu;
+    rho = (uint32_t)(((ent >> 32) & 0xffffu) + kHdr) % kM;
   }
-  if (tid == 0) {
-    X[1] = nev;
-    X[4] = b0;
-    X[5] = (uint64_t)U;
+  X[1] = 1 + total;
+  X[4] = b0;
+  X[5] = (uint64_t)U;
+}
+
+// one thread per window: its events along the hn-chain; evb[w] = index of the last event before it
+__global__ __launch_bounds__(64) void k_ev_emit(const uint64_t* __restrict__ da, const uint64_t* __restrict__ emisc,
+                                                const uint32_t* __restrict__ evw, const uint16_t* __restrict__ hnl,
+                                                Ev* __restrict__ ev, uint32_t* __restrict__ evb) {
+  const uint64_t N = emisc[X_NDENSE];
+  const uint64_t w = blockIdx.x * 64ull + threadIdx.x;
+  if (w * kEvWin >= N) return;
+  const uint32_t before = evw[3 * w + 2];
+  evb[w] = before;
+  uint32_t q = evw[3 * w];
+  if (q == 0xffffffffu) return;
+  uint32_t rho = evw[3 * w + 1];
+  uint64_t g = 1ull + before;
+  const uint64_t base = w * kEvWin;
+  for (;;) {
+    const uint64_t rec = base + q;
+    const uint16_t nx = hnl[rec];
+    const uint32_t rq = (uint32_t)(da[rec] % kM);
+    const uint32_t d = rho >= rq ? rho - rq : rho + kM - rq;  // (rho - r) mod M <= 6: the pad
+    ev[g++] = {0, 0, (uint32_t)rec, d};
+    rho = (rq + kHdr) % kM;
+    if (nx == kNone16) break;
+    q = nx;
   }
 }
 
@@ -506,33 +609,53 @@ __global__ __launch_bounds__(256) void k_recoff(const uint64_t* __restrict__ da,
 }
 
 // ------------------------------------------------------------------------------------------
-// Payload programs: a record's payload as up to 6 pieces, each literal bytes (computed here) or a
-// range of the source record's payload.
+// Payload programs: a record's payload as up to 6 pieces, each literal bytes (computed here, kept by a
+// literal sink: a local array, or a thread's dword-interleaved slice of LDS) or a range of the source
+// record's payload.
 struct Prog {
   uint32_t len[6];
-  uint64_t off[6];   // literal: offset into lit; source: payload offset in the source record
+  uint64_t off[6];   // literal: offset into the literals; source: payload offset in the source record
   uint8_t src[6];
   uint32_t n;
-  uint8_t lit[48];
 };
+struct LitLocal {  // a local array
+  uint8_t* p;
+  __device__ __forceinline__ void put(uint32_t k, uint32_t b) const { p[k] = (uint8_t)b; }
+  __device__ __forceinline__ uint32_t get(uint32_t k) const { return p[k]; }
+};
+struct LitLds {  // byte k of thread t at dword (k / 4) * 256 + t: lanes at one k read consecutive dwords
+  uint8_t* base;
+  uint32_t t;
+  __device__ __forceinline__ uint8_t* at(uint32_t k) const { return base + ((((k >> 2) << 8) + t) << 2) + (k & 3u); }
+  __device__ __forceinline__ void put(uint32_t k, uint32_t b) const { *at(k) = (uint8_t)b; }
+  __device__ __forceinline__ uint32_t get(uint32_t k) const { return *at(k); }
+};
+template <class LIT>
+__device__ __forceinline__ uint32_t uvput_l(const LIT& l, uint32_t o, uint64_t v) {
+  uint32_t n = 0;
+  while (v >= 0x80) { l.put(o + n++, (uint32_t)(v | 0x80) & 0xffu); v >>= 7; }
+  l.put(o + n++, (uint32_t)v);
+  return n;
+}
 
 // Record.Encode (record.go:57-138) of source row i against the dst baseTime
-__device__ void prog_record(const EncDev& e, uint64_t i, bool mdrop, Prog& p) {
+template <class LIT>
+__device__ void prog_record(const EncDev& e, uint64_t i, bool mdrop, Prog& p, const LIT& lit) {
   const bcw_record_table& t = e.t;
   const uint32_t flags = t.flags[i];
   const uint64_t klen = t.key_len[i], vlen = t.val_len[i], expire = t.expire[i];
   const uint64_t mlen = mdrop ? 0 : t.meta_len[i];
   const uint32_t el = (flags & 1u) ? 0u : e.etag;
-  uint8_t flag = (uint8_t)((el == 0 ? 1u : 0u) | (flags & 4u) | (expire == 0 ? 2u : 0u));
+  const uint32_t flag = (el == 0 ? 1u : 0u) | (flags & 4u) | (expire == 0 ? 2u : 0u);
   uint32_t o = 1;
-  p.lit[o++] = flag;
-  o += uvput(p.lit + o, klen);
-  o += uvput(p.lit + o, vlen);
-  o += uvput(p.lit + o, mlen);
+  lit.put(o++, flag);
+  o += uvput_l(lit, o, klen);
+  o += uvput_l(lit, o, vlen);
+  o += uvput_l(lit, o, mlen);
   const uint32_t vend = o;
-  if (expire != 0) o += uvput(p.lit + o, expire - e.dst_base);
+  if (expire != 0) o += uvput_l(lit, o, expire - e.dst_base);
   const uint32_t hn = 1 + e.ns + (vend - 1) + el + (o - vend);
-  p.lit[0] = (uint8_t)hn;  // byte(headerSize) (record.go:109)
+  lit.put(0, hn & 0xffu);  // byte(headerSize) (record.go:109)
   p.n = 6;
   p.src[0] = 0; p.len[0] = 1; p.off[0] = 0;
   p.src[1] = 1; p.len[1] = e.ns; p.off[1] = 1;
@@ -543,19 +666,23 @@ __device__ void prog_record(const EncDev& e, uint64_t i, bool mdrop, Prog& p) {
 }
 
 // HintRecord.Encode (hint.go:32-48): ns | uvarint(len(key)) | key | uvarint fid | off | size
-__device__ void prog_hint(const EncDev& e, uint64_t i, uint64_t off, uint64_t size, Prog& p) {
+template <class LIT>
+__device__ void prog_hint(const EncDev& e, uint64_t i, uint64_t off, uint64_t size, Prog& p, const LIT& lit) {
   const bcw_record_table& t = e.t;
   const uint64_t klen = t.key_len[i];
-  uint32_t o = uvput(p.lit, klen);
+  uint32_t o = uvput_l(lit, 0, klen);
   const uint32_t k1 = o;
-  o += uvput(p.lit + o, e.fid);
-  o += uvput(p.lit + o, off);
-  o += uvput(p.lit + o, size);
+  o += uvput_l(lit, o, e.fid);
+  o += uvput_l(lit, o, off);
+  o += uvput_l(lit, o, size);
   p.n = 4;
   p.src[0] = 1; p.len[0] = e.ns; p.off[0] = 1;
   p.src[1] = 0; p.len[1] = k1; p.off[1] = 0;
   p.src[2] = 1; p.len[2] = (uint32_t)klen; p.off[2] = t.hdr_size[i];
   p.src[3] = 0; p.len[3] = o - k1; p.off[3] = k1;
+  p.src[4] = p.src[5] = 0;
+  p.len[4] = p.len[5] = 0;
+  p.off[4] = p.off[5] = 0;
 }
 
 enum { PM_DST = 0, PM_HINT_DST = 1, PM_HINT_SRC = 2 };
@@ -615,89 +742,108 @@ struct RecDescW {
 };
 static_assert(sizeof(RecDescW) == 128, "RecDescW layout");
 
-template <int PM>
+template <int PM, class LIT>
 __device__ __forceinline__ void prog_of(const EncDev& e, uint64_t j, uint64_t row, const uint64_t* __restrict__ dst_da,
-                                        const uint64_t* __restrict__ dpos, const uint8_t* __restrict__ mflag, Prog& p) {
-  if (PM == PM_DST) prog_record(e, row, mflag[row] != 0, p);
-  else if (PM == PM_HINT_DST) prog_hint(e, row, dpos[j], dst_da[j + 1] - dst_da[j] - kHdr, p);
-  else prog_hint(e, row, e.t.foff[row] - kHdr, e.t.size[row], p);
+                                        const uint64_t* __restrict__ dpos, const uint8_t* __restrict__ mflag, Prog& p,
+                                        const LIT& lit) {
+  if (PM == PM_DST) prog_record(e, row, mflag[row] != 0, p, lit);
+  else if (PM == PM_HINT_DST) prog_hint(e, row, dpos[j], dst_da[j + 1] - dst_da[j] - kHdr, p, lit);
+  else prog_hint(e, row, e.t.foff[row] - kHdr, e.t.size[row], p, lit);
 }
 
+// One thread per dense record. Byte work happens in LDS (a thread's bytes dword-interleaved with its
+// neighbours', LitLds): the program's literals, the first 128 bytes of the source payload (staged with
+// 16 B loads) and the descriptor under construction, which then leaves as 8 x 16 B stores.
 template <int PM>
 __global__ __launch_bounds__(256) void k_recdesc_w(EncDev e, const uint64_t* __restrict__ emisc,
                                                     const uint32_t* __restrict__ dsrc, const uint64_t* __restrict__ dst_da,
                                                     const uint64_t* __restrict__ dpos, const uint8_t* __restrict__ mflag,
                                                     const uint32_t* __restrict__ ops, RecDescW* __restrict__ rd) {
   __shared__ uint32_t t0[256];
+  __shared__ uint32_t s_src[32 * 256];
+  __shared__ uint32_t s_desc[32 * 256];
+  __shared__ uint32_t s_plit[12 * 256];
+  const uint32_t t = threadIdx.x;
   if (PM == PM_DST) {
-    uint32_t c = threadIdx.x;
+    uint32_t c = t;
     for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
-    t0[threadIdx.x] = c;
-    __syncthreads();
+    t0[t] = c;
   }
-  const uint64_t j = blockIdx.x * 256ull + threadIdx.x;
+  __syncthreads();
+  const uint64_t j = blockIdx.x * 256ull + t;
   if (j >= emisc[X_NDENSE]) return;
+  const LitLds plit{reinterpret_cast<uint8_t*>(s_plit), t};
+  const LitLds sl{reinterpret_cast<uint8_t*>(s_src), t};
+  const LitLds dl{reinterpret_cast<uint8_t*>(s_desc), t};
   const uint64_t row = dsrc[j];
   Prog p;
-  prog_of<PM>(e, j, row, dst_da, dpos, mflag, p);
+  prog_of<PM>(e, j, row, dst_da, dpos, mflag, p, plit);
   const SrcRec sr = src_rec(e.t, e.frags, row);
   const Frag F0 = e.frags[sr.f0];
-  RecDescW d;
-  d.d0 = frag_file(F0, e.start_off);
-  d.l0 = F0.len;
-  d.f0 = sr.f0;
-  d.f1 = sr.f1;
+  const uint64_t d0 = frag_file(F0, e.start_off);
+  const uint32_t l0 = F0.len;
   bool reg = true;
   for (uint32_t f = sr.f0 + 1; f <= sr.f1 && reg; ++f) {
     const Frag F = e.frags[f];
     reg = F.blk == F0.blk + (f - sr.f0) && F.start == kHdr && (f == sr.f1 || F.len == kM);
   }
-  d.regular = reg ? 1 : 0;
-  // the source range: the longest source piece (none: everything is prefix)
-  uint32_t m = p.n, ml = 0;
-  for (uint32_t q = 0; q < p.n; ++q)
-    if (p.src[q] && p.len[q] > ml) { m = q; ml = p.len[q]; }
-  uint32_t npre = 0, nsuf = 0;
-  for (uint32_t q = 0; q < p.n; ++q) {
-    if (q < m) npre += p.len[q];
-    else if (q > m) nsuf += p.len[q];
-  }
-  d.general = npre + nsuf > (uint32_t)kWLit ? 1 : 0;
-  d.npre = (uint8_t)(d.general ? 0 : npre);
-  d.nsuf = (uint8_t)(d.general ? 0 : nsuf);
-  d.mid_off = m < p.n ? (uint32_t)p.off[m] : 0u;
-  d.mid_len = ml;
+  // the source payload's first bytes (those of its first fragment) -> LDS
+  const uint32_t nst = l0 < 128u ? l0 : 128u;
+  if (d0 + 128 <= e.src_len) {
 #pragma unroll
-  for (int b = 0; b < kWLit; ++b) d.lit[b] = 0;
-  if (!d.general) {
-    uint32_t o = 0;
-    for (uint32_t q = 0; q < p.n; ++q) {
-      if (q == m) continue;
-      for (uint32_t b = 0; b < p.len[q]; ++b) {
-        uint8_t v;
-        if (!p.src[q]) {
-          v = p.lit[p.off[q] + b];
-        } else {
-          const uint64_t z = p.off[q] + b;
-          if (reg) { uint64_t run; v = e.seg[src_at(d.d0, d.l0, e.start_off, z, run)]; }
-          else v = src_byte(e.seg, e.frags, e.start_off, sr, z);
-        }
-        d.lit[o++] = v;
-      }
+    for (int k = 0; k < 8; ++k) {
+      uint4 v;
+      __builtin_memcpy(&v, e.seg + d0 + 16 * k, 16);
+      s_src[(4 * k + 0) * 256 + t] = v.x;
+      s_src[(4 * k + 1) * 256 + t] = v.y;
+      s_src[(4 * k + 2) * 256 + t] = v.z;
+      s_src[(4 * k + 3) * 256 + t] = v.w;
+    }
+  } else {
+    for (uint32_t k = 0; k < nst; ++k) sl.put(k, e.seg[d0 + k]);
+  }
+  auto srcb = [&](uint64_t z) -> uint32_t {
+    if (z < nst) return sl.get((uint32_t)z);
+    if (reg) {
+      uint64_t run;
+      return e.seg[src_at(d0, l0, e.start_off, z, run)];
+    }
+    return src_byte(e.seg, e.frags, e.start_off, sr, z);
+  };
+  // the source range: the longest source piece (none: everything is prefix)
+  uint32_t m = 6, ml = 0;
+  uint64_t moff = 0;
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    if ((uint32_t)q < p.n && p.src[q] && p.len[q] > ml) { m = q; ml = p.len[q]; moff = p.off[q]; }
+  uint32_t npre = 0, nsuf = 0;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    if ((uint32_t)q >= p.n) continue;
+    if ((uint32_t)q < m) npre += p.len[q];
+    else if ((uint32_t)q > m) nsuf += p.len[q];
+  }
+  const bool general = npre + nsuf > (uint32_t)kWLit;
+#pragma unroll
+  for (int k = 8; k < 32; ++k) s_desc[k * 256 + t] = 0;  // literal bytes (and rcrc)
+  if (!general) {
+    uint32_t o = 32;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      if ((uint32_t)q >= p.n || (uint32_t)q == m) continue;
+      const bool sq = p.src[q] != 0;
+      const uint64_t oq = p.off[q];
+      for (uint32_t b = 0; b < p.len[q]; ++b) dl.put(o++, sq ? srcb(oq + b) : plit.get((uint32_t)(oq + b)));
     }
   }
-  d.rcrc = 0;
-  if (PM == PM_DST && !d.general && nsuf == 0 && m < p.n && (uint64_t)d.mid_off + ml == e.t.size[row]) {
+  uint32_t regular = reg ? 1u : 0u, rcrc = 0;
+  if (PM == PM_DST && !general && nsuf == 0 && m < 6 && moff + ml == e.t.size[row]) {
     // R(pre) ^ R(src[0, h)): both header strings right-aligned to hl bytes, XOR-ed, one CRC pass
-    const uint32_t h = d.mid_off, hl = npre > h ? npre : h;
+    const uint32_t h = (uint32_t)moff, hl = npre > h ? npre : h;
     uint32_t x = 0;
     for (uint32_t b = 0; b < hl; ++b) {
-      uint32_t z = b + npre >= hl ? d.lit[b + npre - hl] : 0u;
-      if (b + h >= hl) {
-        const uint64_t zz = b + h - hl;
-        uint64_t run;
-        z ^= reg ? e.seg[src_at(d.d0, d.l0, e.start_off, zz, run)] : src_byte(e.seg, e.frags, e.start_off, sr, zz);
-      }
+      uint32_t z = b + npre >= hl ? dl.get(32 + b + npre - hl) : 0u;
+      if (b + h >= hl) z ^= srcb(b + h - hl);
       x = (x >> 8) ^ t0[(x ^ z) & 0xffu];
     }
     const uint32_t* p2 = ops + kOpPow2 * 128;
@@ -706,13 +852,23 @@ __global__ __launch_bounds__(256) void k_recdesc_w(EncDev e, const uint64_t* __r
       const Frag F = e.frags[f];
       cs = shift_by(p2, cs, F.len) ^ F.chk;
     }
-    d.rcrc = shift_by(p2, x, ml) ^ cs;
-    d.regular |= 2;
+    rcrc = shift_by(p2, x, ml) ^ cs;
+    regular |= 2u;
   }
+  s_desc[0 * 256 + t] = (uint32_t)d0;
+  s_desc[1 * 256 + t] = (uint32_t)(d0 >> 32);
+  s_desc[2 * 256 + t] = l0;
+  s_desc[3 * 256 + t] = sr.f0;
+  s_desc[4 * 256 + t] = sr.f1;
+  s_desc[5 * 256 + t] = m < 6 ? (uint32_t)moff : 0u;
+  s_desc[6 * 256 + t] = ml;
+  s_desc[7 * 256 + t] = (general ? 0u : npre) | ((general ? 0u : nsuf) << 8) | (regular << 16) | ((general ? 1u : 0u) << 24);
+  s_desc[31 * 256 + t] = rcrc;
   uint4* dst = reinterpret_cast<uint4*>(rd + j);
-  const uint4* s = reinterpret_cast<const uint4*>(&d);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) dst[k] = s[k];
+  for (int k = 0; k < 8; ++k)
+    dst[k] = make_uint4(s_desc[(4 * k) * 256 + t], s_desc[(4 * k + 1) * 256 + t], s_desc[(4 * k + 2) * 256 + t],
+                        s_desc[(4 * k + 3) * 256 + t]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1233,7 +1389,9 @@ __global__ __launch_bounds__(256) void k_write_general(WArgs WA, uint32_t li, co
   const EncDev& e = WA.e;
   const uint64_t row = dsrc[j];
   Prog p;
-  prog_of<PM>(e, j, row, dst_da, dpos, mflag, p);
+  uint8_t plit[48];
+  const LitLocal lit{plit};
+  prog_of<PM>(e, j, row, dst_da, dpos, mflag, p, lit);
   const SrcRec sr = src_rec(e.t, e.frags, row);
   const uint64_t P = A.fpos[j];
   const uint64_t len = A.da[j + 1] - A.da[j] - kHdr;
@@ -1255,7 +1413,7 @@ __global__ __launch_bounds__(256) void k_write_general(WArgs WA, uint32_t li, co
     for (uint64_t i = 0; i < flen; ++i, ++z) {
       while (z >= qb + p.len[q]) { qb += p.len[q]; ++q; }
       const uint32_t by = p.src[q] ? src_byte(e.seg, e.frags, e.start_off, sr, p.off[q] + (z - qb))
-                                   : p.lit[p.off[q] + (z - qb)];
+                                   : plit[p.off[q] + (z - qb)];
       A.out[ds + i - A.pos] = (uint8_t)by;
       crc = (crc >> 8) ^ t0[(crc ^ by) & 0xffu];
     }
@@ -1590,7 +1748,10 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
   auto layout = [&](int lay, const uint64_t* da, uint64_t pos) {
     const int kid = lay == 1 ? K_ENC_EVENTS_HINT : K_ENC_EVENTS;
     pr.begin(kid, st, ev0);
-    k_events<<<1, kEvThreads, 0, st>>>(da, s.emisc, lay, pos - 40, evs, s.evb);
+    const uint32_t nwin = (uint32_t)(L.rows / kEvWin + 1);
+    k_ev_win<<<nwin, 1024, 0, st>>>(da, s.emisc, lay, pos - 40, s.evt, s.hnl);
+    k_ev_walk<<<1, 64, 0, st>>>(s.emisc, lay, pos - 40, s.evt, s.evw, evs);
+    k_ev_emit<<<(nwin + 63) / 64, 64, 0, st>>>(da, s.emisc, s.evw, s.hnl, evs, s.evb);
     k_ev_fix<<<1, 1024, 0, st>>>(da, s.emisc, lay, evs);
     pr.end(kid, st, ev0);
   };

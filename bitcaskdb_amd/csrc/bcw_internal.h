@@ -133,7 +133,10 @@ struct EncScratch {
   uint64_t* hpos = nullptr;   // [rows] hint record offsets (compaction)
   void* tiles = nullptr;      // scan tile sums
   void* ev = nullptr;         // [rows+2] layout events
-  uint32_t* evb = nullptr;    // [rows/win+2] governing event per k_events window
+  uint32_t* evb = nullptr;    // [rows/win+2] governing event per event-scan window
+  uint64_t* evt = nullptr;    // [rows/win+2][32768] per-window entry tables (k_ev_win)
+  uint16_t* hnl = nullptr;    // [rows] next event inside the window (k_ev_win)
+  uint32_t* evw = nullptr;    // [rows/win+2][3] window entries (k_ev_walk)
   void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc_w -> k_write), dst WAL
   void* recdesc_h = nullptr;  // [rows] the same for the hint WAL
   uint64_t* emisc = nullptr;  // [64] counters
