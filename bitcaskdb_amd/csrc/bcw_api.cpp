@@ -333,7 +333,7 @@ static void free_scratch(Scratch& s) {
 
 static void free_enc_scratch(EncScratch& e) {
   void* ptrs[] = {e.sz,    e.mflag, e.dsrc, e.da,      e.hda,       e.hsz,  e.dpos,
-                  e.hpos,  e.tiles, e.ev,   e.evb,     e.recdesc,   e.recdesc_h, e.emisc, e.evt,
+                  e.hpos,  e.tiles, e.ev,   e.evb,     e.recdesc,   e.emisc, e.evt,
                   e.hnl,   e.evw};
   for (void* q : ptrs) (void)hipFree(q);
   hipStream_t aux = e.aux;
@@ -644,7 +644,6 @@ static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows) {
             hipMalloc(&e.evt, nwin * 32768 * 8) == hipSuccess && hipMalloc(&e.hnl, r * 2) == hipSuccess &&
             hipMalloc(&e.evw, nwin * 12) == hipSuccess &&
             hipMalloc(&e.recdesc, r * enc_sizeof_recdesc()) == hipSuccess &&
-            hipMalloc(&e.recdesc_h, r * enc_sizeof_recdesc()) == hipSuccess &&
             hipMalloc(&e.emisc, 64 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_enc_scratch(e); return BCW_E_NOMEM; }
   if (!e.aux && (hipStreamCreateWithFlags(&e.aux, hipStreamNonBlocking) != hipSuccess ||

@@ -1637,6 +1637,177 @@ __global__ __launch_bounds__(kCT) void k_wcopy(WArgs A) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// k_hwrite: the hint WAL (HintRecord.Encode hint.go:32-48 appended with Wal.WriteRecord). Hint records
+// are short (NsSize + key + a few varints), so one lane generates one record: its payload bytes in
+// order (namespace and key streamed from the source payload in 16 B loads, varints computed), folded
+// into the fragment's CRC-32C (bytewise table). Fragments follow the writer's rule (data up to the
+// block end, continuation headers at block starts); a header is written once its fragment's CRC is
+// known. The 64 records of a wave are contiguous in the output: they are assembled in a staging
+// area in LDS (with the zero pads before block-start records) and leave as aligned 16 B stores; a wave
+// whose records span more than the staging area writes its bytes straight to HBM instead.
+constexpr int kHStage = 12288;  // staging bytes per wave
+
+struct HintOut {
+  uint8_t* dst;        // where file offset `org` lives (LDS staging area or the output in HBM)
+  uint64_t org;
+  const uint32_t* t0;  // byte table (LDS)
+  uint64_t a = 0;      // file offset of the next data byte
+  uint64_t fend = 0;   // end of the current fragment's data
+  uint64_t hp = 0;     // its header
+  uint64_t rem = 0;    // payload bytes not yet placed in a fragment
+  uint32_t fl = 0, type = 0, crc = 0;
+  bool first = true;
+  __device__ __forceinline__ void open(uint64_t h) {  // a fragment whose header is at file offset h
+    hp = h;
+    const uint64_t be = h + kL - (h - 40) % kL, ds = h + kHdr;
+    const uint64_t f = rem < be - ds ? rem : be - ds;
+    fl = (uint32_t)f;
+    type = first ? (f == rem ? BCW_RECORD_FULL : BCW_RECORD_FIRST) : (f == rem ? BCW_RECORD_LAST : BCW_RECORD_MIDDLE);
+    first = false;
+    rem -= f;
+    a = ds;
+    fend = ds + f;
+    crc = 0xffffffffu;
+  }
+  __device__ __forceinline__ void close() {  // header of the current fragment
+    const uint32_t c = ~crc;
+    const uint32_t masked = ((c >> 15) | (c << 17)) + 0xa282ead8u;  // ComputeCRC32 (utils.go:24-29)
+    uint8_t* h = dst + (hp - org);
+    h[0] = (uint8_t)masked;
+    h[1] = (uint8_t)(masked >> 8);
+    h[2] = (uint8_t)(masked >> 16);
+    h[3] = (uint8_t)(masked >> 24);
+    h[4] = (uint8_t)fl;
+    h[5] = (uint8_t)(fl >> 8);
+    h[6] = (uint8_t)type;
+  }
+  __device__ __forceinline__ void put(uint32_t b) {
+    while (a == fend) {  // the fragment is full (or zero-length): the next one starts at the block end
+      close();
+      open(fend);
+    }
+    crc = (crc >> 8) ^ t0[(crc ^ b) & 0xffu];
+    dst[a - org] = (uint8_t)b;
+    ++a;
+  }
+  __device__ __forceinline__ void uv(uint64_t v) {
+    while (v >= 0x80) { put((uint32_t)(v | 0x80) & 0xffu); v >>= 7; }
+    put((uint32_t)v);
+  }
+};
+
+template <int PM>
+__global__ __launch_bounds__(256) void k_hwrite(WArgs A, uint32_t li, const uint32_t* __restrict__ dsrc,
+                                                 const uint64_t* __restrict__ dst_da, const uint64_t* __restrict__ dpos) {
+  __shared__ uint32_t t0[256];
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[4][kHStage];
+  {
+    uint32_t c = threadIdx.x;
+    for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    t0[threadIdx.x] = c;
+  }
+  __syncthreads();
+  const WLay& W = li ? A.w[1] : A.w[0];
+  if (!lay_ok(A.emisc, W)) return;
+  const uint64_t N = A.emisc[X_NDENSE];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t j0 = blockIdx.x * 256ull + wave * 64ull, j = j0 + lane;
+  if (j0 >= N) return;
+  const bool act = j < N;
+  const EncDev& e = A.e;
+  const uint64_t row = act ? dsrc[j] : 0;
+  uint64_t P = 0, len = 0, prev = 0;
+  if (act) {
+    P = W.fpos[j];
+    len = W.da[j + 1] - W.da[j] - kHdr;
+    // the record's region starts after the previous record (the zero pad before a block start, wal.go:509-512)
+    prev = P;
+    if ((P - 40) % kL == 0) prev = j == 0 ? W.pos : rec_end(W.fpos[j - 1], W.da[j] - W.da[j - 1] - kHdr);
+  }
+  const uint64_t end = act ? rec_end(P, len) : 0;
+  // the wave's output span [lo, hi): its records are consecutive
+  const uint64_t lo = uni64(prev), hi = __shfl(end, (int)(N - j0 < 64 ? N - j0 - 1 : 63), 64);
+  uint8_t* const out = W.out - W.pos;  // file offset -> memory
+  // staging offset of file offset f: f - lo + (address of lo mod 16), so output units are aligned in LDS
+  const uint64_t ma = (uint64_t)(uintptr_t)(out + lo), me = ma + (hi - lo);
+  const bool staged = hi - lo + 16 <= (uint64_t)kHStage;
+  uint8_t* stage = s_stage[wave];
+  if (act) {
+    uint64_t off, size;
+    if (PM == PM_HINT_DST) {
+      off = dpos[j];
+      size = dst_da[j + 1] - dst_da[j] - kHdr;
+    } else {
+      off = e.t.foff[row] - kHdr;
+      size = e.t.size[row];
+    }
+    const uint64_t klen = e.t.key_len[row], hdr = e.t.hdr_size[row];
+    const SrcRec sr = src_rec(e.t, e.frags, row);
+    const Frag F0 = e.frags[sr.f0];
+    const uint64_t d0 = frag_file(F0, e.start_off);
+    const uint32_t l0 = F0.len;
+    bool reg = true;
+    for (uint32_t f = sr.f0 + 1; f <= sr.f1 && reg; ++f) {
+      const Frag F = e.frags[f];
+      reg = F.blk == F0.blk + (f - sr.f0) && F.start == kHdr && (f == sr.f1 || F.len == kM);
+    }
+    HintOut o;
+    o.dst = staged ? stage : out;
+    o.org = staged ? lo - (ma & 15u) : 0;
+    o.t0 = t0;
+    for (uint64_t b = prev; b < P; ++b) o.dst[b - o.org] = 0;
+    o.rem = len;
+    o.open(P);
+    // source payload bytes [z, z + n), in 16 B loads within each source run
+    auto src = [&](uint64_t z, uint64_t n) {
+      while (n > 0) {
+        uint64_t run = 0, S = 0;
+        if (reg) S = src_at(d0, l0, e.start_off, z, run);
+        const uint32_t c = (uint32_t)(n < 16 ? n : 16);
+        if (reg && run >= c && S + 16 <= e.src_len) {
+          uint4 v;
+          __builtin_memcpy(&v, e.seg + S, 16);
+          const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (uint32_t k = 0; k < 16; ++k)
+            if (k < c) o.put((w4[k >> 2] >> (8 * (k & 3))) & 0xffu);
+          z += c;
+          n -= c;
+        } else {
+          o.put(reg ? e.seg[S] : src_byte(e.seg, e.frags, e.start_off, sr, z));
+          ++z;
+          --n;
+        }
+      }
+    };
+    src(1, e.ns);  // namespace
+    o.uv(klen);
+    src(hdr, klen);  // key
+    o.uv(e.fid);
+    o.uv(off);
+    o.uv(size);
+    o.close();
+  }
+  if (!staged) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the staged span -> HBM: 16 B units aligned to the output memory, partial units at the ends bytewise
+  const uint64_t u0 = ma >> 4, nu = ((me - 1) >> 4) - u0 + 1;
+  for (uint64_t k = lane; k < nu; k += 64) {
+    const uint64_t ua = (u0 + k) << 4;
+    uint8_t* d = reinterpret_cast<uint8_t*>((uintptr_t)ua);
+    const uint8_t* sp = stage + 16 * k;  // unit k of the staging area
+    if (ua >= ma && ua + 16 <= me) {
+      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(sp);
+    } else {
+      const uint64_t b0 = ua < ma ? ma - ua : 0, b1 = ua + 16 > me ? me - ua : 16;
+      for (uint64_t b = b0; b < b1; ++b) d[b] = sp[b];
+    }
+  }
+}
+
 // hint payload sizes of the written records of a compaction (hint.go:32-48 with off/size of the
 // dst record, compaction.go:314-320)
 __global__ __launch_bounds__(256) void k_hint_sizes(EncDev e, const uint64_t* __restrict__ emisc,
@@ -1732,14 +1903,11 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
   W.abl = (uint32_t)abl_env;
   const uint32_t rgrid = (uint32_t)((rows + 255) / 256) + 1;
   RecDescW* wd = static_cast<RecDescW*>(s.recdesc);
-  RecDescW* wh = static_cast<RecDescW*>(s.recdesc_h);
   // persistent write grid: as many workgroups per CU as are resident
   auto wgrid = [&](int g) {
-    static int wpc[17] = {};
-    int& n = wpc[g];
+    static int n = 0;
     if (n == 0) {
-      hipError_t rc = g == 8 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_write<8>, kWT, 0)
-                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_write<16>, kWT, 0);
+      const hipError_t rc = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_write<16>, kWT, 0);
       if (rc != hipSuccess || n < 1) n = 2;
     }
     const uint64_t groups = (uint64_t)kWT / g;
@@ -1756,15 +1924,15 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     pr.end(kid, st, ev0);
   };
   if (compact) {
-    // stream st: the layouts (two serial one-workgroup event scans) and the writers; stream aux: the
-    // payload descriptors of the dst records (after the dense scan) and of the hint records (after the
-    // dst offsets), built while the event scans run
+    // stream st: the layouts and the writers; stream aux: the dst records' payload descriptors (after the
+    // dense scan), built while the layouts run
     pr.begin(K_ENC_SCAN, st, ev0);
     scan(s.sz, 1, 0, s.da);
     pr.end(K_ENC_SCAN, st, ev0);
     (void)hipEventRecord(s.ev_scan, st);
     (void)hipStreamWaitEvent(s.aux, s.ev_scan, 0);
     k_recdesc_w<PM_DST><<<rgrid, 256, 0, s.aux>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, L.crc_ops, wd);
+    (void)hipEventRecord(s.ev_desc, s.aux);
     layout(0, s.da, L.p.wal_pos);
     k_recoff<<<rgrid, 256, 0, st>>>(s.da, s.dsrc, s.emisc, 0, evs, s.evb, s.dpos, L.out.rec_off);
     // the hint WAL's layout needs the dst offsets (its records carry them)
@@ -1772,33 +1940,22 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     k_hint_sizes<<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.hsz);
     scan(s.hsz, 0, 1, s.hda);
     pr.end(K_ENC_HINT_LAYOUT, st, ev0);
-    (void)hipEventRecord(s.ev_hscan, st);
-    (void)hipStreamWaitEvent(s.aux, s.ev_hscan, 0);
-    k_recdesc_w<PM_HINT_DST><<<rgrid, 256, 0, s.aux>>>(e, s.emisc, s.dsrc, s.da, s.dpos, s.mflag, L.crc_ops, wh);
-    (void)hipEventRecord(s.ev_desc, s.aux);
     layout(1, s.hda, L.p.hint_pos);
     k_recoff<<<rgrid, 256, 0, st>>>(s.hda, s.dsrc, s.emisc, 1, evs, s.evb, s.hpos, nullptr);
     (void)hipStreamWaitEvent(st, s.ev_desc, 0);
     W.w[0] = WLay{s.da, s.dpos, wd, L.out.wal, L.p.wal_pos, L.out.wal_cap, 0};
-    W.w[1] = WLay{s.hda, s.hpos, wh, L.out.hint, L.p.hint_pos, L.out.hint_cap, 1};
+    W.w[1] = WLay{s.hda, s.hpos, nullptr, L.out.hint, L.p.hint_pos, L.out.hint_cap, 1};
     W.nlay = 1;
-    WArgs H = W;
-    H.w[0] = W.w[1];
     const int abl = abl_env & 3;
-    static const int hg = [] { const char* v = getenv("BCW_HINT_G"); return v ? atoi(v) : 8; }();
     pr.begin(K_ENC_WRITE, st, ev0);
     // measurement-only ablation (BCW_ENC_ABL: 1 = dst WAL only, 2 = hint WAL only); 0 in the product
     if (abl != 2) {
       k_wcopy<<<(uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, (uint64_t)L.num_cus * 8)), kCT, 0,
                 st>>>(W);
       k_write<16><<<wgrid(16), kWT, 0, st>>>(W);
+      k_write_general<PM_DST><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr, s.mflag);
     }
-    if (abl != 1) {
-      if (hg == 16) k_write<16><<<wgrid(16), kWT, 0, st>>>(H);
-      else k_write<8><<<wgrid(8), kWT, 0, st>>>(H);
-    }
-    k_write_general<PM_DST><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr, s.mflag);
-    k_write_general<PM_HINT_DST><<<rgrid, 256, 0, st>>>(W, 1, s.dsrc, s.da, s.dpos, s.mflag);
+    if (abl != 1) k_hwrite<PM_HINT_DST><<<rgrid, 256, 0, st>>>(W, 1, s.dsrc, s.da, s.dpos);
     pr.end(K_ENC_WRITE, st, ev0);
   } else {
     pr.begin(K_ENC_SCAN, st, ev0);
@@ -1806,13 +1963,11 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     pr.end(K_ENC_SCAN, st, ev0);
     layout(0, s.hda, L.p.hint_pos);
     k_recoff<<<rgrid, 256, 0, st>>>(s.hda, s.dsrc, s.emisc, 0, evs, s.evb, s.hpos, nullptr);
-    W.w[0] = WLay{s.hda, s.hpos, wd, L.out.hint, L.p.hint_pos, L.out.hint_cap, 0};
+    W.w[0] = WLay{s.hda, s.hpos, nullptr, L.out.hint, L.p.hint_pos, L.out.hint_cap, 0};
     W.w[1] = W.w[0];
     W.nlay = 1;
     pr.begin(K_ENC_WRITE, st, ev0);
-    k_recdesc_w<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(e, s.emisc, s.dsrc, nullptr, nullptr, s.mflag, L.crc_ops, wd);
-    k_write<8><<<wgrid(8), kWT, 0, st>>>(W);
-    k_write_general<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr, s.mflag);
+    k_hwrite<PM_HINT_SRC><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr);
     pr.end(K_ENC_WRITE, st, ev0);
   }
   k_enc_finalize<<<1, 1, 0, st>>>(s.emisc, L.p.mode, L.p.wal_pos, L.out.wal_cap, L.p.hint_pos, L.out.hint_cap,

@@ -138,7 +138,6 @@ struct EncScratch {
   uint16_t* hnl = nullptr;    // [rows] next event inside the window (k_ev_win)
   uint32_t* evw = nullptr;    // [rows/win+2][3] window entries (k_ev_walk)
   void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc_w -> k_write), dst WAL
-  void* recdesc_h = nullptr;  // [rows] the same for the hint WAL
   uint64_t* emisc = nullptr;  // [64] counters
   // the payload descriptors are built on an auxiliary stream while the serial layout scans run
   hipStream_t aux = nullptr;
