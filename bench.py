@@ -39,11 +39,132 @@ def parse():
     ap.add_argument("--config", default="B", choices=["B", "C"], help="B: 4 KiB values; C: Zipf 128 B-64 KiB")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the extra legs (all-core / pread CPU baselines, file-to-file end-to-end rates)")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the all-core CPU baseline")
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events bracket every N-th k_crc launch of the timed region")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_k_crc_pmc.json"),
                     help="PMC traffic summary (rocprofv3 --pmc of this command) to report as roofline.traffic")
     return ap.parse_args()
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_all_cores(O, hb, n_rec, seconds, threads):
+    """the restated decode loop on `threads` host threads at once, each over the same segment (ctypes releases
+    the GIL inside the C call); returns (GiB/s, passes, seconds)"""
+    import threading
+    seg_len = int(hb.size)
+    counts = [0] * threads
+    t0 = time.perf_counter()
+    stop = t0 + seconds
+
+    def run(i):
+        while time.perf_counter() < stop:
+            got, ec, _ = O.decode_fast(hb, 40, BASE_TIME, 20, 20)
+            assert got == n_rec and ec == 0
+            counts[i] += 1
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    return seg_len * sum(counts) / 2 ** 30 / dt, sum(counts), dt
+
+
+def cpu_pread_config_a(O, L, seconds):
+    """config A: a 64 MiB 4 KiB-value segment on disk (page cache), decoded with a pread per 32 KiB block as
+    the reference iterator does (wal_iterator.go:55 -> utils.go:32-48), 1 thread"""
+    import tempfile
+    n, r = C.c_uint64(), C.c_uint64()
+    assert L.lib.bcw_synth_segment(64 << 20, 0, 7, 20, 100, 4096, 0, BASE_TIME, None, 0, C.byref(n), C.byref(r)) == 0
+    buf = np.zeros(n.value, dtype=np.uint8)
+    assert L.lib.bcw_synth_segment(64 << 20, 0, 7, 20, 100, 4096, 0, BASE_TIME, C.c_void_p(buf.ctypes.data),
+                                   n.value, C.byref(n), C.byref(r)) == 0
+    with tempfile.NamedTemporaryFile(dir="/tmp", suffix=".wal") as fh:
+        fh.write(buf.tobytes())
+        fh.flush()
+        fd = os.open(fh.name, os.O_RDONLY)
+        try:
+            passes, t = 0, time.perf_counter()
+            while True:
+                got, ec, _ = O.decode_fast_pread(fd, int(n.value), 40, BASE_TIME, 20, 20)
+                assert got == r.value and ec == 0
+                passes += 1
+                if time.perf_counter() - t >= seconds:
+                    break
+            dt = time.perf_counter() - t
+        finally:
+            os.close(fd)
+    return int(n.value) * passes / 2 ** 30 / dt, passes, dt, int(n.value)
+
+
+def end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec, reps=3):
+    """file -> pinned slices -> HBM -> decode, and file -> decode -> re-encode (all kept) -> dst WAL + hint
+    files, through bcw_stage (f3); the files sit in the page cache (written just before)"""
+    import tempfile
+    import torch
+    from bitcaskdb_amd import Stage
+    dev = d_seg.device
+    st = Stage(ctx, 8 << 20, 8)
+    cap = table.capacity
+    keep = torch.ones(cap, dtype=torch.uint8, device=dev)
+    d_wal = torch.empty(seg_len + (seg_len >> 6) + (1 << 20), dtype=torch.uint8, device=dev)
+    d_hint = torch.empty(n_rec * 200 + (1 << 20), dtype=torch.uint8, device=dev)
+    e_res = torch.zeros(C.sizeof(L.EncodeResult), dtype=torch.uint8, device=dev)
+    ep = L.EncodeParams(seg_len, BASE_TIME, 2, 40, 40, 40, L.ENC_COMPACT, 20, 20)
+    out = L.EncodeOut(C.cast(C.c_void_p(d_wal.data_ptr()), L.u8p), d_wal.numel(),
+                      C.cast(C.c_void_p(d_hint.data_ptr()), L.u8p), d_hint.numel(), None, 0)
+    res = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as tmp:
+        src = os.path.join(tmp, "1.wal")
+        host.numpy().tofile(src)
+        fd = os.open(src, os.O_RDONLY)
+        try:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(reps):
+                st.read(fd, 0, seg_len, d_seg.data_ptr(), stream.cuda_stream, threads=4)
+                step()
+                torch.cuda.synchronize()
+            res["decode_file_GiBs"] = round(seg_len / 2 ** 30 / ((time.perf_counter() - t) / reps), 2)
+            t = time.perf_counter()
+            for i in range(reps):
+                st.read(fd, 0, seg_len, d_seg.data_ptr(), stream.cuda_stream, threads=4)
+                step()
+                rc = L.lib.bcw_encode_segment_async(ctx.handle, C.c_void_p(d_seg.data_ptr()), C.byref(ep),
+                                                    C.byref(table), C.c_void_p(d_res.data_ptr()),
+                                                    C.c_void_p(keep.data_ptr()), C.byref(out),
+                                                    C.c_void_p(e_res.data_ptr()))
+                assert rc == 0
+                stream.synchronize()
+                r = L.EncodeResult.from_buffer_copy(bytes(e_res.cpu().numpy()))
+                assert r.err_class == 0 and r.fits and r.n_written == n_rec
+                for name, dbuf, nb in (("2.merge", d_wal, r.wal_need), ("2.tmp", d_hint, r.hint_need)):
+                    ofd = os.open(os.path.join(tmp, f"{i}.{name}"), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+                    try:
+                        st.write(ofd, 40, dbuf.data_ptr(), int(nb), stream.cuda_stream)
+                    finally:
+                        os.close(ofd)
+            res["compaction_file_to_file_GiBs"] = round(seg_len / 2 ** 30 / ((time.perf_counter() - t) / reps), 2)
+        finally:
+            os.close(fd)
+    st.close()
+    res["note"] = ("source and output files in the page cache; pinned 8 MiB slices, 4 pread threads; compaction = "
+                   "read + decode + re-encode + hint rebuild + dst WAL and hint written back")
+    return res
 
 
 def main():
@@ -190,6 +311,11 @@ def main():
                 "pipeline_GBs": round(seg_len / (ms_per_step * 1e-3) / 1e9, 1),
                 "kernel_ms_all": {k: round(v, 4) for k, v in kern.items()}}
 
+    # ---- end-to-end through the host I/O staging (rank 0, N=1) ----
+    extras = {}
+    if world == 1 and not args.no_extras:
+        extras["e2e"] = end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec)
+
     # ---- CPU baseline: restated reference decode loop (oracle/, hardware CRC, 1 thread) ----
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -204,10 +330,21 @@ def main():
             if time.perf_counter() - t >= args.cpu_seconds:
                 break
         dt = time.perf_counter() - t
+        model = cpu_model()
         cpu = {"value": round(seg_len * passes / 2 ** 30 / dt, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
                "sample": f"{passes} full decode passes over the same {seg_len} B config-{args.config} segment "
                          f"(host copy), restated wal_iterator.go Next + RecordFromBytes with SSE4.2 CRC, 1 thread, "
-                         f"{dt:.1f} s, {platform.processor() or platform.machine()}"}
+                         f"{dt:.1f} s, {model}"}
+        if not args.no_extras:
+            thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+            v, p, d = cpu_all_cores(O, hb, n_rec, args.cpu_seconds, thr)
+            extras["cpu_all_cores"] = {"value": round(v, 3), "unit": "GiB/s", "cores": thr, "kind": "port",
+                                       "sample": f"{p} passes over the config-{args.config} segment on {thr} "
+                                                 f"threads in {d:.1f} s, {model}"}
+            v, p, d, a_len = cpu_pread_config_a(O, L, min(args.cpu_seconds, 5.0))
+            extras["cpu_config_a_pread"] = {"value": round(v, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                                            "sample": f"config A: {p} passes over a {a_len} B segment file (page "
+                                                      f"cache), one pread per 32 KiB block, {d:.1f} s, {model}"}
 
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -222,6 +359,7 @@ def main():
         "pcie_inclusive_GiBs": round(pcie, 2) if pcie else None,
         "event_ms_per_step": round(ev_ms / args.steps, 4),
     }
+    line.update(extras)
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -604,15 +604,15 @@ __device__ __forceinline__ void load_window(const uint8_t* __restrict__ seg, uin
 // last-window fix: keep bytes < hi (hi in [109,124]), put J at [hi, hi+4), zero the rest
 // (touches words 27..31 only); branch-free per word
 __device__ __forceinline__ void fix_last(uint32_t (&w)[32], uint32_t hi, uint32_t J) {
+  const uint32_t kh = hi >> 2, sh = 8u * (hi & 3u);
+  const uint64_t jj = (uint64_t)J << sh;
+  const uint32_t jlo = (uint32_t)jj, jhi = (uint32_t)(jj >> 32);
+  const uint32_t keep = (uint32_t)((1ull << sh) - 1ull);  // bytes of word kh below hi
 #pragma unroll
   for (int k = 27; k < 32; ++k) {
-    const int t = (int)hi - 4 * k;                       // byte index of hi relative to the word
-    const int tk = t < 0 ? 0 : (t > 4 ? 4 : t);           // bytes kept
-    const uint32_t keep = (uint32_t)((1ull << (8 * tk)) - 1ull);
-    const uint64_t jw = (uint64_t)J << 32;                // J at byte 4 of a 64-bit lane
-    const int sh = 32 - 8 * t;                            // J byte 0 lands at byte t
-    const uint32_t jp = (t > -4 && t < 4) ? (uint32_t)(sh >= 0 ? (jw >> sh) : (jw << -sh)) : 0u;
-    w[k] = (w[k] & keep) | jp;
+    const uint32_t uk = (uint32_t)k;
+    const uint32_t v = uk < kh ? w[k] : (uk == kh ? ((w[k] & keep) | jlo) : (uk == kh + 1u ? jhi : 0u));
+    w[k] = v;
   }
 }
 
@@ -859,12 +859,12 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     if ((ABL & 32) && !(ABL & 64)) quad_windows_transpose(w, lane);
     if (d.active()) {
       if (d.cfb() == 0u) {  // first window: zero the bytes before the data (the previous header / fragment)
-        const int32_t lo8 = 8 * (int32_t)d.lo();
+        const uint32_t lo = d.lo(), kf = lo >> 2;
+        const uint32_t pm = 0xffffffffu << (8u * (lo & 3u));  // the word holding the first data byte
 #pragma unroll
         for (int k2 = 0; k2 < 32; ++k2) {
-          int32_t sh = lo8 - 32 * k2;
-          sh = sh < 0 ? 0 : (sh > 32 ? 32 : sh);
-          w[k2] &= (uint32_t)(0xffffffffffffffffull << sh);
+          const uint32_t m = (uint32_t)k2 < kf ? 0u : ((uint32_t)k2 == kf ? pm : 0xffffffffu);
+          w[k2] &= m;
         }
       }
       if (d.last()) fix_last(w, d.hi(), d.J);
@@ -902,9 +902,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   // the chain: advance the ring, take wy into wx, issue pass p+128's
   // loads, then describe pass p+192 -- descriptor work is off the load-to-load critical path.
   // The first three iterations only fill the pipeline (p < 0).
+  if (ABL & 16) tq = __builtin_amdgcn_s_memtime();
   uint32_t wx[32], wy[32];
   BodyDesc dx{}, dy{}, dz{};
-  if (ABL & 16) tq = __builtin_amdgcn_s_memtime();
   for (int64_t p = -192;;) {
     if (p >= 0) {
       stamp(t_issue);

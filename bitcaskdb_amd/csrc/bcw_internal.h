@@ -61,8 +61,10 @@ constexpr int kLdsSlice = 2 * 256 * 32;
 constexpr int kLdsFwd = 8 * 16 * 64;
 constexpr int kLdsOps = 2 * 8 * 16;
 constexpr int kLdsImage = kLdsSlice + kLdsFwd + kLdsOps;
-constexpr int kCrcWaves = 12;  // waves per k_crc workgroup (one workgroup per CU; 12 x 8 KiB of window
-                               // loads in flight per CU keeps an XCD's in-flight lines within its 4 MiB L2)
+#ifndef BCW_CRC_WAVES
+#define BCW_CRC_WAVES 12
+#endif
+constexpr int kCrcWaves = BCW_CRC_WAVES;  // waves per k_crc workgroup (one workgroup per CU)
 constexpr int kCrcThreads = kCrcWaves * 64;
 
 struct Scratch {

@@ -3,12 +3,14 @@
  * the parity checker for bitcaskdb_amd/ (see bcw_oracle.h for the reference map and pinning).
  * Every function cites the reference file:line it restates (paths relative to /root/reference).
  */
+#define _GNU_SOURCE  /* pread */
 #include "bcw_oracle.h"
 
 #include <nmmintrin.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 /* ------------------------------------------------------------------------------------------ */
 /* CRC-32C (Castagnoli), reflected poly 0x82F63B78 == Go crc32.MakeTable(crc32.Castagnoli)      */
@@ -518,8 +520,8 @@ void oc_decode_free(oc_decode* d) {
 /* CPU baseline: the same Next() + RecordFromBytes loop with hardware CRC and no per-record      */
 /* allocation (an upper bound on the Go path's speed).                             */
 /* ------------------------------------------------------------------------------------------ */
-uint64_t oc_decode_fast(const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
-                        uint32_t ns_size, uint32_t etag_size, int32_t* err_class, uint64_t* checksum) {
+static uint64_t decode_fast_impl(const uint8_t* seg, int fd, uint64_t len, uint32_t start_off, uint64_t base_time,
+                                 uint32_t ns_size, uint32_t etag_size, int32_t* err_class, uint64_t* checksum) {
   int64_t file_off = start_off, buf_off = 0, buf_size = 0;
   uint64_t acc_len = 0, off = 0, n = 0, sum = 0;
   static __thread uint8_t* acc = NULL;
@@ -533,7 +535,16 @@ uint64_t oc_decode_fast(const uint8_t* seg, uint64_t len, uint32_t start_off, ui
       buf_size = rem < (int64_t)OC_BLOCK_SIZE ? rem : (int64_t)OC_BLOCK_SIZE;
       if (buf_size <= 0) { if (buf_size < 0) *err_class = OC_ERR_PANIC; break; }
       if (buf_size < (int64_t)OC_HEADER_SIZE) { *err_class = OC_ERR_PANIC; break; }
-      memcpy(blk, seg + file_off, (size_t)buf_size);
+      if (seg) {
+        memcpy(blk, seg + file_off, (size_t)buf_size);
+      } else { /* PreadFull (utils.go:32-48) */
+        int64_t got = 0;
+        while (got < buf_size) {
+          ssize_t r = pread(fd, blk + got, (size_t)(buf_size - got), (off_t)(file_off + got));
+          if (r <= 0) { *err_class = OC_ERR_PANIC; return n; }
+          got += r;
+        }
+      }
       buf_off = 0;
     }
     const uint8_t* header = blk + buf_off;
@@ -566,6 +577,16 @@ uint64_t oc_decode_fast(const uint8_t* seg, uint64_t len, uint32_t start_off, ui
   }
   *checksum = sum;
   return n;
+}
+
+uint64_t oc_decode_fast(const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                        uint32_t ns_size, uint32_t etag_size, int32_t* err_class, uint64_t* checksum) {
+  return decode_fast_impl(seg, -1, len, start_off, base_time, ns_size, etag_size, err_class, checksum);
+}
+
+uint64_t oc_decode_fast_pread(int fd, uint64_t len, uint32_t start_off, uint64_t base_time, uint32_t ns_size,
+                              uint32_t etag_size, int32_t* err_class, uint64_t* checksum) {
+  return decode_fast_impl(NULL, fd, len, start_off, base_time, ns_size, etag_size, err_class, checksum);
 }
 
 /* ------------------------------------------------------------------------------------------ */

@@ -135,6 +135,9 @@ void oc_decode_free(oc_decode* d);
  * returns records delivered; *err_class gets OC_ERR_*. */
 uint64_t oc_decode_fast(const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
                         uint32_t ns_size, uint32_t etag_size, int32_t* err_class, uint64_t* checksum);
+/* the same loop reading each 32 KiB block from a file descriptor with pread (wal_iterator.go:55, PreadFull) */
+uint64_t oc_decode_fast_pread(int fd, uint64_t len, uint32_t start_off, uint64_t base_time, uint32_t ns_size,
+                              uint32_t etag_size, int32_t* err_class, uint64_t* checksum);
 
 /* ---- compaction re-encode (compactOneWal) and hint rebuild (NewHintByWal) ----
  * err_class: OC_ENC_OK, OC_ENC_SRC (the source iteration failed at row *err_rec, or a fragment error when

@@ -102,6 +102,9 @@ lib.oc_index_put_segment.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64,
 lib.oc_compact_filter.restype = C.c_uint64
 lib.oc_compact_filter.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, vp,
                                   C.c_uint64]
+lib.oc_decode_fast_pread.restype = C.c_uint64
+lib.oc_decode_fast_pread.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                                     C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
 lib.oc_read_record.restype = C.c_int
 lib.oc_read_record.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, vp]
 lib.oc_record_parse.restype = None
@@ -258,6 +261,13 @@ def decode_fast(seg, start_off, base_time, ns_size, etag_size):
     ec = C.c_int32()
     cs = C.c_uint64()
     n = lib.oc_decode_fast(_ptr(seg), seg.size, start_off, base_time, ns_size, etag_size, C.byref(ec), C.byref(cs))
+    return int(n), int(ec.value), int(cs.value)
+
+
+def decode_fast_pread(fd: int, length: int, start_off, base_time, ns_size, etag_size):
+    ec = C.c_int32()
+    cs = C.c_uint64()
+    n = lib.oc_decode_fast_pread(fd, length, start_off, base_time, ns_size, etag_size, C.byref(ec), C.byref(cs))
     return int(n), int(ec.value), int(cs.value)
 
 
