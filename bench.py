@@ -118,7 +118,7 @@ def end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec, 
     import torch
     from bitcaskdb_amd import Stage
     dev = d_seg.device
-    st = Stage(ctx, 8 << 20, 8)
+    st = Stage(ctx, 8 << 20, 16)
     cap = table.capacity
     keep = torch.ones(cap, dtype=torch.uint8, device=dev)
     d_wal = torch.empty(seg_len + (seg_len >> 6) + (1 << 20), dtype=torch.uint8, device=dev)
@@ -136,13 +136,13 @@ def end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec, 
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(reps):
-                st.read(fd, 0, seg_len, d_seg.data_ptr(), stream.cuda_stream, threads=4)
+                st.read(fd, 0, seg_len, d_seg.data_ptr(), stream.cuda_stream, threads=8)
                 step()
                 torch.cuda.synchronize()
             res["decode_file_GiBs"] = round(seg_len / 2 ** 30 / ((time.perf_counter() - t) / reps), 2)
             t = time.perf_counter()
             for i in range(reps):
-                st.read(fd, 0, seg_len, d_seg.data_ptr(), stream.cuda_stream, threads=4)
+                st.read(fd, 0, seg_len, d_seg.data_ptr(), stream.cuda_stream, threads=8)
                 step()
                 rc = L.lib.bcw_encode_segment_async(ctx.handle, C.c_void_p(d_seg.data_ptr()), C.byref(ep),
                                                     C.byref(table), C.c_void_p(d_res.data_ptr()),
@@ -155,14 +155,14 @@ def end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec, 
                 for name, dbuf, nb in (("2.merge", d_wal, r.wal_need), ("2.tmp", d_hint, r.hint_need)):
                     ofd = os.open(os.path.join(tmp, f"{i}.{name}"), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
                     try:
-                        st.write(ofd, 40, dbuf.data_ptr(), int(nb), stream.cuda_stream)
+                        st.write(ofd, 40, dbuf.data_ptr(), int(nb), stream.cuda_stream, threads=8)
                     finally:
                         os.close(ofd)
             res["compaction_file_to_file_GiBs"] = round(seg_len / 2 ** 30 / ((time.perf_counter() - t) / reps), 2)
         finally:
             os.close(fd)
     st.close()
-    res["note"] = ("source and output files in the page cache; pinned 8 MiB slices, 4 pread threads; compaction = "
+    res["note"] = ("source and output files in the page cache; 16 pinned 8 MiB slices, 8 pread / pwrite threads; compaction = "
                    "read + decode + re-encode + hint rebuild + dst WAL and hint written back")
     return res
 

@@ -111,7 +111,8 @@ int bcw_stage_read(bcw_stage* s, int fd, uint64_t file_off, uint64_t len, uint8_
   return err.load();
 }
 
-int bcw_stage_write(bcw_stage* s, int fd, uint64_t file_off, const uint8_t* d_src, uint64_t len, void* hip_stream) {
+int bcw_stage_write(bcw_stage* s, int fd, uint64_t file_off, const uint8_t* d_src, uint64_t len, void* hip_stream,
+                    uint32_t threads) {
   if (!s || fd < 0 || (len && !d_src)) return BCW_E_INVAL;
   if (len == 0) return BCW_OK;
   DeviceGuard dg(s->ctx->device);
@@ -119,38 +120,37 @@ int bcw_stage_write(bcw_stage* s, int fd, uint64_t file_off, const uint8_t* d_sr
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : s->ctx->cur;
   const uint64_t nsl = (len + s->slice - 1) / s->slice;
   const uint32_t ns = (uint32_t)s->slots.size();
-  // every slice's copy is queued up to ns ahead of the pwrite that drains it
-  uint64_t issued = 0;
-  auto issue = [&](uint64_t k) -> int {
-    Slot& q = s->slots[k % ns];
-    if (q.busy && hipEventSynchronize(q.done) != hipSuccess) return BCW_E_HIP;  // a copy of an earlier call
-    const uint64_t off = k * s->slice, n = std::min(s->slice, len - off);
-    if (hipMemcpyAsync(q.host, d_src + off, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipEventRecord(q.done, st) != hipSuccess)
-      return BCW_E_HIP;
-    q.busy = true;
-    return BCW_OK;
+  const uint32_t nt = std::max<uint32_t>(1, std::min<uint32_t>({threads ? threads : 4, ns, (uint32_t)nsl}));
+  const uint32_t per = ns / nt;
+  std::atomic<int> err{BCW_OK};
+  // thread t: slices t, t + nt, ...: the slice's copy is queued on the stream (after the work that
+  // produced the data), then pwritten once it has landed while the other threads' copies proceed
+  auto worker = [&](uint32_t t) {
+    uint32_t use = 0;
+    for (uint64_t k = t; k < nsl && err.load() == BCW_OK; k += nt, ++use) {
+      Slot& q = s->slots[t + nt * (use % per)];
+      if (q.busy && hipEventSynchronize(q.done) != hipSuccess) { err = BCW_E_HIP; return; }  // an earlier read
+      const uint64_t off = k * s->slice, n = std::min(s->slice, len - off);
+      if (hipMemcpyAsync(q.host, d_src + off, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipEventRecord(q.done, st) != hipSuccess || hipEventSynchronize(q.done) != hipSuccess) {
+        err = BCW_E_HIP;
+        return;
+      }
+      q.busy = false;
+      uint64_t put = 0;
+      while (put < n) {
+        const ssize_t r = pwrite(fd, q.host + put, n - put, (off_t)(file_off + off + put));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) { err = BCW_E_IO; return; }
+        put += (uint64_t)r;
+      }
+    }
   };
-  for (; issued < nsl && issued < ns; ++issued)
-    if (issue(issued) != BCW_OK) return BCW_E_HIP;
-  for (uint64_t k = 0; k < nsl; ++k) {
-    Slot& q = s->slots[k % ns];
-    if (hipEventSynchronize(q.done) != hipSuccess) return BCW_E_HIP;
-    q.busy = false;
-    const uint64_t off = k * s->slice, n = std::min(s->slice, len - off);
-    uint64_t put = 0;
-    while (put < n) {
-      const ssize_t r = pwrite(fd, q.host + put, n - put, (off_t)(file_off + off + put));
-      if (r < 0 && errno == EINTR) continue;
-      if (r <= 0) return BCW_E_IO;
-      put += (uint64_t)r;
-    }
-    if (issued < nsl) {
-      if (issue(issued) != BCW_OK) return BCW_E_HIP;
-      ++issued;
-    }
-  }
-  return BCW_OK;
+  std::vector<std::thread> th;
+  for (uint32_t t = 1; t < nt; ++t) th.emplace_back(worker, t);
+  worker(0);
+  for (auto& x : th) x.join();
+  return err.load();
 }
 
 }  // extern "C"

@@ -43,9 +43,9 @@ class Stage:
         if rc != 0:
             raise OSError(f"bcw_stage_read: {L.lib.bcw_strerror(rc).decode()}")
 
-    def write(self, fd: int, file_off: int, d_src: int, length: int, stream: int | None = None):
+    def write(self, fd: int, file_off: int, d_src: int, length: int, stream: int | None = None, threads: int = 4):
         """length bytes of device memory at d_src into fd at file_off (after the work queued on `stream`)."""
-        rc = L.lib.bcw_stage_write(self._h, fd, file_off, C.c_void_p(d_src), length, C.c_void_p(stream or 0))
+        rc = L.lib.bcw_stage_write(self._h, fd, file_off, C.c_void_p(d_src), length, C.c_void_p(stream or 0), threads)
         if rc != 0:
             raise OSError(f"bcw_stage_write: {L.lib.bcw_strerror(rc).decode()}")
 
@@ -59,10 +59,10 @@ class Stage:
         finally:
             os.close(fd)
 
-    def append_file(self, path: str, d_src: int, length: int, stream: int | None = None):
+    def append_file(self, path: str, d_src: int, length: int, stream: int | None = None, threads: int = 4):
         """append length device bytes to a file (Wal.Flush of the rewriter's buffered output)"""
         fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
         try:
-            self.write(fd, os.fstat(fd).st_size, d_src, length, stream)
+            self.write(fd, os.fstat(fd).st_size, d_src, length, stream, threads)
         finally:
             os.close(fd)

@@ -425,7 +425,7 @@ int bcw_read_records(bcw_ctx* ctx, const uint8_t* h_seg, const bcw_read_params* 
  * and writes the rewritten WAL through a buffer flushed every >= 1 MiB (WalRewriter
  * wal_rewriter.go:37-49 -> Wal.Flush wal.go:451-465). A stage owns `nslices` pinned host buffers of
  * `slice_bytes`; reads pread whole slices (up to `threads` reader threads) while earlier slices are
- * already copied to the device, writes copy slices back and pwrite each one while the next is in flight.
+ * already copied to the device, writes copy slices back and pwrite them on writer threads while the next copies are in flight.
  * Copies are queued on hip_stream (a hipStream_t; NULL: the context's stream), so a decode launched on
  * that stream after bcw_stage_read returns sees the whole segment. */
 typedef struct bcw_stage bcw_stage;
@@ -434,10 +434,11 @@ int bcw_stage_destroy(bcw_stage* st);
 /* len bytes of fd at file_off -> d_dst (device). Returns BCW_E_IO on a read error or a short file. */
 int bcw_stage_read(bcw_stage* st, int fd, uint64_t file_off, uint64_t len, uint8_t* d_dst, void* hip_stream,
                    uint32_t threads);
-/* len bytes of d_src (device) -> fd at file_off (waits for the work queued on hip_stream before each
- * slice, then pwrites it). Synchronous: returns once every byte is written. */
+/* len bytes of d_src (device) -> fd at file_off: each slice is copied back after the work queued on
+ * hip_stream and pwritten by one of up to `threads` writer threads while the others' copies proceed.
+ * Synchronous: returns once every byte is written. */
 int bcw_stage_write(bcw_stage* st, int fd, uint64_t file_off, const uint8_t* d_src, uint64_t len,
-                    void* hip_stream);
+                    void* hip_stream, uint32_t threads);
 
 #ifdef __cplusplus
 }

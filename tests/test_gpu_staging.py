@@ -31,7 +31,7 @@ def test_stage_roundtrip(ctx, tmp_path, size, slice_, threads):
     assert bytes(buf.download(size, 3)) == data.tobytes()
     dst = tmp_path / "dst.bin"
     dst.write_bytes(b"HEAD")
-    st.append_file(str(dst), buf.ptr + 3, size)
+    st.append_file(str(dst), buf.ptr + 3, size, threads=threads)
     assert dst.read_bytes() == b"HEAD" + data.tobytes()
     # a short file is an I/O error, as a truncated pread
     with pytest.raises(OSError):
