@@ -24,12 +24,52 @@ BASE_TIME = 1_700_000_000
 HBM_PEAK_GBS = 8000.0
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds: float) -> dict:
+    """the oracle's restated compactOneWal (oc_compact_append: iterate, Record.Encode, WriteRecord,
+    HintRecord.Encode; 1 thread) over a bounded sample of the same record shape, in GB/s of the same
+    algorithmic bytes (source read + WAL + hint written) and records/s"""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O  # noqa: E402  (cpu_baseline leg only)
+    src = np.frombuffer(O.synth(256 << 20, 0, 42, 20, 100, 4096, 0, BASE_TIME), dtype=np.uint8)
+    dec = O.decode(src, 40, BASE_TIME, 20, 20, want_bytes=False)
+    keep = np.ones(len(dec.recs), np.uint8)
+    passes, alg, t = 0, 0, time.perf_counter()
+    while True:
+        dst, hint = O.Writer(BASE_TIME, BASE_TIME), O.Writer(BASE_TIME, BASE_TIME)
+        ec, _, nin, _ = O.compact_append(dst, hint, 1, src, 40, BASE_TIME, BASE_TIME, 20, 20, keep)
+        assert ec == 0 and nin == len(keep)
+        alg += src.size + (dst.size() - 40) + (hint.size() - 40)
+        passes += 1
+        if time.perf_counter() - t >= seconds:
+            break
+    dt = time.perf_counter() - t
+    return {"value": round(alg / dt / 1e9, 3), "unit": "GB/s (src read + WAL + hint written)", "cores": 1,
+            "kind": "port", "records_per_s": round(passes * len(keep) / dt),
+            "sample": f"{passes} compactions of a {src.size} B segment ({len(keep)} records of the config-E shape) "
+                      f"with the restated compactOneWal (oc_compact_append, SSE4.2 CRC), 1 thread, {dt:.1f} s, "
+                      f"{cpu_model()}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=10_000_000)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     import torch
     from bitcaskdb_amd import _lib as L
@@ -170,6 +210,8 @@ def main():
         "layout_events": {"wal": int(res.wal_events), "hint": int(res.hint_events)},
         "parity": {"wal_equals_source": same, "hint_decodes_to_offsets": hint_ok},
     }
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     s = json.dumps(line)
     print(s, flush=True)
     if args.out:
