@@ -12,6 +12,11 @@
 #include <string.h>
 #include <unistd.h>
 
+/* memcpy of n bytes; n == 0 with a NULL pointer (an empty Go slice) is allowed */
+static inline void oc_memcpy(void* d, const void* s, size_t n) {
+  if (n) memcpy(d, s, n);
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* CRC-32C (Castagnoli), reflected poly 0x82F63B78 == Go crc32.MakeTable(crc32.Castagnoli)      */
 /* ------------------------------------------------------------------------------------------ */
@@ -82,7 +87,7 @@ static uint32_t g_shift_2stripe[32];
 static int g_shift_init = 0;
 
 static uint32_t hw_run(uint32_t c, const uint8_t* p, size_t n) {
-  while (n >= 8) { uint64_t w; memcpy(&w, p, 8); c = (uint32_t)_mm_crc32_u64(c, w); p += 8; n -= 8; }
+  while (n >= 8) { uint64_t w; oc_memcpy(&w, p, 8); c = (uint32_t)_mm_crc32_u64(c, w); p += 8; n -= 8; }
   while (n) { c = _mm_crc32_u8(c, *p++); --n; }
   return c;
 }
@@ -99,7 +104,7 @@ uint32_t oc_crc32c_hw(const uint8_t* p, size_t n) {
     const uint8_t* q = p;
     for (size_t i = 0; i < HW_STRIPE; i += 8) {
       uint64_t w0, w1, w2;
-      memcpy(&w0, q + i, 8); memcpy(&w1, q + HW_STRIPE + i, 8); memcpy(&w2, q + 2 * HW_STRIPE + i, 8);
+      oc_memcpy(&w0, q + i, 8); oc_memcpy(&w1, q + HW_STRIPE + i, 8); oc_memcpy(&w2, q + 2 * HW_STRIPE + i, 8);
       a = (uint32_t)_mm_crc32_u64(a, w0);
       b = (uint32_t)_mm_crc32_u64(b, w1);
       d = (uint32_t)_mm_crc32_u64(d, w2);
@@ -153,10 +158,10 @@ int oc_put_uvarint(uint8_t* out, uint64_t v) {
   return i;
 }
 
-static inline void put_u32(uint8_t* p, uint32_t v) { memcpy(p, &v, 4); }
-static inline void put_u64(uint8_t* p, uint64_t v) { memcpy(p, &v, 8); }
-static inline uint32_t get_u32(const uint8_t* p) { uint32_t v; memcpy(&v, p, 4); return v; }
-static inline uint64_t get_u64(const uint8_t* p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static inline void put_u32(uint8_t* p, uint32_t v) { oc_memcpy(p, &v, 4); }
+static inline void put_u64(uint8_t* p, uint64_t v) { oc_memcpy(p, &v, 8); }
+static inline uint32_t get_u32(const uint8_t* p) { uint32_t v; oc_memcpy(&v, p, 4); return v; }
+static inline uint64_t get_u64(const uint8_t* p) { uint64_t v; oc_memcpy(&v, p, 8); return v; }
 
 /* ------------------------------------------------------------------------------------------ */
 /* super block: wal.go:332-360 (write), wal.go:362-398 (load: crc -> magic -> blockSize)        */
@@ -199,7 +204,7 @@ static void w_append(oc_writer* w, const void* p, uint64_t n) {
     w->buf = (uint8_t*)realloc(w->buf, nc);
     w->cap = nc;
   }
-  memcpy(w->buf + w->len, p, n);
+  oc_memcpy(w->buf + w->len, p, n);
   w->len += n;
 }
 
@@ -230,7 +235,7 @@ uint64_t oc_writer_write(oc_writer* w, const uint8_t* rec, size_t n) {
     uint8_t hdr[7];
     put_u32(hdr, oc_compute_crc32(rec, frag));
     uint16_t l16 = (uint16_t)frag;
-    memcpy(hdr + 4, &l16, 2);
+    oc_memcpy(hdr + 4, &l16, 2);
     hdr[6] = type;
     w_append(w, hdr, 7);
     w_append(w, rec, frag);
@@ -271,14 +276,14 @@ int64_t oc_record_encode(uint8_t* out, const uint8_t* ns, size_t ns_len, const u
   size_t header = (size_t)t + expire_size + ns_len + etag_len + 2;
   size_t o = 0;
   out[o++] = (uint8_t)header; /* byte(headerSize): truncates above 255 (record.go:109) */
-  memcpy(out + o, ns, ns_len); o += ns_len;
+  oc_memcpy(out + o, ns, ns_len); o += ns_len;
   out[o++] = flag;
-  memcpy(out + o, tmp, t); o += t;
-  memcpy(out + o, etag, etag_len); o += etag_len;
-  memcpy(out + o, expb, expire_size); o += expire_size;
-  memcpy(out + o, key, key_len); o += key_len;
-  memcpy(out + o, val, val_len); o += val_len;
-  memcpy(out + o, meta, meta_len); o += meta_len;
+  oc_memcpy(out + o, tmp, t); o += t;
+  oc_memcpy(out + o, etag, etag_len); o += etag_len;
+  oc_memcpy(out + o, expb, expire_size); o += expire_size;
+  oc_memcpy(out + o, key, key_len); o += key_len;
+  oc_memcpy(out + o, val, val_len); o += val_len;
+  oc_memcpy(out + o, meta, meta_len); o += meta_len;
   return (int64_t)o;
 }
 
@@ -347,9 +352,9 @@ void oc_record_parse(const uint8_t* data, size_t len, size_t cap, uint64_t base_
 size_t oc_hint_encode(uint8_t* out, const uint8_t* ns, size_t ns_len, const uint8_t* key, size_t key_len,
                       uint64_t fid, uint64_t off, uint64_t size) {
   size_t o = 0;
-  memcpy(out, ns, ns_len); o += ns_len;
+  oc_memcpy(out, ns, ns_len); o += ns_len;
   o += oc_put_uvarint(out + o, key_len);
-  memcpy(out + o, key, key_len); o += key_len;
+  oc_memcpy(out + o, key, key_len); o += key_len;
   o += oc_put_uvarint(out + o, fid);
   o += oc_put_uvarint(out + o, off);
   o += oc_put_uvarint(out + o, size);
@@ -413,7 +418,7 @@ static void push_rec(oc_decode* d, const oc_rec* r, const uint8_t* bytes, uint64
     d->cap_bytes = nc;
   }
   d->byte_offs[d->n_recs] = d->n_bytes;
-  memcpy(d->bytes + d->n_bytes, bytes, n);
+  oc_memcpy(d->bytes + d->n_bytes, bytes, n);
   d->n_bytes += n;
   d->recs[d->n_recs++] = *r;
   d->byte_offs[d->n_recs] = d->n_bytes;
@@ -449,7 +454,7 @@ oc_decode* oc_decode_segment(const uint8_t* seg, uint64_t len, uint32_t start_of
     const uint8_t* header = buf + buf_off;
     buf_off += OC_HEADER_SIZE;
     uint32_t crc = get_u32(header);
-    uint16_t l16; memcpy(&l16, header + 4, 2);
+    uint16_t l16; oc_memcpy(&l16, header + 4, 2);
     int64_t length = l16;
     uint8_t type = header[6];
     if (acc_len == 0) { off = (uint64_t)(file_off + buf_off); rec_first = (uint32_t)d->n_frags; }
@@ -478,7 +483,7 @@ oc_decode* oc_decode_segment(const uint8_t* seg, uint64_t len, uint32_t start_of
         acc_cap = (acc_len + (uint64_t)length) * 2 + 64;
         acc = (uint8_t*)realloc(acc, acc_cap);
       }
-      memcpy(acc + acc_len, data, (size_t)length);
+      oc_memcpy(acc + acc_len, data, (size_t)length);
       acc_len += (uint64_t)length;
       if (type != OC_LAST) continue;
       rec_bytes = acc; rec_len = acc_len; rec_cap = acc_len;
@@ -505,11 +510,11 @@ void oc_decode_counts(const oc_decode* d, uint64_t* n_frags, uint64_t* n_recs, u
   *n_frags = d->n_frags; *n_recs = d->n_recs; *err_frag = d->err_frag; *err_class = d->err_class;
   *rec_bytes = d->n_bytes;
 }
-void oc_decode_frags(const oc_decode* d, oc_frag* dst) { memcpy(dst, d->frags, d->n_frags * sizeof(oc_frag)); }
-void oc_decode_recs(const oc_decode* d, oc_rec* dst) { memcpy(dst, d->recs, d->n_recs * sizeof(oc_rec)); }
+void oc_decode_frags(const oc_decode* d, oc_frag* dst) { oc_memcpy(dst, d->frags, d->n_frags * sizeof(oc_frag)); }
+void oc_decode_recs(const oc_decode* d, oc_rec* dst) { oc_memcpy(dst, d->recs, d->n_recs * sizeof(oc_rec)); }
 void oc_decode_bytes(const oc_decode* d, uint8_t* dst, uint64_t* offs) {
-  memcpy(dst, d->bytes, d->n_bytes);
-  memcpy(offs, d->byte_offs, (d->n_recs + 1) * sizeof(uint64_t));
+  oc_memcpy(dst, d->bytes, d->n_bytes);
+  oc_memcpy(offs, d->byte_offs, (d->n_recs + 1) * sizeof(uint64_t));
 }
 void oc_decode_free(oc_decode* d) {
   if (!d) return;
@@ -536,7 +541,7 @@ static uint64_t decode_fast_impl(const uint8_t* seg, int fd, uint64_t len, uint3
       if (buf_size <= 0) { if (buf_size < 0) *err_class = OC_ERR_PANIC; break; }
       if (buf_size < (int64_t)OC_HEADER_SIZE) { *err_class = OC_ERR_PANIC; break; }
       if (seg) {
-        memcpy(blk, seg + file_off, (size_t)buf_size);
+        oc_memcpy(blk, seg + file_off, (size_t)buf_size);
       } else { /* PreadFull (utils.go:32-48) */
         int64_t got = 0;
         while (got < buf_size) {
@@ -550,7 +555,7 @@ static uint64_t decode_fast_impl(const uint8_t* seg, int fd, uint64_t len, uint3
     const uint8_t* header = blk + buf_off;
     buf_off += OC_HEADER_SIZE;
     uint32_t crc = get_u32(header);
-    uint16_t l16; memcpy(&l16, header + 4, 2);
+    uint16_t l16; oc_memcpy(&l16, header + 4, 2);
     int64_t length = l16;
     uint8_t type = header[6];
     if (acc_len == 0) off = (uint64_t)(file_off + buf_off);
@@ -563,7 +568,7 @@ static uint64_t decode_fast_impl(const uint8_t* seg, int fd, uint64_t len, uint3
     if (type == OC_FULL) { rb = data; rl = (uint64_t)length; }
     else if (type >= OC_FIRST && type <= OC_LAST) {
       if (acc_len + (uint64_t)length > acc_cap) { acc_cap = (acc_len + length) * 2 + 64; acc = (uint8_t*)realloc(acc, acc_cap); }
-      memcpy(acc + acc_len, data, (size_t)length);
+      oc_memcpy(acc + acc_len, data, (size_t)length);
       acc_len += (uint64_t)length;
       if (type != OC_LAST) continue;
       rb = acc; rl = acc_len;
@@ -688,8 +693,8 @@ static inline uint64_t splitmix64(uint64_t* s) {
 }
 static void fill_rand(uint64_t* s, uint8_t* p, size_t n) {
   size_t i = 0;
-  for (; i + 8 <= n; i += 8) { uint64_t v = splitmix64(s); memcpy(p + i, &v, 8); }
-  if (i < n) { uint64_t v = splitmix64(s); memcpy(p + i, &v, n - i); }
+  for (; i + 8 <= n; i += 8) { uint64_t v = splitmix64(s); oc_memcpy(p + i, &v, 8); }
+  if (i < n) { uint64_t v = splitmix64(s); oc_memcpy(p + i, &v, n - i); }
 }
 
 oc_writer* oc_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_t seed, uint32_t ns_size,
@@ -717,7 +722,7 @@ oc_writer* oc_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_
       vl = 128u * (size_t)(lo + 1);
     }
     fill_rand(&s, key, key_len);
-    if (key_len >= 8) memcpy(key, &i, 8);
+    if (key_len >= 8) oc_memcpy(key, &i, 8);
     fill_rand(&s, val, vl);
     int64_t n = oc_record_encode(rec, ns, ns_size, key, key_len, val, vl, NULL, 0, 0, 0, NULL, 0, base_time);
     oc_writer_write(w, rec, (size_t)n);
@@ -767,13 +772,13 @@ static uint64_t oc_hash_bytes(uint64_t h, const uint8_t* p, uint64_t n) {
   uint64_t i = 0;
   for (; i + 8 <= n; i += 8) {
     uint64_t w;
-    memcpy(&w, p + i, 8);
+    oc_memcpy(&w, p + i, 8);
     h = (h ^ w) * 0x9E3779B97F4A7C15ull;
     h = (h << 27) | (h >> 37);
   }
   if (i < n) {
     uint64_t w = 0;
-    memcpy(&w, p + i, (size_t)(n - i));
+    oc_memcpy(&w, p + i, (size_t)(n - i));
     h = (h ^ w ^ ((n - i) << 56)) * 0xC2B2AE3D27D4EB4Full;
     h = (h << 31) | (h >> 33);
   }
@@ -810,7 +815,7 @@ void oc_gather_payload_hashes(const uint8_t* seg, uint64_t seg_len, const uint64
     for (uint64_t g = f0; g <= f1 && w <= n; ++g) {
       uint64_t o = data_off[g], l = flen[g];
       if (o + l > seg_len || w + l > n) { w = n + 1; break; }
-      memcpy(tmp + w, seg + o, l);
+      oc_memcpy(tmp + w, seg + o, l);
       w += l;
     }
     out[r] = (w == n) ? oc_hash_bytes(0x5EEDull ^ n, tmp, n) : 0;
@@ -922,7 +927,7 @@ static oc_islot* oc_index_find(oc_index* x, const uint8_t* k, uint32_t kl, uint6
     if (!e->key) {
       if (!create) return NULL;
       e->key = (uint8_t*)malloc(kl ? kl : 1);
-      memcpy(e->key, k, kl);
+      oc_memcpy(e->key, k, kl);
       e->klen = kl;
       e->h = h;
       e->live = 0;
@@ -935,8 +940,8 @@ static oc_islot* oc_index_find(oc_index* x, const uint8_t* k, uint32_t kl, uint6
 }
 static uint8_t* merged_key(const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl) {
   uint8_t* m = (uint8_t*)malloc(nsl + kl + 1);
-  if (nsl) memcpy(m, ns, nsl);
-  if (kl) memcpy(m + nsl, key, kl);
+  if (nsl) oc_memcpy(m, ns, nsl);
+  if (kl) oc_memcpy(m + nsl, key, kl);
   return m;
 }
 void oc_index_set(oc_index* x, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, int op, uint64_t fid,
@@ -1046,7 +1051,7 @@ int oc_read_record(const uint8_t* seg, uint64_t seg_len, uint64_t offset, uint64
     blk_off += OC_HEADER_SIZE;
     uint32_t crc = get_u32(h);
     uint16_t l16;
-    memcpy(&l16, h + 4, 2);
+    oc_memcpy(&l16, h + 4, 2);
     uint64_t length = l16;
     uint8_t type = h[6];
     if (length > blk_size - blk_off) return OC_RD_CORRUPTED;  /* ErrWalCorruptedData */
@@ -1054,7 +1059,7 @@ int oc_read_record(const uint8_t* seg, uint64_t seg_len, uint64_t offset, uint64
     blk_off += length;
     if (verify && oc_compute_crc32(data, (size_t)length) != crc) return OC_RD_CRC;
     /* record = append(record, data...): the capacity is `size`, appending beyond it just grows */
-    if (got + length <= size) memcpy(out + got, data, (size_t)length);
+    if (got + length <= size) oc_memcpy(out + got, data, (size_t)length);
     got += length;
     if (type == OC_FULL || type == OC_LAST) return got != size ? OC_RD_SIZE : OC_RD_OK;
     if (type != OC_FIRST && type != OC_MIDDLE) return OC_RD_TYPE;
