@@ -11,10 +11,14 @@
 //   k_ev_win/walk/emit/fix  the writer's layout recurrence as an event scan              wal.go:505-549
 //   k_recoff        per record: the file offset WriteRecord returns                     wal.go:514-516
 //   (compaction) k_hint_sizes + scan + event scan + k_recoff for the hint WAL           hint.go:32-48
-//   k_recdesc_w     per record: payload as literal prefix | source range | literal suffix
-//   k_write         one persistent launch over every record of both WALs: fragments in closed form,
-//                   16 B units copied and folded into each fragment's CRC-32C (utils.go:24-29)
+//   k_recdesc_w     per dst record: payload as literal prefix | source range | literal suffix, and the
+//                   record's CRC from the source fragments' verified check words (CRC combine)
+//   k_wcopy         the dst WAL, one wave per record in one or two fragments: a re-layout copy, only
+//                   the shorter piece of a split record is hashed (utils.go:24-29)
+//   k_write         the other dst records (more fragments, irregular sources): 16 B units copied and
+//                   folded into each fragment's CRC-32C
 //   k_write_general the rare records with more literal bytes than the descriptor holds
+//   k_hwrite        the hint WAL, one record per lane, staged per wave in LDS
 //   k_enc_finalize  bcw_encode_result
 //
 // Layout as an event scan. Concatenate the records' (7 B header + payload) units into a y axis:
@@ -872,8 +876,8 @@ __global__ __launch_bounds__(256) void k_recdesc_w(EncDev e, const uint64_t* __r
 }
 
 // ------------------------------------------------------------------------------------------
-// k_write: the record-parallel WAL writer (Wal.WriteRecord wal.go:505-549 for every written record
-// at once). One wave per record, persistent waves striding over the records. A record's fragments
+// k_write: the record-parallel WAL writer (Wal.WriteRecord wal.go:505-549) for the dst records k_wcopy
+// does not take. One 16-lane group per record, persistent groups striding over the records. A record's fragments
 // follow in closed form from its header offset (data up to the block end, continuation headers at
 // block starts). A fragment's data is cut into 16 B units aligned to the output address; lane l
 // takes k = ceil(units/64) consecutive units (one pass per fragment) and, per unit:
@@ -1088,7 +1092,7 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
   // items: the records of layout 0, then those of layout 1 (short hint records last), one per group
   // of kG lanes. An item's descriptor is loaded one item ahead: the RecDescW spread over the group's
   // lanes 0-7 (header, then the literal bytes), da[j], da[j+1] and fpos[j] in every lane.
-  static_assert(kG >= 8 && kG <= 64, "group size");
+  static_assert(kG == 16, "group size: the DPP row rotation shares source blocks within rows of 16 lanes");
   const uint64_t nitems = N * A.nlay;
   struct Pre {
     uint4 q;
@@ -1189,7 +1193,6 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
         uint64_t S = 0;
         int64_t run = -1;
         constexpr int64_t kStep = 16 * kG;
-        if constexpr (kG == 16) {
         for (uint32_t r0 = gl; r0 - gl < nunits; r0 += kG * kWRounds) {
           // source of the fast units: one aligned block per lane and round; the block after it is the
           // next lane's (lane 15: lane 0's of the next round, or its own extra load in the last round),
@@ -1264,64 +1267,6 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
             if (crc_on) c = op_apply_s(hop, c) ^ crc_step16(t8, 0u, v);
           }
           zb += kStep * kWRounds;
-        }
-        } else {
-        for (uint32_t r0 = gl; r0 - gl < nunits; r0 += kG * kWRounds) {
-          uint4 va[kWRounds][2];
-          uint32_t shv[kWRounds];
-          bool fast[kWRounds];
-#pragma unroll
-          for (int q = 0; q < kWRounds; ++q) {
-            const uint32_t r = r0 + kG * q;
-            const int64_t z = zb + kStep * q;
-            fast[q] = false;
-            shv[q] = 0;
-            if (r < rlast && r != 0 && R.regular && z >= R.zA && z + 16 <= R.zB) {
-              if (run < 16) {
-                uint64_t ru;
-                S = src_at(R.d0, R.l0, e.start_off, R.mid_off + (uint64_t)(z - R.zA), ru);
-                run = (int64_t)ru;
-              }
-              if (run >= 16 && (S & ~15ull) + 32 <= e.src_len) {
-                const uint4* sp2 = reinterpret_cast<const uint4*>(e.seg + (S & ~15ull));
-                va[q][0] = sp2[0];
-                va[q][1] = sp2[1];
-                shv[q] = (uint32_t)(S & 15u);
-                fast[q] = true;
-              }
-            } else {
-              run = -1;
-            }
-            S += kStep;
-            run -= kStep;
-          }
-#pragma unroll
-          for (int q = 0; q < kWRounds; ++q) {
-            const uint32_t r = r0 + kG * q;
-            if (r >= nunits) continue;
-            const uint64_t ua = (uf + r) << 4;
-            uint4 v;
-            int32_t b0 = 0, b1 = 16;
-            if (fast[q]) {
-              v = shift16(va[q][0], va[q][1], shv[q]);
-            } else {
-              b0 = ua < as ? (int32_t)(as - ua) : 0;
-              b1 = ua + 16 > ae ? (int32_t)(ae - ua) : 16;
-              v = unit_general(e, R, sl, zb + kStep * q, b0, b1);
-            }
-            uint8_t* d = reinterpret_cast<uint8_t*>((uintptr_t)ua);
-            if (b1 - b0 == 16) {
-              __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(d));
-              __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(d) + 1);
-              __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(d) + 2);
-              __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(d) + 3);
-            } else {
-              for (int32_t b = b0; b < b1; ++b) d[b] = (uint8_t)sel_byte(v, (uint32_t)b);
-            }
-            if (crc_on) c = op_apply_s(hop, c) ^ crc_step16(t8, 0u, v);
-          }
-          zb += kStep * kWRounds;
-        }
         }
         if (crc_on) {
         // shift each lane's chain to the end of the fragment's last unit (d < kG units follow it)
