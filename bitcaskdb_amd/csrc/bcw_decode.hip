@@ -695,7 +695,9 @@ struct BodyDesc {
 
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
 // 4 no lane-operator / scan combine, 8 no record-state tail, 16 phase stamps, 32 quad-layout loads
-// instead of per-lane windows, 64 no quad transpose
+// instead of per-lane windows, 64 no quad transpose, 128 no first-window mask, 256 no last-window fix,
+// 512 per-wave wall-clock stamps (entry, tables loaded, loop done) into lpre as u64[4] per wave, 1024 no
+// priority balancing
 template <int ABL = 0>
 __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                      uint32_t start_off, uint64_t nblocks,
@@ -704,6 +706,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
                                                      Xf* __restrict__ wpre, Xf* __restrict__ wgx,
                                                      uint64_t* __restrict__ misc) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kCrcLds / 4];
+  const uint64_t t_entry = (ABL & 512) ? wall_clock64() : 0;
   uint32_t* s_slice = lds;
   uint32_t* s_fwd = lds + kLdsSlice;
   uint32_t* s_carry = s_fwd + kLdsFwd;
@@ -712,6 +715,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint32_t tid = threadIdx.x;
   __shared__ Xf s_wagg[kCrcWaves];  // wave aggregates of this workgroup
   __shared__ uint32_t s_wdone;      // waves of this workgroup done
+  __shared__ uint32_t s_rem[kCrcWaves];  // windows each wave has left (balance)
   if (tid == 0) s_wdone = 0;
   {  // table image -> LDS: all 16 B loads in flight before the first store
     constexpr uint32_t kVec = kLdsImage / 4;
@@ -729,6 +733,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   __syncthreads();
 
   if (blockIdx.x == 0 && tid == 0) misc[M_T_CRC0] = wall_clock64();
+  const uint64_t t_tables = (ABL & 512) ? wall_clock64() : 0;
   const uint32_t lane = tid & 63u;
   const uint32_t lo = lane & 31u;
   const uint32_t lb = lo * 4u;  // lane slot in a slice-table row
@@ -750,8 +755,10 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   uint32_t r_head = 0, r_tail = 0;  // absolute ring positions (wave-uniform)
   uint32_t cbase = 0;               // windows appended so far
   uint32_t kwin = 0;                // next group of 64 fragments to append
-  Frag pf{};                        // the next group's fragment descriptor (loaded one group ahead)
-  if (lane < nfr) pf = frags[f0 + lane];
+  // the next group's fragment descriptor, loaded one group ahead as a raw 16 B vector (decoded only when the
+  // group is appended, so the load does not make the compiler wait for it -- and the window loads -- early)
+  uint4 pf = make_uint4(0, 0, 0, 0);
+  if (lane < nfr) pf = reinterpret_cast<const uint4*>(frags)[f0 + lane];
 
   // Group kwin (64 fragments, one per lane): every fragment is appended to the ring with its C windows
   // (GE tiling, see above); the group after it is prefetched. No window is loaded here: the first window
@@ -760,8 +767,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     const uint32_t fi = kwin * 64u + lane;
     ++kwin;
     const bool valid = fi < nfr;
-    const Frag f = pf;
-    if (fi + 64u < nfr) pf = frags[f0 + fi + 64u];
+    Frag f;
+    __builtin_memcpy(&f, &pf, sizeof f);
+    if (fi + 64u < nfr) pf = reinterpret_cast<const uint4*>(frags)[f0 + fi + 64u];
     FragGeo geo{0, 0, 0};
     uint32_t e = 0;
     if (valid) {
@@ -840,16 +848,22 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     return d;
   };
 
+  // the window loads of one pass. Every lane loads (an inactive lane reads a fixed in-bounds window), so in
+  // the common case the pass's loads are one straight-line group of 8; only passes with a window crossing the
+  // segment's ends (its first and last bytes) take bounds-checked 16 B loads.
+  const int64_t gblk = wbase + 128 > 0 ? wbase + 128 : 0;  // the wave's first block
+  const int64_t gsafe = seg_len < 128 ? -1 : (gblk < (int64_t)seg_len - 128 ? gblk : (int64_t)seg_len - 128);
   auto issue = [&](const BodyDesc& d, uint32_t (&w)[32]) {
     if (ABL & 2) return;
-    const int64_t goff = wbase + d.woff;
-    const bool inb = __all(!d.active() || (goff >= 0 && (uint64_t)goff + 128 <= seg_len));
-    if (!(ABL & 32)) {
-      if (d.active()) load_window(seg, seg_len, goff, inb, w);
+    const int64_t goff = d.active() ? wbase + d.woff : gsafe;
+    const bool inb = __all(goff >= 0 && (uint64_t)goff + 128 <= seg_len);
+    if (ABL & 32) {
+      if (inb) load_windows_quad<false>(seg, seg_len, wbase, d.woff, d.active(), lane, w);
+      else load_windows_quad<true>(seg, seg_len, wbase, d.woff, d.active(), lane, w);
     } else if (inb) {
-      load_windows_quad<false>(seg, seg_len, wbase, d.woff, d.active(), lane, w);
-    } else {
-      load_windows_quad<true>(seg, seg_len, wbase, d.woff, d.active(), lane, w);
+      load_window(seg, seg_len, goff, true, w);
+    } else if (d.active()) {
+      load_window(seg, seg_len, goff, false, w);
     }
   };
 
@@ -858,7 +872,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     uint32_t v = 0;
     if ((ABL & 32) && !(ABL & 64)) quad_windows_transpose(w, lane);
     if (d.active()) {
-      if (d.cfb() == 0u) {  // first window: zero the bytes before the data (the previous header / fragment)
+      if (!(ABL & 128) && d.cfb() == 0u) {  // first window: zero the bytes before the data (the previous header / fragment)
         const uint32_t lo = d.lo(), kf = lo >> 2;
         const uint32_t pm = 0xffffffffu << (8u * (lo & 3u));  // the word holding the first data byte
 #pragma unroll
@@ -867,7 +881,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
           w[k2] &= m;
         }
       }
-      if (d.last()) fix_last(w, d.hi(), d.J);
+      if (!(ABL & 256) && d.last()) fix_last(w, d.hi(), d.J);
       // a fragment continuing from the previous pass: its state so far seeds lane 0's chain
       const uint32_t seed = (lane == 0u && d.cfb() > 0u) ? carry : 0u;
       if (!(ABL & 1)) {
@@ -888,7 +902,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   };
 
   // software pipeline: the next pass's windows are in flight while this pass chains
-  // (ABL & 16: per-phase cycle stamps for tools/kbench, summed into misc[7..9])
+  // (ABL & 16: per-phase cycle stamps for tools/kbench, summed into misc[7..9]: describe = ring upkeep +
+  // descriptor + load issue, issue = unused, compute = the chain, including any wait for its loads)
   uint64_t t_desc = 0, t_issue = 0, t_comp = 0, tq = 0;
   auto stamp = [&](uint64_t& acc) {
     if (ABL & 16) {
@@ -897,31 +912,53 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       tq = t;
     }
   };
-  // One copy of the loop body (instruction-cache footprint). At the top of an iteration wx holds pass
-  // p (chained now), wy the loads of pass p+64 in flight, dz the descriptors of pass p+128. After
-  // the chain: advance the ring, take wy into wx, issue pass p+128's
-  // loads, then describe pass p+192 -- descriptor work is off the load-to-load critical path.
-  // The first three iterations only fill the pipeline (p < 0).
   if (ABL & 16) tq = __builtin_amdgcn_s_memtime();
-  uint32_t wx[32], wy[32];
-  BodyDesc dx{}, dy{}, dz{};
-  for (int64_t p = -192;;) {
-    if (p >= 0) {
-      stamp(t_issue);
-      compute(dx, wx);
-      stamp(t_comp);
-    }
-    p += 64;
-    if (p >= 0 && (uint64_t)p >= cbase) break;
-    advance((uint32_t)(p + 128));
+  // Balance within the workgroup: the SIMD arbiter favours older waves, so with equal shares the workgroup's
+  // last four waves would finish ~15 % after its first four. Each wave publishes its remaining windows (an
+  // estimate: 256 per block + one per fragment, less the windows done) and takes issue priority while it has
+  // (nearly) the most left.
+  const uint32_t est = (uint32_t)(b1 - b0) * 256u + nfr;
+  if (lane == 0) s_rem[wave] = est;
+  auto balance = [&](uint32_t done) {
+    if (ABL & 1024) return;
+    const uint32_t rem = est > done ? est - done : 0u;
+    if (lane == 0) s_rem[wave] = rem;
+    const uint32_t v = lane < (uint32_t)kCrcWaves ? s_rem[lane] : 0u;
+    const uint32_t mx = __builtin_amdgcn_readlane(wave_max_scan(v, lane), 63);
+    if (rem + 128u >= mx) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
+  };
+  auto pipeline = [&]() {
+    // One copy of the loop body (instruction-cache footprint). At the top of an iteration wx holds pass p
+    // (chained now), wy the loads of pass p+64, dz the descriptors of pass p+128. After the chain: advance
+    // the ring, take wy into wx, issue pass p+128's loads into wy, then describe pass p+192. The first three
+    // iterations only fill the pipeline (p < 0).
+    // Measured (tools/kbench, config B): the compiler's back-edge copy of wy waits for those loads at the
+    // end of the iteration, so they overlap only the describe; issuing them before the chain instead (full
+    // overlap) is slower, 265 vs 246 us: more lane-per-window loads in flight per CU make the texture
+    // addresser (TA busy 71 % vs 50 %, one tag lookup per 16 B piece) the bottleneck.
+    uint32_t wx[32], wy[32];
+    BodyDesc dx{}, dy{}, dz{};
+    for (int64_t p = -192;;) {
+      if (p >= 0) {
+        compute(dx, wx);
+        balance((uint32_t)p + 64u);
+        stamp(t_comp);
+      }
+      p += 64;
+      if (p >= 0 && (uint64_t)p >= cbase) break;
+      advance((uint32_t)(p + 128));
 #pragma unroll
-    for (int k2 = 0; k2 < 32; ++k2) wx[k2] = wy[k2];
-    dx = dy;
-    issue(dz, wy);
-    dy = dz;
-    stamp(t_desc);
-    dz = describe((uint32_t)(p + 128));
-  }
+      for (int k2 = 0; k2 < 32; ++k2) wx[k2] = wy[k2];
+      dx = dy;
+      issue(dz, wy);
+      dy = dz;
+      stamp(t_desc);
+      dz = describe((uint32_t)(p + 128));
+      stamp(t_desc);
+    }
+  };
+  if (nfr > 0u) pipeline();
   stamp(t_comp);
   if ((ABL & 16) && lane == 0) {
     atomicAdd(reinterpret_cast<unsigned long long*>(&misc[7]), (unsigned long long)t_desc);
@@ -929,6 +966,11 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     atomicAdd(reinterpret_cast<unsigned long long*>(&misc[9]), (unsigned long long)t_comp);
   }
 
+  __builtin_amdgcn_s_setprio(0);
+  if ((ABL & 512) && lane == 0) {
+    uint64_t* q = reinterpret_cast<uint64_t*>(lpre) + 4 * gw;
+    q[0] = t_entry; q[1] = t_tables; q[2] = wall_clock64(); q[3] = nfr;
+  }
   if (ABL & 8) return;
   // ---- record-state transforms of this wave's blocks (the verdicts were written by its lanes) ----
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

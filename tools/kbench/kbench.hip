@@ -5,6 +5,7 @@
 #include "../../bitcaskdb_amd/csrc/bcw_encode.hip"
 #include "../../bitcaskdb_amd/csrc/bcw_index.hip"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -270,9 +271,70 @@ int main(int argc, char** argv) {
   }
   if (argc > 3) {  // counter-collection mode: only the product k_crc, a few launches
     const int k = atoi(argv[3]);
-    for (int i = 0; i < k; ++i) run(k_crc<0>, cus);
+    const int v = argc > 4 ? atoi(argv[4]) : 0;  // ablation variant
+    float t = 0;
+    for (int i = 0; i < k; ++i) {
+      switch (v) {
+        case 1: t = run(k_crc<1>, cus); break;
+        case 2: t = run(k_crc<2>, cus); break;
+        case 4: t = run(k_crc<4>, cus); break;
+        case 8: t = run(k_crc<8>, cus); break;
+        case 128: t = run(k_crc<128>, cus); break;
+        case 256: t = run(k_crc<256>, cus); break;
+        case 384: t = run(k_crc<384>, cus); break;
+        case 7: t = run(k_crc<7>, cus); break;
+        case 32: t = run(k_crc<32>, cus); break;
+        case 520: t = run(k_crc<520>, cus); break;
+        case 1544: t = run(k_crc<1544>, cus); break;
+        case 1024: t = run(k_crc<1024>, cus); break;
+        default: t = run(k_crc<0>, cus);
+      }
+    }
     CK(hipStreamSynchronize(st));
-    printf("k_crc x%d done\n", k);
+    printf("k_crc<%d> x%d done, %.4f ms\n", v, k, t);
+    if (v == 520 || v == 1544) {  // per-wave stamps of the last launch: start / tables / loop end, by XCD (blockIdx % 8)
+      const int nw = cus * kCrcWaves;
+      std::vector<uint64_t> q(4 * (size_t)nw);
+      CK(hipMemcpy(q.data(), s.pre, q.size() * 8, hipMemcpyDeviceToHost));
+      uint64_t t0 = ~0ull, tmax = 0;
+      for (int w = 0; w < nw; ++w) { t0 = std::min(t0, q[4 * w]); tmax = std::max(tmax, q[4 * w + 2]); }
+      std::vector<double> ends(nw);
+      double xs[8] = {0}, xe[8] = {0}, xm[8] = {0}; int xn[8] = {0};
+      for (int w = 0; w < nw; ++w) {
+        const int x = (w / kCrcWaves) % 8;
+        const double st = (q[4 * w] - t0) / 100.0, en = (q[4 * w + 2] - t0) / 100.0;
+        ends[w] = en; xs[x] += st; xe[x] += en; xm[x] = std::max(xm[x], en); ++xn[x];
+      }
+      std::vector<double> so = ends; std::sort(so.begin(), so.end());
+      printf("wave loop end (us from first entry): min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f\n", so[0], so[nw / 10],
+             so[nw / 2], so[nw * 9 / 10], so[nw - 1]);
+      for (int x = 0; x < 8; ++x)
+        printf("  xcd %d: mean start %.1f  mean end %.1f  max end %.1f us\n", x, xs[x] / xn[x], xe[x] / xn[x], xm[x]);
+      double ss[kCrcWaves] = {0};
+      for (int w = 0; w < nw; ++w) ss[w % kCrcWaves] += ends[w];
+      printf("  mean end by wave slot:");
+      for (int k = 0; k < kCrcWaves; ++k) printf(" %.1f", ss[k] / (nw / kCrcWaves));
+      printf("\n");
+      std::vector<double> cuend(cus), cuspread(cus);
+      for (int c = 0; c < cus; ++c) {
+        double mx = 0, mn = 1e30, sm = 0;
+        for (int k = 0; k < kCrcWaves; ++k) { const double e = ends[c * kCrcWaves + k]; mx = std::max(mx, e); mn = std::min(mn, e); sm += e; }
+        cuend[c] = sm / kCrcWaves; cuspread[c] = mx - mn;
+      }
+      std::sort(cuend.begin(), cuend.end()); std::sort(cuspread.begin(), cuspread.end());
+      printf("  per-WG mean end: min %.1f p50 %.1f max %.1f | per-WG spread (max-min): p10 %.1f p50 %.1f p90 %.1f\n",
+             cuend[0], cuend[cus / 2], cuend[cus - 1], cuspread[cus / 10], cuspread[cus / 2], cuspread[cus * 9 / 10]);
+      {  // slowest waves: their fragment counts
+        std::vector<std::pair<double, int>> ew(nw);
+        for (int w = 0; w < nw; ++w) ew[w] = {ends[w], w};
+        std::sort(ew.begin(), ew.end());
+        printf("  fastest/slowest waves (end us, frags):");
+        for (int k : {0, 1, 2, nw - 3, nw - 2, nw - 1}) printf(" [w%d %.1f %lu]", ew[k].second, ew[k].first, q[4 * ew[k].second + 3]);
+        printf("\n");
+      }
+      double tl = 0; for (int w = 0; w < nw; ++w) tl += (q[4 * w + 1] - q[4 * w]) / 100.0;
+      printf("  mean table-load time %.2f us\n", tl / nw);
+    }
     return 0;
   }
   float a0 = run(k_crc<0>, cus), a1 = run(k_crc<1>, cus), a2 = run(k_crc<2>, cus), a4 = run(k_crc<4>, cus),
