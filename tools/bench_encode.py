@@ -62,6 +62,74 @@ def cpu_baseline(seconds: float) -> dict:
                       f"{cpu_model()}"}
 
 
+def index_leg(L, ctx, stream, d_src, dparams, table, d_res, n_rec, steps, decode_checked, encode, keep):
+    """SURVEY.md §8 f2 / f1 on the same 10 M records: the index rebuild (recoverFromWal's Put of every
+    delivered row, bcw_index_put_decoded_async) into an empty device index, then the compaction filter
+    (doFilter against that index, bcw_compact_filter_async) producing the keep mask the encode consumes.
+    Every row must be kept (the index points at exactly these records)."""
+    import torch
+    from bitcaskdb_amd.index import Index
+    ix = Index(ctx, keys=n_rec + (n_rec >> 2), arena_bytes=n_rec * 160 + (1 << 20))
+    d_ir = torch.zeros(C.sizeof(L.IndexResult), dtype=torch.uint8, device=d_src.device)
+    decode_checked(d_src.data_ptr(), dparams)
+
+    def put():
+        assert L.lib.bcw_index_put_decoded_async(ix.handle, C.c_void_p(d_src.data_ptr()), C.byref(dparams),
+                                                 C.byref(table), C.c_void_p(d_res.data_ptr()), 7, 0,
+                                                 C.c_void_p(d_ir.data_ptr())) == 0
+
+    def filt():
+        assert L.lib.bcw_compact_filter_async(ix.handle, C.c_void_p(d_src.data_ptr()), C.byref(dparams),
+                                              C.byref(table), C.c_void_p(d_res.data_ptr()), 7,
+                                              C.c_void_p(keep.data_ptr()), C.c_void_p(d_ir.data_ptr())) == 0
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    put()  # first insert of every key into the empty index (slot claims)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    first_ms = e0.elapsed_time(e1)
+    r = L.IndexResult.from_buffer_copy(bytes(d_ir.cpu().numpy()))
+    assert r.err_class == 0 and r.n_done == n_rec, (r.err_class, r.n_done)
+    e0.record(stream)
+    for _ in range(steps):
+        put()  # rebuild over an index already holding the keys (replace in place)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    put_ms = e0.elapsed_time(e1) / steps
+    keep.zero_()
+    e0.record(stream)
+    for _ in range(steps):
+        filt()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    filt_ms = e0.elapsed_time(e1) / steps
+    r = L.IndexResult.from_buffer_copy(bytes(d_ir.cpu().numpy()))
+    kept = int(keep[:n_rec].sum().item())
+    assert r.err_class == 0 and kept == n_rec, (r.err_class, kept)
+    # decode -> filter -> encode without leaving HBM (the whole device compactOneWal with doFilter)
+    e0.record(stream)
+    for _ in range(steps):
+        decode_checked_async = L.lib.bcw_decode_segment_async(ctx.handle, C.c_void_p(d_src.data_ptr()),
+                                                              C.byref(dparams), C.byref(table),
+                                                              C.c_void_p(d_res.data_ptr()))
+        assert decode_checked_async == 0
+        filt()
+        encode()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    full_ms = e0.elapsed_time(e1) / steps
+    st = ix.stats()
+    ix.close()
+    return {"rebuild_first_insert_ms": round(first_ms, 3), "rebuild_put_ms": round(put_ms, 3), "rebuild_keys_per_s": round(n_rec / (put_ms * 1e-3)),
+            "filter_ms": round(filt_ms, 3), "filter_rows_per_s": round(n_rec / (filt_ms * 1e-3)),
+            "decode_filter_encode_ms": round(full_ms, 3), "kept": kept, "index_live": int(st.live),
+            "note": "rebuild = recoverFromWal Put of every delivered row (murmur3 over ns||key, probe, last op "
+                    "wins) into a device index already holding the keys; filter = doFilter Get + (fid, off) "
+                    "compare per row; decode_filter_encode = decode + filter + re-encode + hint, all in HBM"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=10_000_000)
@@ -70,6 +138,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-index", action="store_true", help="skip the index rebuild / compaction filter leg")
     args = ap.parse_args()
     import torch
     from bitcaskdb_amd import _lib as L
@@ -210,6 +279,9 @@ def main():
         "layout_events": {"wal": int(res.wal_events), "hint": int(res.hint_events)},
         "parity": {"wal_equals_source": same, "hint_decodes_to_offsets": hint_ok},
     }
+    if not args.no_index:
+        line["index"] = index_leg(L, ctx, stream, d_src, dparams, table, d_res, n_rec, args.steps, decode_checked,
+                                  encode, keep)
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     s = json.dumps(line)

@@ -56,7 +56,7 @@ if has enc; then
   tail -1 "$OUT/benc.log" | cut -c1-600
   rm -rf "$OUT/prof_enc"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_enc" -o run --output-format csv -- \
-    python3 tools/bench_encode.py --records ${RECORDS:-10000000} --steps 3 --no-cpu-baseline > "$OUT/prof_enc.log" 2>&1 || { tail -30 "$OUT/prof_enc.log"; exit 1; }
+    python3 tools/bench_encode.py --records ${RECORDS:-10000000} --steps 3 --no-cpu-baseline --no-index > "$OUT/prof_enc.log" 2>&1 || { tail -30 "$OUT/prof_enc.log"; exit 1; }
   find "$OUT/prof_enc" -name "*stats*" | head
 fi
 echo "== done ($(date +%T))"
