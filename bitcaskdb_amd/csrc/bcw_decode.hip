@@ -1173,11 +1173,23 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
       const uint64_t base = a0 & ~15ull;
       const uint32_t sh = (uint32_t)(a0 - base);
       const uint32_t nld = (uint32_t)((sh + want + 15) >> 4);
-      if (!(ABL & 2))
-        for (uint32_t k = 0; k < nld; ++k) {
-          const uint64_t o = base + 16 * k;
-          *reinterpret_cast<uint4*>(st + 16 * k) = load16_safe(seg, seg_len, (int64_t)o);
+      if (!(ABL & 2)) {
+        // all of the record's prefix loads in flight at once (a rolled load -> LDS store loop would pay one
+        // memory round trip per 16 B); bounds-checked loads only where the prefix touches the segment end
+        uint4 v[kStageArea / 16];
+        if (base + 16ull * nld <= seg_len) {
+#pragma unroll
+          for (uint32_t k = 0; k < kStageArea / 16; ++k)
+            if (k < nld) v[k] = *reinterpret_cast<const uint4*>(seg + base + 16 * k);
+        } else {
+#pragma unroll
+          for (uint32_t k = 0; k < kStageArea / 16; ++k)
+            if (k < nld) v[k] = load16_safe(seg, seg_len, (int64_t)(base + 16 * k));
         }
+#pragma unroll
+        for (uint32_t k = 0; k < kStageArea / 16; ++k)
+          if (k < nld) *reinterpret_cast<uint4*>(st + 16 * k) = v[k];
+      }
       RecReader rd{seg, frags, p.start_off, st + sh, (uint32_t)want, src, (uint32_t)g, src, 0, f0.len, a0};
       uint8_t status, hdr, flags, etag_off;
       uint64_t key_len, val_len, meta_len, expire, aux0, aux1;
