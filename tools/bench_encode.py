@@ -187,8 +187,8 @@ def main():
                                               C.byref(table), C.c_void_p(d_res.data_ptr())) == 0
 
     def decode_checked(seg_ptr, prm):
-        # async API contract: a result with retry_frag_capacity != 0 is invalid; the next call on the
-        # context is sized for it
+        # async API contract: a result with retry_frag_capacity != 0 is invalid; reserve that many fragments
+        # on the context (bcw_ctx_reserve_fragments) and decode again
         for _ in range(2):
             assert L.lib.bcw_decode_segment_async(ctx.handle, C.c_void_p(seg_ptr), C.byref(prm), C.byref(table),
                                                   C.c_void_p(d_res.data_ptr())) == 0
@@ -196,6 +196,7 @@ def main():
             rr = L.DecodeResult.from_buffer_copy(bytes(d_res.cpu().numpy()))
             if not rr.retry_frag_capacity:
                 return rr
+            assert L.lib.bcw_ctx_reserve_fragments(ctx.handle, rr.retry_frag_capacity + 64) == 0
         raise SystemExit("decode retry failed")
 
     def encode():
