@@ -6,6 +6,9 @@ Workload (BASELINE.json configs[1], "B"): a synthetic 1 GiB bitcaskDB WAL segmen
 (bcw_synth_segment) and copied to HBM before timing. One "step" = one full decode of the
 segment through the C-ABI (bcw_decode_segment_async): header chase, CRC-32C verify of every
 fragment, record assembly and RecordFromBytes for every record into the device record table.
+An extra `pipelined` key times the same K steps rotating over --inflight (default 2) independent
+segments, each with its own context (stream, scratch, record table), as a scan over many WAL files
+runs: one segment's latency-bound kernels overlap the next one's CRC pass.
 Multi-GPU = config D: every rank decodes its own independent segment (seed 42 + rank) with no
 collective on the data path ("scaling": "weak"); the barrier + max-over-ranks timing follows the
 driver contract. Prints ONE JSON line on rank 0.
@@ -42,6 +45,9 @@ def parse():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra legs (all-core / pread CPU baselines, file-to-file end-to-end rates)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the all-core CPU baseline")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="segments in flight for the extra pipelined leg: steps rotate over this many contexts "
+                         "(own stream, segment, record table); the headline value is one segment at a time")
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events bracket every N-th k_crc launch of the timed region")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_v3_k_crc_pmc.json"),
@@ -186,95 +192,150 @@ def main():
     from bitcaskdb_amd import Context
     from bitcaskdb_amd import shard
 
-    # ---- build this rank's segment on the host with the product writer, then copy to HBM ----
-    seed = shard.segment_seed(42, rank)
+    # ---- this rank's segments: built on the host with the product writer, then copied to HBM ----
+    # A scan over many WAL files (recovery, compaction of every wal, config D) keeps `inflight` segments in
+    # flight on independent contexts, so one segment's latency-bound header chase / record emission and the
+    # kernel boundaries overlap another segment's CRC pass. Every step is still one complete decode of one
+    # whole segment; the steps rotate over the contexts.
     vmode = 0 if args.config == "B" else 1
-    n, r = C.c_uint64(), C.c_uint64()
-    rc = L.lib.bcw_synth_segment(args.seg_bytes, 0, seed, 20, 100, 4096, vmode, BASE_TIME, None, 0, C.byref(n),
-                                 C.byref(r))
-    assert rc == 0
-    host = torch.empty(n.value, dtype=torch.uint8).pin_memory()
-    rc = L.lib.bcw_synth_segment(args.seg_bytes, 0, seed, 20, 100, 4096, vmode, BASE_TIME,
-                                 C.c_void_p(host.data_ptr()), n.value, C.byref(n), C.byref(r))
-    assert rc == 0
-    seg_len, n_rec = int(n.value), int(r.value)
-    d_seg = host.to(dev, non_blocking=True)
-    torch.cuda.synchronize()
+    nslot = max(1, args.inflight)
 
-    # ---- device record table + result ----
-    cap = n_rec + 64
-    cols = {}
-    for name, dt in L.TABLE_COLUMNS:
-        tdt = {"u8": torch.int64, "u4": torch.int32, "u1": torch.uint8}[dt]
-        cols[name] = torch.empty(cap, dtype=tdt, device=dev)
+    def build_segment(seed):
+        n, r = C.c_uint64(), C.c_uint64()
+        rc = L.lib.bcw_synth_segment(args.seg_bytes, 0, seed, 20, 100, 4096, vmode, BASE_TIME, None, 0, C.byref(n),
+                                     C.byref(r))
+        assert rc == 0
+        host = torch.empty(n.value, dtype=torch.uint8).pin_memory()
+        rc = L.lib.bcw_synth_segment(args.seg_bytes, 0, seed, 20, 100, 4096, vmode, BASE_TIME,
+                                     C.c_void_p(host.data_ptr()), n.value, C.byref(n), C.byref(r))
+        assert rc == 0
+        return host, int(n.value), int(r.value)
+
     ptr_t = {"u8": L.u64p, "u4": L.u32p, "u1": L.u8p}
-    table = L.RecordTable(cap, *[C.cast(C.c_void_p(cols[name].data_ptr()), ptr_t[dt]) for name, dt in L.TABLE_COLUMNS])
-    d_res = torch.zeros(C.sizeof(L.DecodeResult), dtype=torch.uint8, device=dev)
-    params = L.DecodeParams(seg_len, BASE_TIME, 40, 20, 20, L.MODE_RECORD)
+    slots = []
+    for j in range(nslot):
+        host, seg_len, n_rec = build_segment(shard.segment_seed(42 + 1000 * j, rank))
+        d_seg = host.to(dev, non_blocking=True)
+        # ---- device record table + result ----
+        cap = n_rec + 64
+        cols = {}
+        for name, dt in L.TABLE_COLUMNS:
+            tdt = {"u8": torch.int64, "u4": torch.int32, "u1": torch.uint8}[dt]
+            cols[name] = torch.empty(cap, dtype=tdt, device=dev)
+        table = L.RecordTable(cap, *[C.cast(C.c_void_p(cols[name].data_ptr()), ptr_t[dt])
+                                     for name, dt in L.TABLE_COLUMNS])
+        d_res = torch.zeros(C.sizeof(L.DecodeResult), dtype=torch.uint8, device=dev)
+        params = L.DecodeParams(seg_len, BASE_TIME, 40, 20, 20, L.MODE_RECORD)
+        sctx = Context(torch.cuda.current_device())
+        sstream = torch.cuda.Stream()  # dedicated stream: the codec's kernels and the timing events share it
+        sctx.set_stream(sstream.cuda_stream)
+        slots.append(dict(host=host, seg_len=seg_len, n_rec=n_rec, d_seg=d_seg, cols=cols, table=table, d_res=d_res,
+                          params=params, ctx=sctx, stream=sstream))
+        if j == 0:
+            del host  # slot 0's host copy is kept in its slot (end-to-end and CPU legs)
+    torch.cuda.synchronize()
+    s0 = slots[0]
+    host, seg_len, n_rec, d_seg = s0["host"], s0["seg_len"], s0["n_rec"], s0["d_seg"]
+    table, d_res, ctx, stream = s0["table"], s0["d_res"], s0["ctx"], s0["stream"]
 
-    ctx = Context(torch.cuda.current_device())
-    stream = torch.cuda.Stream()  # dedicated stream: the codec's kernels and the timing events share it
-    ctx.set_stream(stream.cuda_stream)
-
-    def step():
-        rc = L.lib.bcw_decode_segment_async(ctx.handle, C.c_void_p(d_seg.data_ptr()), C.byref(params),
-                                            C.byref(table), C.c_void_p(d_res.data_ptr()))
+    def decode(sl):
+        rc = L.lib.bcw_decode_segment_async(sl["ctx"].handle, C.c_void_p(sl["d_seg"].data_ptr()),
+                                            C.byref(sl["params"]), C.byref(sl["table"]),
+                                            C.c_void_p(sl["d_res"].data_ptr()))
         if rc != 0:
             raise RuntimeError(L.lib.bcw_strerror(rc).decode())
 
+    def step():  # slot 0 alone (end-to-end legs)
+        decode(s0)
+
+    rot = [0]
+
+    def step_rot():
+        decode(slots[rot[0] % nslot])
+        rot[0] += 1
+
     # ---- warmup + correctness gate (not timed) ----
     for _ in range(max(args.warmup, 1)):
-        step()
+        for sl in slots:
+            decode(sl)
     torch.cuda.synchronize()
-    res = L.DecodeResult.from_buffer_copy(bytes(d_res.cpu().numpy()))
-    ok = (res.err_class == 0 and res.n_records == n_rec and res.first_bad_record == -1
-          and int((cols["status"][:n_rec] != 0).sum().item()) == 0
-          and int((cols["size"][:n_rec] <= 0).sum().item()) == 0)
-    if not ok:
-        raise SystemExit(f"rank {rank}: decode check failed: err={res.err_class} n={res.n_records}/{n_rec} "
-                         f"bad={res.first_bad_record}")
-    n_frags = int(res.n_frags)
+    n_frags = 0
+    for j, sl in enumerate(slots):
+        res = L.DecodeResult.from_buffer_copy(bytes(sl["d_res"].cpu().numpy()))
+        nr, cols = sl["n_rec"], sl["cols"]
+        ok = (res.err_class == 0 and res.n_records == nr and res.first_bad_record == -1
+              and int((cols["status"][:nr] != 0).sum().item()) == 0
+              and int((cols["size"][:nr] <= 0).sum().item()) == 0)
+        if not ok:
+            raise SystemExit(f"rank {rank} slot {j}: decode check failed: err={res.err_class} n={res.n_records}/{nr} "
+                             f"bad={res.first_bad_record}")
+        if j == 0:
+            n_frags = int(res.n_frags)
 
     # kernel ids by name (the pipeline's kernel list is the library's)
     nk = int(L.lib.bcw_ctx_kernel_times(ctx.handle, None, None, 0))
     names = [L.lib.bcw_kernel_name(k).decode() for k in range(nk)]
     roof_k = names.index("k_crc")
 
-    def kernel_times():
-        tot = (C.c_double * nk)()
-        cnt = (C.c_uint64 * nk)()
-        L.lib.bcw_ctx_kernel_times(ctx.handle, tot, cnt, nk)
-        return {names[k]: (tot[k] / cnt[k]) for k in range(nk) if cnt[k]}
+    def kernel_times(ctxs):
+        """per-kernel average over the given contexts (reading resets their accumulators)"""
+        agg_t, agg_c = [0.0] * nk, [0] * nk
+        for cx in ctxs:
+            tot = (C.c_double * nk)()
+            cnt = (C.c_uint64 * nk)()
+            L.lib.bcw_ctx_kernel_times(cx.handle, tot, cnt, nk)
+            for k in range(nk):
+                agg_t[k] += tot[k]
+                agg_c[k] += cnt[k]
+        return {names[k]: (agg_t[k] / agg_c[k], agg_c[k]) for k in range(nk) if agg_c[k]}
 
+    all_ctx = [sl["ctx"] for sl in slots]
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks ----
-    # HIP events bracket only the roofline kernel (k_crc) on the codec's stream
-    # (every --event-every-th launch: an event pair idles the GPU for a few microseconds)
-    L.lib.bcw_ctx_set_profiling(ctx.handle, 1 << roof_k)
-    L.lib.bcw_ctx_set_profiling_sample(ctx.handle, args.event_every)
+    # HIP events bracket only the roofline kernel (k_crc) on each codec stream
+    # (every --event-every-th launch: an event pair idles that stream for a few microseconds)
+    for cx in all_ctx:
+        L.lib.bcw_ctx_set_profiling(cx.handle, 1 << roof_k)
+        L.lib.bcw_ctx_set_profiling_sample(cx.handle, args.event_every)
+    kernel_times(all_ctx)  # reset (synchronises the codec streams)
+    torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-
-    kernel_times()  # reset (synchronises the codec's stream)
     ev0.record(stream)
     # warmup already ran above (with the correctness gate)
     wall = shard.timed_steps(step, args.steps, 0, torch.cuda.synchronize, dist.barrier if world > 1 else None)
     ev1.record(stream)
     torch.cuda.synchronize()
     ev_ms = ev0.elapsed_time(ev1)
-    tot = (C.c_double * nk)()
-    cnt = (C.c_uint64 * nk)()
-    L.lib.bcw_ctx_kernel_times(ctx.handle, tot, cnt, nk)
-    crc_ms, crc_samples = tot[roof_k] / cnt[roof_k], int(cnt[roof_k])
-    # every kernel's average (untimed repeat, events around each kernel)
+    crc_ms, crc_samples = kernel_times(all_ctx)["k_crc"]
+    bytes_total = seg_len * args.steps
+    # pipelined: the same K steps rotating over the in-flight segments (an extra key, never `value`: with two
+    # streams a k_crc event pair also spans the other segment's kernels)
+    pipelined = None
+    if nslot > 1:
+        for cx in all_ctx:
+            L.lib.bcw_ctx_set_profiling(cx.handle, 0)
+        wall_p = shard.timed_steps(step_rot, args.steps, 0, torch.cuda.synchronize,
+                                   dist.barrier if world > 1 else None)
+        wall_p = shard.max_over_ranks(wall_p, dist, dev)
+        bytes_p = sum(slots[i % nslot]["seg_len"] for i in range(args.steps))
+        pipelined = {"inflight": nslot, "value": round(shard.aggregate_gib_s([bytes_p / args.steps] * world, wall_p,
+                                                                               args.steps), 2),
+                     "unit": "GiB/s", "ms_per_step": round(wall_p / args.steps * 1e3, 4),
+                     "note": "steps rotate over independent segments on their own contexts/streams (a multi-file "
+                             "scan): one segment's k_chase / k_records and the kernel boundaries overlap the next "
+                             "one's k_crc"}
+    # every kernel's average, one segment at a time (untimed repeat, events around each kernel)
     L.lib.bcw_ctx_set_profiling_sample(ctx.handle, 1)
     L.lib.bcw_ctx_set_profiling(ctx.handle, -1)
     for _ in range(min(args.steps, 10)):
         step()
-    kern = kernel_times()
-    L.lib.bcw_ctx_set_profiling(ctx.handle, 0)
+    kern = {k: v[0] for k, v in kernel_times([ctx]).items()}
+    for cx in all_ctx:
+        L.lib.bcw_ctx_set_profiling(cx.handle, 0)
 
     wall_max = shard.max_over_ranks(wall, dist, dev)
     ms_per_step = wall_max / args.steps * 1e3
-    value = shard.aggregate_gib_s([seg_len] * world, wall_max, args.steps)  # same-size segment per rank
+    # whole job: this rank's bytes per step (segments of equal size on every rank, to a record) x ranks
+    value = shard.aggregate_gib_s([bytes_total / args.steps] * world, wall_max, args.steps)
 
     # end-to-end PCIe-inclusive rate (pinned H2D of the segment + decode), rank 0 only, not `value`
     pcie = None
@@ -308,7 +369,7 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_crc",
                 "kernel_ms": round(crc_ms, 4), "kernel_launches_timed": crc_samples, "alg_bytes": alg_bytes,
-                "pipeline_GBs": round(seg_len / (ms_per_step * 1e-3) / 1e9, 1),
+                "pipeline_GBs": round(bytes_total / args.steps / (ms_per_step * 1e-3) / 1e9, 1),
                 "kernel_ms_all": {k: round(v, 4) for k, v in kern.items()}}
 
     # ---- end-to-end through the host I/O staging (rank 0, N=1) ----
@@ -354,11 +415,14 @@ def main():
                                + ("4 KiB values" if args.config == "B" else "Zipf(1.1) 128 B-64 KiB values")
                                + ", device-resident decode+CRC+record parse",
                    "seg_bytes": seg_len, "records": n_rec, "fragments": n_frags,
-                   "parallelism": f"one independent segment per GPU x{world}"},
+                   "parallelism": f"one independent segment per GPU x{world}",
+                   },
         "roofline": roofline, "cpu_baseline": cpu,
         "pcie_inclusive_GiBs": round(pcie, 2) if pcie else None,
         "event_ms_per_step": round(ev_ms / args.steps, 4),
     }
+    if pipelined:
+        line["pipelined"] = pipelined
     line.update(extras)
     print(json.dumps(line), flush=True)
     if world > 1:

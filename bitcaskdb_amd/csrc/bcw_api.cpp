@@ -286,11 +286,15 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
     }
   }
   std::vector<uint32_t> image(kLdsImage);
-  for (int e = 0; e < 256; ++e)
-    for (int r = 0; r < 32; ++r) {
-      image[e * 64 + r] = slice[256 + e];  // T1: applied to the low byte of x
-      image[e * 64 + 32 + r] = slice[e];   // T0: applied to byte 1 of x
-    }
+  {  // slice-by-4 rows (see crc_window): row e = {T3[e] x16, T2[e] x16, T1[e] x16, T0[e] x16}
+    uint32_t tk[4][256];
+    byte_table(tk[0]);
+    for (int k = 1; k < 4; ++k)
+      for (int e = 0; e < 256; ++e) tk[k][e] = (tk[k - 1][e] >> 8) ^ tk[0][tk[k - 1][e] & 0xffu];
+    for (int e = 0; e < 256; ++e)
+      for (int t = 0; t < 4; ++t)
+        for (int r = 0; r < 16; ++r) image[e * 64 + t * 16 + r] = tk[3 - t][e];
+  }
   for (int i = 0; i < kLdsFwd; ++i) image[kLdsSlice + i] = fwd[(i & 63) * 128 + (i >> 6)];
   for (int i = 0; i < 128; ++i) {
     image[kLdsSlice + kLdsFwd + i] = carry[i];

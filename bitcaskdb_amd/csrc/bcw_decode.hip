@@ -522,29 +522,45 @@ constexpr int kRingWords = 10;           // cpre, cend (SoA) + 8-word entry reco
 constexpr int kWaveLds = kRing * kRingWords;
 constexpr size_t kCrcLds = (size_t)(kLdsSlice + kLdsFwd + kLdsOps + kCrcWaves * kWaveLds) * 4;
 
-// CRC-32C (zero xor-out, no final inversion) of one 128 B window from state `seed`: two slice-by-2
-// chains over the two 64 B halves, joined with the half operator A_{8*64}.
-// LDS slice layout: 256-B rows, row e = { T1[e] x32 lanes, T0[e] x32 lanes }, so the byte address of a
-// lookup is (index byte << 8) | lane slot, built by one v_perm_b32 and always on bank lane % 32.
-// Each chain carries x = state ^ next halfword: a step is perm, perm, ds_read x2, xor3.
+// CRC-32C (zero xor-out, no final inversion) of one 128 B window from state `seed`: two slice-by-4
+// chains over the two 64 B halves (16 dependent steps each), joined with the half operator A_{8*64}.
+// LDS slice layout: 256-B rows, row e = { T3[e] x16, T2[e] x16, T1[e] x16, T0[e] x16 } (T_k: a byte
+// followed by k zero bytes), so a lookup address is (index byte << 8) | table slot | lane slot, built by
+// one v_perm_b32 with a per-lane selector. Lanes 0-15 / 16-31 of each 32-lane bank group look up the
+// tables of a pair in opposite orders (T3,T2 / T2,T3, then T1,T0 / T0,T1): the two table copies of a
+// pair sit 16 banks apart, so every ds_read_b32 is conflict-free with 16 copies per table.
+// Each chain carries x = state ^ next word: a step is 4 perm, 4 ds_read, 2 xor3.
+struct SliceLane {
+  uint32_t lbx, lby;    // lane slot | table-pair slot of the first / second lookup of a pair
+  uint32_t s0, s1;      // perm selectors: byte k of x into byte 1, the lane base into byte 0
+};
+__device__ __forceinline__ SliceLane slice_lane(uint32_t lane) {
+  const bool hi = (lane & 16u) != 0u;
+  const uint32_t slot = (lane & 15u) * 4u;
+  SliceLane s;
+  s.lbx = slot + (hi ? 64u : 0u);
+  s.lby = slot + (hi ? 0u : 64u);
+  s.s0 = hi ? 0x0c0c0500u : 0x0c0c0400u;  // lanes 0-15: byte 0 -> T3 (slot 0); 16-31: byte 1 -> T2 (slot 64)
+  s.s1 = hi ? 0x0c0c0400u : 0x0c0c0500u;
+  return s;
+}
+__device__ __forceinline__ uint32_t slice4_step(const uint8_t* __restrict__ tb, const SliceLane& sl, uint32_t x,
+                                                uint32_t next) {
+  const uint32_t a0 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(x, sl.lbx, sl.s0));
+  const uint32_t a1 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(x, sl.lby, sl.s1));
+  const uint32_t a2 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(x, sl.lbx, sl.s0 + 0x200u) + 128u);
+  const uint32_t a3 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(x, sl.lby, sl.s1 + 0x200u) + 128u);
+  return a0 ^ a1 ^ a2 ^ a3 ^ next;
+}
 __device__ __forceinline__ uint32_t crc_window(const uint32_t* __restrict__ tab, const uint32_t* __restrict__ half,
-                                               uint32_t lb, uint32_t seed, const uint32_t (&w)[32]) {
+                                               const SliceLane& sl, uint32_t seed, const uint32_t (&w)[32]) {
   const uint8_t* tb = reinterpret_cast<const uint8_t*>(tab);
-  uint32_t xa = seed ^ (w[0] & 0xffffu);
-  uint32_t xb = w[16] & 0xffffu;
+  uint32_t xa = seed ^ w[0];
+  uint32_t xb = w[16];
 #pragma unroll
-  for (int q = 0; q < 32; ++q) {
-    uint32_t ha = 0, hb = 0;  // next halfword of each half
-    if (q < 31) {
-      ha = (q & 1) ? (w[(q + 1) >> 1] & 0xffffu) : (w[q >> 1] >> 16);
-      hb = (q & 1) ? (w[16 + ((q + 1) >> 1)] & 0xffffu) : (w[16 + (q >> 1)] >> 16);
-    }
-    const uint32_t a0 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(xa, lb, 0x0c0c0400u));
-    const uint32_t a1 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(xa, lb, 0x0c0c0500u) + 128u);
-    const uint32_t b0 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(xb, lb, 0x0c0c0400u));
-    const uint32_t b1 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(xb, lb, 0x0c0c0500u) + 128u);
-    xa = a0 ^ a1 ^ ((xa >> 16) ^ ha);
-    xb = b0 ^ b1 ^ ((xb >> 16) ^ hb);
+  for (int q = 0; q < 16; ++q) {
+    xa = slice4_step(tb, sl, xa, q < 15 ? w[q + 1] : 0u);
+    xb = slice4_step(tb, sl, xb, q < 15 ? w[16 + q + 1] : 0u);
   }
   uint32_t r = xb;
 #pragma unroll
@@ -735,8 +751,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   if (blockIdx.x == 0 && tid == 0) misc[M_T_CRC0] = wall_clock64();
   const uint64_t t_tables = (ABL & 512) ? wall_clock64() : 0;
   const uint32_t lane = tid & 63u;
-  const uint32_t lo = lane & 31u;
-  const uint32_t lb = lo * 4u;  // lane slot in a slice-table row
+  const SliceLane sl = slice_lane(lane);  // slice-table lookup constants
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of fragments: first window (wave-relative)
   uint32_t* r_cend = r_cpre + kRing;                 //   end of its windows
@@ -885,7 +900,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       // a fragment continuing from the previous pass: its state so far seeds lane 0's chain
       const uint32_t seed = (lane == 0u && d.cfb() > 0u) ? carry : 0u;
       if (!(ABL & 1)) {
-        v = crc_window(s_slice, s_half, lb, seed, w);
+        v = crc_window(s_slice, s_half, sl, seed, w);
       } else {
         v = seed ^ w[0] ^ w[31];
       }

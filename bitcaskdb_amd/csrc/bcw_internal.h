@@ -57,7 +57,7 @@ constexpr int kEncOpsWords = 103 * 128;
 
 // k_crc LDS table image (dwords): slice-by-2 tables as 256-B rows {T1[e] x32, T0[e] x32} (lane l
 // reads bank l % 32), lane operators transposed to [8][16][64 lanes], then the carry and half operators.
-constexpr int kLdsSlice = 2 * 256 * 32;
+constexpr int kLdsSlice = 256 * 64;  // slice-by-4 rows (crc_window)
 constexpr int kLdsFwd = 8 * 16 * 64;
 constexpr int kLdsOps = 2 * 8 * 16;
 constexpr int kLdsImage = kLdsSlice + kLdsFwd + kLdsOps;

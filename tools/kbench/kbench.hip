@@ -57,6 +57,7 @@ __global__ __launch_bounds__(1024) void k_core(const uint8_t* __restrict__ p, ui
   for (uint32_t i = threadIdx.x; i < (uint32_t)kLdsImage; i += 1024) lds[i] = img[i];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, lb = (lane & 31u) * 4u;
+  const bcw::SliceLane sl = bcw::slice_lane(lane);
   const uint64_t nw = (uint64_t)gridDim.x * 16, w0 = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
   const uint64_t per = n / 8192 / nw;
   const uint8_t* base = p + w0 * per * 8192;
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(1024) void k_core(const uint8_t* __restrict__ p, ui
 #pragma unroll
       for (int k = 0; k < 32; ++k) acc ^= wx[k];
     } else {
-      acc ^= bcw::crc_window(lds, lds + kLdsSlice + kLdsFwd + 128, lb, acc, wx);
+      acc ^= bcw::crc_window(lds, lds + kLdsSlice + kLdsFwd + 128, sl, acc, wx);
     }
 #pragma unroll
     for (int k = 0; k < 32; ++k) wx[k] = wy[k];
@@ -103,6 +104,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_depth(const uint8_t* __restrict_
   for (uint32_t i = threadIdx.x; i < (uint32_t)kLdsImage; i += WAVES * 64) lds[i] = img[i];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, lb = (lane & 31u) * 4u;
+  const bcw::SliceLane sl = bcw::slice_lane(lane);
   const uint64_t nw = (uint64_t)gridDim.x * WAVES, w0 = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
   const uint64_t per = n / 8192 / nw;
   const uint8_t* base = p + w0 * per * 8192;
@@ -126,7 +128,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_depth(const uint8_t* __restrict_
     issue(it + DEPTH, w[DEPTH]);
     if (QUAD) bcw::quad_windows_transpose(w[0], lane);
     if (CHAIN) {
-      acc ^= bcw::crc_window(lds, lds + kLdsSlice + kLdsFwd + 128, lb, acc, w[0]);
+      acc ^= bcw::crc_window(lds, lds + kLdsSlice + kLdsFwd + 128, sl, acc, w[0]);
     } else {
 #pragma unroll
       for (int k = 0; k < 32; ++k) acc ^= w[0][k];
