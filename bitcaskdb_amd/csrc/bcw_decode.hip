@@ -64,50 +64,30 @@ template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
 }
-__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v, uint32_t lane) {
-  const uint32_t rl = lane & 15u;
-  uint32_t t;
-  t = dpp_mov<0x111>(v); if (rl >= 1u) v = max(v, t);
-  t = dpp_mov<0x112>(v); if (rl >= 2u) v = max(v, t);
-  t = dpp_mov<0x114>(v); if (rl >= 4u) v = max(v, t);
-  t = dpp_mov<0x118>(v); if (rl >= 8u) v = max(v, t);
-  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v = max(v, t);
-  t = dpp_mov<0x143>(v); if (lane >= 32u) v = max(v, t);
+// zero-filled DPP move: lanes without a source (row edges, rows outside ROWMASK) read 0, so inclusive OR / ADD /
+// unsigned-MAX scans need no per-step lane conditions (one DPP-operand VALU per step)
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_z(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWMASK, 0xf, true);
+}
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_scan_z(uint32_t v, Op op) {
+  v = op(v, dpp_z<0x111>(v));
+  v = op(v, dpp_z<0x112>(v));
+  v = op(v, dpp_z<0x114>(v));
+  v = op(v, dpp_z<0x118>(v));
+  v = op(v, dpp_z<0x142, 0xa>(v));  // row 0 / 2 totals into rows 1 / 3
+  v = op(v, dpp_z<0x143, 0xc>(v));  // lane 31 into rows 2, 3
   return v;
 }
-__device__ __forceinline__ uint32_t wave_or_scan(uint32_t v, uint32_t lane) {
-  const uint32_t rl = lane & 15u;
-  uint32_t t;
-  t = dpp_mov<0x111>(v); if (rl >= 1u) v |= t;
-  t = dpp_mov<0x112>(v); if (rl >= 2u) v |= t;
-  t = dpp_mov<0x114>(v); if (rl >= 4u) v |= t;
-  t = dpp_mov<0x118>(v); if (rl >= 8u) v |= t;
-  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v |= t;
-  t = dpp_mov<0x143>(v); if (lane >= 32u) v |= t;
-  return v;
+__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v, uint32_t) {
+  return wave_scan_z(v, [](uint32_t x, uint32_t y) { return max(x, y); });
 }
-// segmented inclusive XOR scan; seg = first lane of this lane's segment
-__device__ __forceinline__ uint32_t wave_seg_xor_scan(uint32_t v, uint32_t lane, uint32_t seg) {
-  const uint32_t rl = lane & 15u;
-  uint32_t t;
-  t = dpp_mov<0x111>(v); if (rl >= 1u && lane - 1u >= seg) v ^= t;
-  t = dpp_mov<0x112>(v); if (rl >= 2u && lane - 2u >= seg) v ^= t;
-  t = dpp_mov<0x114>(v); if (rl >= 4u && lane - 4u >= seg) v ^= t;
-  t = dpp_mov<0x118>(v); if (rl >= 8u && lane - 8u >= seg) v ^= t;
-  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u && (lane & ~15u) - 1u >= seg) v ^= t;  // from lane 15 / 47
-  t = dpp_mov<0x143>(v); if (lane >= 32u && 31u >= seg) v ^= t;                       // from lane 31
-  return v;
+__device__ __forceinline__ uint32_t wave_or_scan(uint32_t v, uint32_t) {
+  return wave_scan_z(v, [](uint32_t x, uint32_t y) { return x | y; });
 }
-__device__ __forceinline__ uint32_t wave_add_scan(uint32_t v, uint32_t lane) {
-  const uint32_t rl = lane & 15u;
-  uint32_t t;
-  t = dpp_mov<0x111>(v); if (rl >= 1u) v += t;
-  t = dpp_mov<0x112>(v); if (rl >= 2u) v += t;
-  t = dpp_mov<0x114>(v); if (rl >= 4u) v += t;
-  t = dpp_mov<0x118>(v); if (rl >= 8u) v += t;
-  t = dpp_mov<0x142>(v); if ((lane & 31u) >= 16u) v += t;
-  t = dpp_mov<0x143>(v); if (lane >= 32u) v += t;
-  return v;
+__device__ __forceinline__ uint32_t wave_add_scan(uint32_t v, uint32_t) {
+  return wave_scan_z(v, [](uint32_t x, uint32_t y) { return x + y; });
 }
 
 // returns the exclusive prefix of v over the workgroup; *total = workgroup sum
@@ -617,18 +597,43 @@ __device__ __forceinline__ void load_window(const uint8_t* __restrict__ seg, uin
   }
 }
 
-// last-window fix: keep bytes < hi (hi in [109,124]), put J at [hi, hi+4), zero the rest
-// (touches words 27..31 only); branch-free per word
+// last-window fix: keep bytes < hi (hi in [109,124]), put J at [hi, hi+4), zero the rest (touches words 27..31
+// only). Compare-free like mask_first: word 27+i is below / at / right after word hi >> 2 by bits of 5-bit patterns.
 __device__ __forceinline__ void fix_last(uint32_t (&w)[32], uint32_t hi, uint32_t J) {
-  const uint32_t kh = hi >> 2, sh = 8u * (hi & 3u);
+  const uint32_t q = (hi >> 2) - 27u, sh = 8u * (hi & 3u);
   const uint64_t jj = (uint64_t)J << sh;
   const uint32_t jlo = (uint32_t)jj, jhi = (uint32_t)(jj >> 32);
-  const uint32_t keep = (uint32_t)((1ull << sh) - 1ull);  // bytes of word kh below hi
+  const uint32_t keep = (uint32_t)((1ull << sh) - 1ull);  // bytes of word hi >> 2 below hi
+  const uint32_t lt = (1u << q) - 1u, eq = 1u << q, nx = 2u << q;
 #pragma unroll
-  for (int k = 27; k < 32; ++k) {
-    const uint32_t uk = (uint32_t)k;
-    const uint32_t v = uk < kh ? w[k] : (uk == kh ? ((w[k] & keep) | jlo) : (uk == kh + 1u ? jhi : 0u));
-    w[k] = v;
+  for (int i = 0; i < 5; ++i) {
+    const uint32_t L = (uint32_t)((int32_t)(lt << (31 - i)) >> 31);
+    const uint32_t E = (uint32_t)((int32_t)(eq << (31 - i)) >> 31);
+    const uint32_t N = (uint32_t)((int32_t)(nx << (31 - i)) >> 31);
+    w[27 + i] = (w[27 + i] & (L | (E & keep))) | (E & jlo) | (N & jhi);
+  }
+}
+
+// first-window fix: zero the bytes before `lo` (the previous header / fragment), lo in [0, 127]. Piece p = lo >> 4
+// (16 B, words 4p..4p+3) holds the first data byte: earlier pieces are zeroed, piece p keeps the bytes from lo & 15
+// on (word masks mj), later pieces are kept. No lane-mask compares (their SGPR results cost hazard nops): -(g > p)
+// and -(g < p) are sign-extended single-bit extracts of two 8-bit patterns, and each word takes one bitop3 + one and.
+__device__ __forceinline__ void mask_first(uint32_t (&w)[32], uint32_t lo) {
+  const uint32_t p = lo >> 4, r = lo & 15u;
+  uint32_t mj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int32_t c = min(max((int32_t)r - 4 * j, 0), 4);  // bytes of word j below r
+    mj[j] = (uint32_t)(0xffffffffull << (8 * c));
+  }
+  const uint32_t gt = 0xfeu << p;      // bit g: g > p (kept)
+  const uint32_t lt = (1u << p) - 1u;  // bit g: g < p (zeroed)
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const uint32_t G = (uint32_t)((int32_t)(gt << (31 - g)) >> 31);
+    const uint32_t L = (uint32_t)((int32_t)(lt << (31 - g)) >> 31);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[4 * g + j] &= (mj[j] & ~L) | G;
   }
 }
 
@@ -887,15 +892,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     uint32_t v = 0;
     if ((ABL & 32) && !(ABL & 64)) quad_windows_transpose(w, lane);
     if (d.active()) {
-      if (!(ABL & 128) && d.cfb() == 0u) {  // first window: zero the bytes before the data (the previous header / fragment)
-        const uint32_t lo = d.lo(), kf = lo >> 2;
-        const uint32_t pm = 0xffffffffu << (8u * (lo & 3u));  // the word holding the first data byte
-#pragma unroll
-        for (int k2 = 0; k2 < 32; ++k2) {
-          const uint32_t m = (uint32_t)k2 < kf ? 0u : ((uint32_t)k2 == kf ? pm : 0xffffffffu);
-          w[k2] &= m;
-        }
-      }
+      if (!(ABL & 128) && d.cfb() == 0u) mask_first(w, d.lo());  // zero the bytes before the data
       if (!(ABL & 256) && d.last()) fix_last(w, d.hi(), d.J);
       // a fragment continuing from the previous pass: its state so far seeds lane 0's chain
       const uint32_t seed = (lane == 0u && d.cfb() > 0u) ? carry : 0u;
@@ -909,8 +906,12 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     }
     uint32_t U = v;
     if (!(ABL & 4)) {
+      // segment sum = prefix XOR at this lane ^ prefix XOR just before the segment's first lane (one
+      // zero-filled DPP scan and one ds_bpermute instead of a segmented scan's per-step lane conditions)
       const uint32_t segl = d.active() ? (d.cfb() > lane ? 0u : lane - d.cfb()) : lane;
-      U = wave_seg_xor_scan(v, lane, segl);
+      const uint32_t P = wave_scan_z(v, [](uint32_t x, uint32_t y) { return x ^ y; });
+      const uint32_t Pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((segl > 0u ? segl - 1u : 0u) << 2), (int)P);
+      U = segl > 0u ? P ^ Pb : P;
     }
     if (d.active() && d.last()) frags[f0 + d.fi].ok = (U == 0u) ? 1 : 0;
     carry = __builtin_amdgcn_readlane(U, 63);
