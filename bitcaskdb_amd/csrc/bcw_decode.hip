@@ -637,54 +637,6 @@ __device__ __forceinline__ void mask_first(uint32_t (&w)[32], uint32_t lo) {
   }
 }
 
-// Quad-coalesced window loads. Loading each lane's own 128 B window (lane l: 8 x 16 B at its
-// window) touches 64 windows per load instruction and streams at ~60% of HBM; instead load g
-// (g = 4*p2 + 2*w1 + w0) gives the 4 lanes of quad a the 16 B pieces 4*p2 .. 4*p2+3 of window
-// 4a + (g & 3): 64 contiguous bytes per quad. Two lane-bit <-> register-bit exchanges (DPP
-// quad_perm) then leave piece p of window W in w[4p..4p+3] of lane W.
-template <int K>
-__device__ __forceinline__ void swap_lane_reg_bit(uint32_t (&w)[32], uint32_t lane) {
-  constexpr int CTRL = K == 0 ? 0xB1 : 0x4E;  // quad_perm partner lane ^ 1 / lane ^ 2
-  const bool hi = (lane >> K) & 1u;
-#pragma unroll
-  for (int x = 0; x < 8; ++x) {
-    if (x & (1 << K)) continue;
-    const int y = x | (1 << K);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const uint32_t rx = w[4 * x + d], ry = w[4 * y + d];
-      const uint32_t px = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rx, CTRL, 0xf, 0xf, true);
-      const uint32_t py = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ry, CTRL, 0xf, 0xf, true);
-      w[4 * x + d] = hi ? py : rx;
-      w[4 * y + d] = hi ? ry : px;
-    }
-  }
-}
-__device__ __forceinline__ void quad_windows_transpose(uint32_t (&w)[32], uint32_t lane) {
-  swap_lane_reg_bit<0>(w, lane);
-  swap_lane_reg_bit<1>(w, lane);
-}
-// loads of the quad layout; woff/act: this lane's window offset (from wbase) and active flag;
-// SAFE: bounds-checked 16 B loads (windows touching the segment's ends)
-template <bool SAFE>
-__device__ __forceinline__ void load_windows_quad(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t wbase,
-                                                  uint32_t woff, bool act, uint32_t lane, uint32_t (&w)[32]) {
-  uint32_t wo[4], ac[4];
-  const uint32_t a = act ? 1u : 0u;
-  wo[0] = dpp_mov<0x00>(woff); wo[1] = dpp_mov<0x55>(woff); wo[2] = dpp_mov<0xAA>(woff); wo[3] = dpp_mov<0xFF>(woff);
-  ac[0] = dpp_mov<0x00>(a); ac[1] = dpp_mov<0x55>(a); ac[2] = dpp_mov<0xAA>(a); ac[3] = dpp_mov<0xFF>(a);
-  const uint32_t q = 16u * (lane & 3u);
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    if (ac[g & 3]) {
-      const uint32_t o = wo[g & 3] + 64u * (g >> 2) + q;
-      const uint4 v = SAFE ? load16_safe(seg, seg_len, wbase + (int64_t)o)
-                           : *reinterpret_cast<const uint4*>(seg + wbase + o);
-      w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
-    }
-  }
-}
-
 // global window geometry of a fragment (block-relative s, e)
 struct FragGeo {
   int64_t gs, GE;
@@ -715,8 +667,7 @@ struct BodyDesc {
 };
 
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
-// 4 no lane-operator / scan combine, 8 no record-state tail, 16 phase stamps, 32 quad-layout loads
-// instead of per-lane windows, 64 no quad transpose, 128 no first-window mask, 256 no last-window fix,
+// 4 no lane-operator / scan combine, 8 no record-state tail, 16 phase stamps, 128 no first-window mask, 256 no last-window fix,
 // 512 per-wave wall-clock stamps (entry, tables loaded, loop done) into lpre as u64[4] per wave, 1024 no
 // priority balancing
 template <int ABL = 0>
@@ -789,7 +740,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     const bool valid = fi < nfr;
     Frag f;
     __builtin_memcpy(&f, &pf, sizeof f);
-    if (fi + 64u < nfr) pf = reinterpret_cast<const uint4*>(frags)[f0 + fi + 64u];
+    // unconditional (a clamped index; lanes past the end reload the last descriptor): a branch would merge
+    // the old and new values right after the load, waiting for it
+    pf = reinterpret_cast<const uint4*>(frags)[f0 + (fi + 64u < nfr ? fi + 64u : nfr - 1u)];
     FragGeo geo{0, 0, 0};
     uint32_t e = 0;
     if (valid) {
@@ -868,42 +821,49 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     return d;
   };
 
-  // the window loads of one pass. Every lane loads (an inactive lane reads a fixed in-bounds window), so in
-  // the common case the pass's loads are one straight-line group of 8; only passes with a window crossing the
-  // segment's ends (its first and last bytes) take bounds-checked 16 B loads.
+  // gsafe: an in-bounds window (the wave's first block, clamped to the segment); safe_win: 128 B every lane may
+  // load without a bounds check -- that window, or the table image for segments shorter than 128 B
   const int64_t gblk = wbase + 128 > 0 ? wbase + 128 : 0;  // the wave's first block
   const int64_t gsafe = seg_len < 128 ? -1 : (gblk < (int64_t)seg_len - 128 ? gblk : (int64_t)seg_len - 128);
-  auto issue = [&](const BodyDesc& d, uint32_t (&w)[32]) {
-    if (ABL & 2) return;
-    const int64_t goff = d.active() ? wbase + d.woff : gsafe;
-    const bool inb = __all(goff >= 0 && (uint64_t)goff + 128 <= seg_len);
-    if (ABL & 32) {
-      if (inb) load_windows_quad<false>(seg, seg_len, wbase, d.woff, d.active(), lane, w);
-      else load_windows_quad<true>(seg, seg_len, wbase, d.woff, d.active(), lane, w);
-    } else if (inb) {
-      load_window(seg, seg_len, goff, true, w);
-    } else if (d.active()) {
-      load_window(seg, seg_len, goff, false, w);
-    }
-  };
+  const uint8_t* safe_win = seg_len >= 128 ? seg + gsafe : reinterpret_cast<const uint8_t*>(tabs.lds_image);
 
   uint32_t carry = 0;  // fragment state at the end of the previous pass (lane 63)
-  auto compute = [&](const BodyDesc& d, uint32_t (&w)[32]) {
+  // chain pass d in w, and load pass dn into w as the chains free its registers (the next pass's loads overlap
+  // the chain's second half and everything up to the next pass's chain, with no second window buffer); a pass
+  // whose windows touch the segment's ends takes bounds-checked loads after the chain instead
+  auto window_goff = [&](const BodyDesc& d) -> int64_t { return d.active() ? wbase + d.woff : gsafe; };
+  auto inbounds = [&](int64_t goff) { return __all(goff >= 0 && (uint64_t)goff + 128 <= seg_len); };
+  auto compute = [&](const BodyDesc& d, uint32_t (&w)[32], const BodyDesc& dn) {
+    // this pass's loads (issued at the end of the previous compute) have landed
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+    // the prefetched fragment descriptor has landed too: make it a plain value here, so that decoding it later
+    // (load_win) waits for nothing -- a wait there would be vmcnt(0) and also wait for the window loads in flight
+    asm volatile("" : "+v"(pf.x), "+v"(pf.y), "+v"(pf.z), "+v"(pf.w));
+    {  // a pass touching the segment's ends was loaded from safe_win: bounds-checked loads now
+      const int64_t goff = window_goff(d);
+      if (!(ABL & 2) && !inbounds(goff) && d.active()) load_window(seg, seg_len, goff, false, w);
+    }
+    const int64_t ngoff = window_goff(dn);
+    const bool nfast = inbounds(ngoff);
+    // unconditional loads (a pass touching the segment's ends reads safe_win here and is
+    // reloaded at the top of its compute): a branch around them makes the compiler copy each landed tuple into the
+    // loop's registers right away, waiting for it
+    const uint4* nq = reinterpret_cast<const uint4*>(nfast ? seg + ngoff : safe_win);
     uint32_t v = 0;
-    if ((ABL & 32) && !(ABL & 64)) quad_windows_transpose(w, lane);
     if (d.active()) {
       if (!(ABL & 128) && d.cfb() == 0u) mask_first(w, d.lo());  // zero the bytes before the data
       if (!(ABL & 256) && d.last()) fix_last(w, d.hi(), d.J);
-      // a fragment continuing from the previous pass: its state so far seeds lane 0's chain
-      const uint32_t seed = (lane == 0u && d.cfb() > 0u) ? carry : 0u;
-      if (!(ABL & 1)) {
-        v = crc_window(s_slice, s_half, sl, seed, w);
-      } else {
-        v = seed ^ w[0] ^ w[31];
-      }
-      // U-domain: lane l holds A_{1024(63-l)} of its window state
-      if (!(ABL & 4)) v = apply_fwd(s_fwd, lane, v);
     }
+    // a fragment continuing from the previous pass: its state so far seeds lane 0's chain
+    const uint32_t seed = (d.active() && lane == 0u && d.cfb() > 0u) ? carry : 0u;
+    if (!(ABL & 1)) {
+      v = crc_window(s_slice, s_half, sl, seed, w);
+    } else {
+      v = seed ^ w[0] ^ w[31];
+    }
+    if (!d.active()) v = 0u;
+    // U-domain: lane l holds A_{1024(63-l)} of its window state
+    if (!(ABL & 4)) v = apply_fwd(s_fwd, lane, v);
     uint32_t U = v;
     if (!(ABL & 4)) {
       // segment sum = prefix XOR at this lane ^ prefix XOR just before the segment's first lane (one
@@ -913,11 +873,23 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       const uint32_t Pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((segl > 0u ? segl - 1u : 0u) << 2), (int)P);
       U = segl > 0u ? P ^ Pb : P;
     }
+    // pass dn's loads: issued here, once the window is dead, so they stay in flight through the ring upkeep
+    // and the descriptor build of the pass after. Issued progressively inside the chains instead (into the
+    // registers each step frees) k_crc took 275 vs 235 us (kbench, one process): a load instruction that
+    // finds the texture addresser's queue full stalls the issuing wave, and inside the chain that stall
+    // lands on its latency-bound critical path.
+    if (!(ABL & 2)) {
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const uint4 q = nq[g];
+        w[4 * g + 0] = q.x; w[4 * g + 1] = q.y; w[4 * g + 2] = q.z; w[4 * g + 3] = q.w;
+      }
+    }
     if (d.active() && d.last()) frags[f0 + d.fi].ok = (U == 0u) ? 1 : 0;
     carry = __builtin_amdgcn_readlane(U, 63);
   };
 
-  // software pipeline: the next pass's windows are in flight while this pass chains
+  // software pipeline: a pass's windows are in flight while the ring upkeep and descriptor build run
   // (ABL & 16: per-phase cycle stamps for tools/kbench, summed into misc[7..9]: describe = ring upkeep +
   // descriptor + load issue, issue = unused, compute = the chain, including any wait for its loads)
   uint64_t t_desc = 0, t_issue = 0, t_comp = 0, tq = 0;
@@ -945,33 +917,33 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     else __builtin_amdgcn_s_setprio(0);
   };
   auto pipeline = [&]() {
-    // One copy of the loop body (instruction-cache footprint). At the top of an iteration wx holds pass p
-    // (chained now), wy the loads of pass p+64, dz the descriptors of pass p+128. After the chain: advance
-    // the ring, take wy into wx, issue pass p+128's loads into wy, then describe pass p+192. The first three
-    // iterations only fill the pipeline (p < 0).
-    // Measured (tools/kbench, config B): the compiler's back-edge copy of wy waits for those loads at the
-    // end of the iteration, so they overlap only the describe; issuing them before the chain instead (full
-    // overlap) is slower, 265 vs 246 us: more lane-per-window loads in flight per CU make the texture
-    // addresser (TA busy 71 % vs 50 %, one tag lookup per 16 B piece) the bottleneck.
-    uint32_t wx[32], wy[32];
-    BodyDesc dx{}, dy{}, dz{};
-    for (int64_t p = -192;;) {
-      if (p >= 0) {
-        compute(dx, wx);
-        balance((uint32_t)p + 64u);
-        stamp(t_comp);
-      }
-      p += 64;
-      if (p >= 0 && (uint64_t)p >= cbase) break;
-      advance((uint32_t)(p + 128));
+    // One window buffer: pass p chains in w, then pass p+64's loads are issued into it and stay in flight while
+    // the ring upkeep and the describe of pass p+128 run. One copy of the loop body (instruction-cache
+    // footprint).
+    uint32_t w[32];
+    advance(0u);
+    BodyDesc dc = describe(0u);
+    if (!(ABL & 2)) {  // the first pass (compute reloads it bounds-checked when it touches the segment's ends)
+      const int64_t goff = window_goff(dc);
+      const uint4* q = reinterpret_cast<const uint4*>(inbounds(goff) ? seg + goff : safe_win);
 #pragma unroll
-      for (int k2 = 0; k2 < 32; ++k2) wx[k2] = wy[k2];
-      dx = dy;
-      issue(dz, wy);
-      dy = dz;
+      for (int g = 0; g < 8; ++g) {
+        const uint4 v = q[g];
+        w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+      }
+    }
+    advance(64u);
+    BodyDesc dn = describe(64u);
+    for (uint32_t p = 0;;) {
       stamp(t_desc);
-      dz = describe((uint32_t)(p + 128));
-      stamp(t_desc);
+      compute(dc, w, dn);
+      balance(p + 64u);
+      stamp(t_comp);
+      p += 64u;
+      if (p >= cbase) break;
+      dc = dn;
+      advance(p + 64u);
+      dn = describe(p + 64u);
     }
   };
   if (nfr > 0u) pipeline();

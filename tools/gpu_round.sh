@@ -35,7 +35,7 @@ if has prof; then
   export TMPDIR=/tmp
   rm -rf "$OUT/prof"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 1; }
+    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras --inflight 1 > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 1; }
   find "$OUT/prof" -name "*stats*" | head
 fi
 if has pmc; then
@@ -44,7 +44,7 @@ if has pmc; then
   for c in FETCH_SIZE WRITE_SIZE; do
     rm -rf "$OUT/pmc_$c"
     timeout -k 10 300 rocprofv3 --pmc $c -d "$OUT/pmc_$c" -o run --output-format csv -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > "$OUT/pmc_$c.log" 2>&1 || { tail -30 "$OUT/pmc_$c.log"; exit 1; }
+      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --inflight 1 > "$OUT/pmc_$c.log" 2>&1 || { tail -30 "$OUT/pmc_$c.log"; exit 1; }
   done
   find "$OUT" -name "*counter_collection*" | head
 fi

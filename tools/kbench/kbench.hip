@@ -8,8 +8,62 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
+#include <vector>
 
 #define CK(x) do { auto e_ = (x); if (e_ != hipSuccess && e_ != 0) { fprintf(stderr, "%s:%d err %d\n", __FILE__, __LINE__, (int)e_); exit(1);} } while (0)
+
+// quad-coalesced window loads + DPP transpose (moved here from k_crc, which no longer uses them)
+namespace bcw {
+// Quad-coalesced window loads. Loading each lane's own 128 B window (lane l: 8 x 16 B at its
+// window) touches 64 windows per load instruction and streams at ~60% of HBM; instead load g
+// (g = 4*p2 + 2*w1 + w0) gives the 4 lanes of quad a the 16 B pieces 4*p2 .. 4*p2+3 of window
+// 4a + (g & 3): 64 contiguous bytes per quad. Two lane-bit <-> register-bit exchanges (DPP
+// quad_perm) then leave piece p of window W in w[4p..4p+3] of lane W.
+template <int K>
+__device__ __forceinline__ void swap_lane_reg_bit(uint32_t (&w)[32], uint32_t lane) {
+  constexpr int CTRL = K == 0 ? 0xB1 : 0x4E;  // quad_perm partner lane ^ 1 / lane ^ 2
+  const bool hi = (lane >> K) & 1u;
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    if (x & (1 << K)) continue;
+    const int y = x | (1 << K);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t rx = w[4 * x + d], ry = w[4 * y + d];
+      const uint32_t px = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rx, CTRL, 0xf, 0xf, true);
+      const uint32_t py = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ry, CTRL, 0xf, 0xf, true);
+      w[4 * x + d] = hi ? py : rx;
+      w[4 * y + d] = hi ? ry : px;
+    }
+  }
+}
+__device__ __forceinline__ void quad_windows_transpose(uint32_t (&w)[32], uint32_t lane) {
+  swap_lane_reg_bit<0>(w, lane);
+  swap_lane_reg_bit<1>(w, lane);
+}
+// loads of the quad layout; woff/act: this lane's window offset (from wbase) and active flag;
+// SAFE: bounds-checked 16 B loads (windows touching the segment's ends)
+template <bool SAFE>
+__device__ __forceinline__ void load_windows_quad(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t wbase,
+                                                  uint32_t woff, bool act, uint32_t lane, uint32_t (&w)[32]) {
+  uint32_t wo[4], ac[4];
+  const uint32_t a = act ? 1u : 0u;
+  wo[0] = dpp_mov<0x00>(woff); wo[1] = dpp_mov<0x55>(woff); wo[2] = dpp_mov<0xAA>(woff); wo[3] = dpp_mov<0xFF>(woff);
+  ac[0] = dpp_mov<0x00>(a); ac[1] = dpp_mov<0x55>(a); ac[2] = dpp_mov<0xAA>(a); ac[3] = dpp_mov<0xFF>(a);
+  const uint32_t q = 16u * (lane & 3u);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    if (ac[g & 3]) {
+      const uint32_t o = wo[g & 3] + 64u * (g >> 2) + q;
+      const uint4 v = SAFE ? bcw::load16_safe(seg, seg_len, wbase + (int64_t)o)
+                           : *reinterpret_cast<const uint4*>(seg + wbase + o);
+      w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+    }
+  }
+}
+
+}  // namespace bcw
 
 // HBM stream-read reference: sum of every 16 B word of the segment
 __global__ __launch_bounds__(256) void k_stream(const uint4* __restrict__ p, uint64_t n, uint32_t* out) {
@@ -220,6 +274,25 @@ int main(int argc, char** argv) {
                   reps, st);
   };
   const int cus = ctx->num_cus;
+  auto runv = [&](int v) -> float {
+    switch (v) {
+      case 1: return run(k_crc<1>, cus);
+      case 2: return run(k_crc<2>, cus);
+      case 128: return run(k_crc<128>, cus);
+      default: return run(k_crc<0>, cus);
+    }
+  };
+  if (argc > 4 && std::string(argv[3]) == "cmp") {  // k_crc variants interleaved in one process (same buffers)
+    const int nv = argc - 4;
+    std::vector<std::vector<float>> ts(nv);
+    for (int r = 0; r < 7; ++r)
+      for (int i = 0; i < nv; ++i) ts[i].push_back(runv(atoi(argv[4 + i])));
+    for (int i = 0; i < nv; ++i) {
+      std::sort(ts[i].begin(), ts[i].end());
+      printf("k_crc<%s>: min %.4f  median %.4f  max %.4f ms\n", argv[4 + i], ts[i][0], ts[i][3], ts[i][6]);
+    }
+    return 0;
+  }
   {
     uint32_t* dout;
     CK(hipMalloc(&dout, 4));
@@ -285,7 +358,6 @@ int main(int argc, char** argv) {
         case 256: t = run(k_crc<256>, cus); break;
         case 384: t = run(k_crc<384>, cus); break;
         case 7: t = run(k_crc<7>, cus); break;
-        case 32: t = run(k_crc<32>, cus); break;
         case 520: t = run(k_crc<520>, cus); break;
         case 1544: t = run(k_crc<1544>, cus); break;
         case 1024: t = run(k_crc<1024>, cus); break;
@@ -348,8 +420,6 @@ int main(int argc, char** argv) {
   printf("k_crc loads+comb only (no chain, no loads) %.4f ms\n", a3);
   printf("k_crc skeleton (1|2|4) %.4f ms\n", a7);
   printf("k_crc no tail   %.4f ms\n", a8);
-  const float q1 = run(k_crc<32>, cus);
-  printf("quad-layout loads: full %.4f ms\n", q1);
   const float as = timeit([&] {
     hipMemsetAsync(&s.misc[5], 0, 8, st);  // M_DONE_CRC: the last workgroup runs the aggregate scan
     k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, s.pre, s.wgagg,

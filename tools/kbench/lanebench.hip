@@ -48,7 +48,7 @@ __device__ __forceinline__ void row_transpose(uint32_t (&w)[32]) {
     }
 }
 
-template <int P>
+template <int P, int VALU = 0>
 __global__ __launch_bounds__(64 * kW) void k_pat(const uint8_t* __restrict__ p, uint64_t n, uint32_t* out, int dump) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t gw = (uint64_t)blockIdx.x * kW + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * kW;
@@ -74,6 +74,14 @@ __global__ __launch_bounds__(64 * kW) void k_pat(const uint8_t* __restrict__ p, 
     }
 #pragma unroll
     for (int k = 0; k < 32; ++k) acc = __builtin_amdgcn_alignbyte(acc, acc, 1) ^ w[k];
+    // VALU: independent 4-chain busy work per pass (issue pressure beside the loads of the next pass)
+    uint32_t c0 = acc, c1 = acc ^ 1u, c2 = acc ^ 2u, c3 = acc ^ 3u;
+#pragma unroll
+    for (int k = 0; k < VALU / 4; ++k) {
+      c0 = __builtin_amdgcn_alignbyte(c0, c1, 1); c1 = __builtin_amdgcn_alignbyte(c1, c2, 2);
+      c2 = __builtin_amdgcn_alignbyte(c2, c3, 3); c3 = __builtin_amdgcn_alignbyte(c3, c0, 1);
+    }
+    acc ^= c0 ^ c1 ^ c2 ^ c3;
   }
   if (acc == 0x12345678u) out[0] = acc;
 }
@@ -123,5 +131,14 @@ int main() {
   t[3] = timeit([&] { k_pat<3><<<cus, 64 * kW>>>(d, n, out, 0); }, reps);
   t[4] = timeit([&] { k_pat<4><<<cus, 64 * kW>>>(d, n, out, 0); }, reps);
   for (int i = 0; i < 5; ++i) printf("%-24s %.4f ms  %.0f GB/s\n", nm[i], t[i], n / (t[i] * 1e-3) / 1e9);
+  // load pattern beside VALU work per pass (per wave; 12 waves per CU = 3 per SIMD)
+  const float v0 = timeit([&] { k_pat<0, 0><<<cus, 64 * kW>>>(d, n, out, 0); }, reps);
+  const float v2 = timeit([&] { k_pat<0, 200><<<cus, 64 * kW>>>(d, n, out, 0); }, reps);
+  const float v4 = timeit([&] { k_pat<0, 400><<<cus, 64 * kW>>>(d, n, out, 0); }, reps);
+  const float v8 = timeit([&] { k_pat<0, 800><<<cus, 64 * kW>>>(d, n, out, 0); }, reps);
+  const float q4 = timeit([&] { k_pat<4, 400><<<cus, 64 * kW>>>(d, n, out, 0); }, reps);
+  const float q8 = timeit([&] { k_pat<4, 800><<<cus, 64 * kW>>>(d, n, out, 0); }, reps);
+  printf("P0 + VALU per pass: 0 %.4f  200 %.4f  400 %.4f  800 %.4f ms | P4 + 400 %.4f  800 %.4f ms\n", v0, v2, v4, v8,
+         q4, q8);
   return 0;
 }
