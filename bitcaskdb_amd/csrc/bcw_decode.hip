@@ -181,7 +181,10 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                               uint64_t nblocks, uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
                                               uint64_t frag_cap, uint64_t* __restrict__ lb, uint64_t* __restrict__ misc,
                                               uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc) {
-  __shared__ uint32_t s_hold[kChaseHold][3][64];  // {crc, start | len << 16, type} of each lane's headers
+  // {crc, start | len << 16} and type of each lane's headers: 9 KiB, so a k_chase workgroup fits beside a k_crc
+  // workgroup (which leaves 11 KiB of the CU's LDS) when another segment's decode is in flight
+  __shared__ uint32_t s_hold[kChaseHold][2][64];
+  __shared__ uint8_t s_type[kChaseHold][64];
   const uint32_t lane = threadIdx.x;
   uint64_t wg = 0;
   if (lane == 0) wg = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_TICKET]), 1ull) - ticket_base;
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                    if (k < (uint32_t)kChaseHold) {
                                      s_hold[k][0][lane] = crc;
                                      s_hold[k][1][lane] = start | (len << 16);
-                                     s_hold[k][2][lane] = type;
+                                     s_type[k][lane] = (uint8_t)type;
                                    }
                                  });
   const uint32_t incl = wave_add_scan(n, lane);
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     const uint32_t nh = n < (uint32_t)kChaseHold ? n : (uint32_t)kChaseHold;
     for (uint32_t k = 0; k < nh; ++k) {
       const uint32_t sl = s_hold[k][1][lane];
-      put_frag(frags, g0 + k, frag_cap, (uint32_t)b, sl & 0xffffu, sl >> 16, s_hold[k][0][lane], s_hold[k][2][lane],
+      put_frag(frags, g0 + k, frag_cap, (uint32_t)b, sl & 0xffffu, sl >> 16, s_hold[k][0][lane], s_type[k][lane],
                initc);
     }
     if (n > (uint32_t)kChaseHold)  // the tail of a block with more headers than held
@@ -498,7 +501,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 constexpr int kRing = 128;               // ring of multi-window fragments per wave
-constexpr int kRingWords = 10;           // cpre, cend (SoA) + 8-word entry record (AoS)
+constexpr int kRingWords = 6;            // cpre, cend (SoA) + 4-word entry record (AoS)
 constexpr int kWaveLds = kRing * kRingWords;
 constexpr size_t kCrcLds = (size_t)(kLdsSlice + kLdsFwd + kLdsOps + kCrcWaves * kWaveLds) * 4;
 
@@ -711,8 +714,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of fragments: first window (wave-relative)
   uint32_t* r_cend = r_cpre + kRing;                 //   end of its windows
-  uint4* r_ent = reinterpret_cast<uint4*>(r_cend + kRing);  // {window end (GE) - wbase, C | last hi << 16,
-                                                             //  J, len}, {fragment index, cpre, lo, -}
+  uint4* r_ent = reinterpret_cast<uint4*>(r_cend + kRing);  // {window end (GE) - wbase, C | last window's hi << 16
+                                                             //  | first window's lo << 24, J, fragment index}
   const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
   const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
   const uint64_t b0 = nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
@@ -760,9 +763,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       const uint32_t lo = (uint32_t)(geo.gs - (geo.GE - 128 * (int64_t)geo.C));  // bytes before the data
       r_cpre[a] = cbase + incl - cb;
       r_cend[a] = cbase + incl;
-      r_ent[2 * a] = make_uint4((uint32_t)(geo.GE - wbase), geo.C | ((uint32_t)(ge - (geo.GE - 128)) << 16), f.chk,
-                                f.len);
-      r_ent[2 * a + 1] = make_uint4(fi, cbase + incl - cb, lo, 0u);
+      r_ent[a] = make_uint4((uint32_t)(geo.GE - wbase), geo.C | ((uint32_t)(ge - (geo.GE - 128)) << 16) | (lo << 24),
+                            f.chk, fi);
     }
     r_tail += (uint32_t)__builtin_popcountll(vm);
     cbase += __builtin_amdgcn_readfirstlane(tot);
@@ -809,15 +811,15 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     const uint32_t a = r_head + cnt - 1u;
     if (!(cnt > 0u && j < cbase && a < r_tail)) return d;  // inactive (meta = 0)
     const uint32_t slot = a & (kRing - 1);
-    const uint4 e0 = r_ent[2 * slot], e1 = r_ent[2 * slot + 1];
+    const uint4 e0 = r_ent[slot];
     const uint32_t chl = e0.y;
-    const uint32_t cfb = j - e1.y;
+    const uint32_t cfb = j - r_cpre[slot];
     const uint32_t c = (chl & 0xffffu) - 1u - cfb;  // windows from the end (0 = last)
     d.woff = e0.x - 128u * (c + 1u);
-    d.meta = (c == 0u ? (chl >> 16) : 0u) | (cfb << 8) | ((c == 0u ? 1u : 0u) << 17) | (1u << 18) |
-             ((cfb == 0u ? e1.z : 0u) << 19);
+    d.meta = (c == 0u ? ((chl >> 16) & 0xffu) : 0u) | (cfb << 8) | ((c == 0u ? 1u : 0u) << 17) | (1u << 18) |
+             ((cfb == 0u ? (chl >> 24) : 0u) << 19);
     d.J = c == 0u ? e0.z : 0u;  // J = ~unmask(stored) ^ A_{8L}(~0) (see above), from the fragment table
-    d.fi = e1.x;
+    d.fi = e0.w;
     return d;
   };
 

@@ -62,7 +62,7 @@ constexpr int kLdsFwd = 8 * 16 * 64;
 constexpr int kLdsOps = 2 * 8 * 16;
 constexpr int kLdsImage = kLdsSlice + kLdsFwd + kLdsOps;
 #ifndef BCW_CRC_WAVES
-#define BCW_CRC_WAVES 12
+#define BCW_CRC_WAVES 16
 #endif
 constexpr int kCrcWaves = BCW_CRC_WAVES;  // waves per k_crc workgroup (one workgroup per CU)
 constexpr int kCrcThreads = kCrcWaves * 64;
