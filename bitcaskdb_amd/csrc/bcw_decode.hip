@@ -119,7 +119,9 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 // fragments of the block had the same length (a run of equal-size records, as in every 4 KiB-value
 // block), a round issues kSpec header loads at once at the positions that stride predicts and consumes
 // them while each lies exactly where the chain arrives; the round ends at the first mismatch and the
-// next one starts from the true position. Without that evidence a round reads one header.
+// next one starts from the true position. Without that evidence a round reads one header. (Speculating
+// right after the first Full fragment, until a prediction fails, measured slower: config B k_chase
+// 27.4 -> 28.2 us, config C 83 -> 91 us.)
 constexpr int kSpec = 8;
 constexpr int kChaseHold = 16;
 constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
