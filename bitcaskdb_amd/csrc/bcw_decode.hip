@@ -1085,20 +1085,40 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
   uint64_t bpw = nf ? (64 * nblocks) / nf : nblocks;
   if (bpw < 1) bpw = 1;
   const uint64_t nitems = (nblocks + bpw - 1) / bpw;
-  for (uint64_t item = (uint64_t)blockIdx.x * kRecWaves + wave; item < nitems;
-       item += (uint64_t)gridDim.x * kRecWaves) {
+  // an item's incoming state (the prefix of the k_crc wave holding its first block b, then that wave's blocks
+  // before b) and fragment range, loaded one item ahead: the next item's loads are in flight while this one
+  // emits (an unconditional load at a clamped item, so no branch merges them into a wait)
+  struct ItemIn {
+    Xf w, p, l;
+    uint32_t g0, g1;
+  };
+  const uint64_t stride = (uint64_t)gridDim.x * kRecWaves;
+  auto fetch_item = [&](uint64_t it) {
+    ItemIn r;
+    const uint64_t bi = (it < nitems ? it : nitems - 1) * bpw;
+    const uint64_t bb = bi < nblocks ? bi : nblocks - 1;
+    const uint64_t be = bb + bpw < nblocks ? bb + bpw : nblocks;
+    const uint64_t gwi = ((bb + 1) * nw - 1) / nblocks;
+    r.w = wgx[gwi / kCrcWaves];
+    r.p = wpre[gwi];
+    r.l = lpre[bb];
+    r.g0 = fbase[bb];
+    r.g1 = fbase[be];
+    return r;
+  };
+  ItemIn nxt_in = fetch_item((uint64_t)blockIdx.x * kRecWaves + wave);
+  for (uint64_t item = (uint64_t)blockIdx.x * kRecWaves + wave; item < nitems; item += stride) {
   const uint64_t b = item * bpw;
+  const ItemIn cur_in = nxt_in;
+  nxt_in = fetch_item(item + stride);
   do {  // this item's record emission
   if (b >= nblocks) break;
-  const uint64_t b_end = b + bpw < nblocks ? b + bpw : nblocks;
-  // incoming state: the prefix of the k_crc wave holding block b, then that wave's blocks before b
-  const uint64_t gw = ((b + 1) * nw - 1) / nblocks;
-  const Xf in = xf_compose(xf_compose(wgx[gw / kCrcWaves], wpre[gw]), lpre[b]);
+  const Xf in = xf_compose(xf_compose(cur_in.w, cur_in.p), cur_in.l);
   if (in.err) break;
   uint64_t acc = in.a, off = in.off;
   uint32_t first = in.first;
   uint64_t rec = in.n_emit;
-  uint64_t g0 = fbase[b], g1 = fbase[b_end];
+  uint64_t g0 = cur_in.g0, g1 = cur_in.g1;
   if (g1 > frag_cap) g1 = frag_cap;
   const uint64_t err_frag = misc[M_ERR_FRAG];
   if (g1 > err_frag) g1 = err_frag;  // nothing at or after the first failing fragment is emitted
