@@ -694,6 +694,16 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   __shared__ uint32_t s_wdone;      // waves of this workgroup done
   __shared__ uint32_t s_rem[kCrcWaves];  // windows each wave has left (balance)
   if (tid == 0) s_wdone = 0;
+  const uint32_t lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
+  const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
+  const uint64_t b0 = nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
+  // the wave's fragment range and its first descriptors are loaded while the table image crosses into LDS
+  // (that chain of dependent loads no longer follows the image copy)
+  const uint64_t f0 = fbase[b0];
+  uint64_t f1 = fbase[b1];
+  uint4 pf = make_uint4(0, 0, 0, 0);  // the next group's 64 fragment descriptors (raw; see load_win)
   {  // table image -> LDS: all 16 B loads in flight before the first store
     constexpr uint32_t kVec = kLdsImage / 4;
     constexpr int kFull = (int)(kVec / kCrcThreads);
@@ -703,7 +713,11 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
 #pragma unroll
     for (int k2 = 0; k2 < kFull; ++k2) v[k2] = src[tid + k2 * kCrcThreads];
     const uint32_t tail = tid + kFull * kCrcThreads;
-    if (tail < kVec) dst[tail] = src[tail];
+    uint4 vt = make_uint4(0, 0, 0, 0);
+    if (tail < kVec) vt = src[tail];
+    if (f1 > frag_cap) f1 = frag_cap;
+    if (f0 + lane < f1) pf = reinterpret_cast<const uint4*>(frags)[f0 + lane];
+    if (tail < kVec) dst[tail] = vt;
 #pragma unroll
     for (int k2 = 0; k2 < kFull; ++k2) dst[tid + k2 * kCrcThreads] = v[k2];
   }
@@ -711,30 +725,20 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
 
   if (blockIdx.x == 0 && tid == 0) misc[M_T_CRC0] = wall_clock64();
   const uint64_t t_tables = (ABL & 512) ? wall_clock64() : 0;
-  const uint32_t lane = tid & 63u;
   const SliceLane sl = slice_lane(lane);  // slice-table lookup constants
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* r_cpre = s_wave_all + wave * kWaveLds;  // ring of fragments: first window (wave-relative)
   uint32_t* r_cend = r_cpre + kRing;                 //   end of its windows
   uint4* r_ent = reinterpret_cast<uint4*>(r_cend + kRing);  // {window end (GE) - wbase, C | last window's hi << 16
                                                              //  | first window's lo << 24, J, fragment index}
-  const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
-  const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
-  const uint64_t b0 = nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
-  const uint64_t f0 = fbase[b0];
   const int64_t wbase = (int64_t)start_off + (int64_t)b0 * kBlock - 128;  // below every window of the wave
-  uint64_t f1 = fbase[b1];
-  if (f1 > frag_cap) f1 = frag_cap;
   const uint32_t nfr = f1 > f0 ? (uint32_t)(f1 - f0) : 0u;
   const uint32_t nwin = (nfr + 63u) / 64u;
 
   uint32_t r_head = 0, r_tail = 0;  // absolute ring positions (wave-uniform)
   uint32_t cbase = 0;               // windows appended so far
   uint32_t kwin = 0;                // next group of 64 fragments to append
-  // the next group's fragment descriptor, loaded one group ahead as a raw 16 B vector (decoded only when the
+  // pf: the next group's fragment descriptor, loaded one group ahead as a raw 16 B vector (decoded only when the
   // group is appended, so the load does not make the compiler wait for it -- and the window loads -- early)
-  uint4 pf = make_uint4(0, 0, 0, 0);
-  if (lane < nfr) pf = reinterpret_cast<const uint4*>(frags)[f0 + lane];
 
   // Group kwin (64 fragments, one per lane): every fragment is appended to the ring with its C windows
   // (GE tiling, see above); the group after it is prefetched. No window is loaded here: the first window
