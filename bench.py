@@ -50,7 +50,7 @@ def parse():
                          "(own stream, segment, record table); the headline value is one segment at a time")
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events bracket every N-th k_crc launch of the timed region")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_v5_k_crc_pmc.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_v6_k_crc_pmc.json"),
                     help="PMC traffic summary (rocprofv3 --pmc of this command) to report as roofline.traffic")
     return ap.parse_args()
 
