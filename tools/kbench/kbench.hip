@@ -219,7 +219,8 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> h(n);
   CK(bcw_synth_segment(target, 0, 42, 20, 100, 4096, mode, 1700000000, h.data(), n, &n, &r));
   uint8_t* d;
-  CK(hipMalloc(&d, n));
+  if (getenv("KB_CONTIG")) CK(hipExtMallocWithFlags((void**)&d, n, hipDeviceMallocContiguous));  // physically contiguous
+  else CK(hipMalloc(&d, n));
   CK(hipMemcpy(d, h.data(), n, hipMemcpyHostToDevice));
   bcw_record_table t{};
   void* mem;
@@ -278,7 +279,9 @@ int main(int argc, char** argv) {
     switch (v) {
       case 1: return run(k_crc<1>, cus);
       case 2: return run(k_crc<2>, cus);
+      case 8: return run(k_crc<8>, cus);
       case 128: return run(k_crc<128>, cus);
+      case 1024: return run(k_crc<1024>, cus);
       default: return run(k_crc<0>, cus);
     }
   };
