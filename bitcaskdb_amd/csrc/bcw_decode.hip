@@ -125,6 +125,7 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 constexpr int kSpec = 8;
 constexpr int kChaseHold = 16;
 constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
+constexpr int kDirect = 1024;  // k_chase workgroups up to which each sums all predecessors' aggregates
 
 // visit(k, start, len, crc, type) for every header of the block; returns the fragment count
 template <typename V>
@@ -209,31 +210,58 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                  });
   const uint32_t incl = wave_add_scan(n, lane);
   const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
-  // publish, then look back 64 workgroups per step
+  // publish, then sum the predecessors. Up to kDirect workgroups (a 2 GiB segment) every workgroup publishes
+  // only its aggregate and sums all of its predecessors' at once (up to kDirect / 64 loads per lane, all in
+  // flight); beyond that, the decoupled look-back (64 predecessors per step, stopping at the nearest
+  // inclusive prefix), whose chain of inclusive prefixes would otherwise serialize the workgroups.
   const uint64_t tag = epoch << 40;
-  if (lane == 0)
-    __hip_atomic_store(&lb[wg], tag | ((wg == 0 ? kLbInc : kLbAgg) << 38) | tot, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t nwg_all = (nblocks + 63) / 64;
   uint64_t excl = 0;
-  for (uint64_t top = wg; top > 0;) {  // predecessors [top - 64, top)
-    const uint64_t q = top - 1 - lane;  // lane 0: the nearest
-    uint64_t v = 0;
-    if (top > lane) {
-      while (((v = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
-        __builtin_amdgcn_s_sleep(1);
+  if (nwg_all <= (uint64_t)kDirect) {
+    if (lane == 0) __hip_atomic_store(&lb[wg], tag | (kLbAgg << 38) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t v[kDirect / 64];
+#pragma unroll
+    for (int k = 0; k < kDirect / 64; ++k) {
+      const uint64_t q = lane + 64u * k;
+      v[k] = q < wg ? __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
     }
-    const uint64_t inc = __ballot(top > lane && ((v >> 38) & 3u) == kLbInc);
-    const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive prefix
-    uint64_t c = (lane <= stop && top > lane) ? (v & kLbMask) : 0ull;
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kDirect / 64; ++k) {
+      const uint64_t q = lane + 64u * k;
+      while ((v[k] >> 40) != epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        v[k] = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (q < wg) c += v[k] & kLbMask;
+    }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) c += (uint64_t)__shfl_xor((long long)c, d, 64);
-    excl += c;
-    if (inc) break;
-    top = top > 64 ? top - 64 : 0;
+    excl = c;
+  } else {
+    if (lane == 0)
+      __hip_atomic_store(&lb[wg], tag | ((wg == 0 ? kLbInc : kLbAgg) << 38) | tot, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t top = wg; top > 0;) {  // predecessors [top - 64, top)
+      const uint64_t q = top - 1 - lane;  // lane 0: the nearest
+      uint64_t v = 0;
+      if (top > lane) {
+        while (((v = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      const uint64_t inc = __ballot(top > lane && ((v >> 38) & 3u) == kLbInc);
+      const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive prefix
+      uint64_t c = (lane <= stop && top > lane) ? (v & kLbMask) : 0ull;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) c += (uint64_t)__shfl_xor((long long)c, d, 64);
+      excl += c;
+      if (inc) break;
+      top = top > 64 ? top - 64 : 0;
+    }
+    if (lane == 0 && wg != 0)
+      __hip_atomic_store(&lb[wg], tag | (kLbInc << 38) | ((excl + tot) & kLbMask), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (lane == 0 && wg != 0)
-    __hip_atomic_store(&lb[wg], tag | (kLbInc << 38) | ((excl + tot) & kLbMask), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t g0 = excl + incl - n;
   if (b < nblocks) {
     fbase[b] = (uint32_t)(g0 < 0xffffffffull ? g0 : 0xffffffffull);
