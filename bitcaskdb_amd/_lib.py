@@ -141,6 +141,8 @@ def _load():
         "bcw_index_reserve": (C.c_int, [vp, C.c_uint64, C.c_uint64]),
         "bcw_index_stats": (C.c_int, [vp, C.POINTER(IndexInfo)]),
         "bcw_index_apply": (C.c_int, [vp, C.c_uint64, vp, u64p, u8p, u64p, u64p, u64p]),
+        "bcw_index_apply_stat": (C.c_int, [vp, C.c_uint64, vp, u64p, u8p, u64p, u64p, u64p, u8p, u64p, u64p]),
+        "bcw_index_clear": (C.c_int, [vp]),
         "bcw_index_get": (C.c_int, [vp, C.c_uint64, vp, u64p, u64p, u64p, u64p, u8p]),
         "bcw_index_put_decoded_async": (C.c_int, [vp, vp, C.POINTER(DecodeParams), C.POINTER(RecordTable), vp,
                                                   C.c_uint64, C.c_int, vp]),

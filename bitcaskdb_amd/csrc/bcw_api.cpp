@@ -274,12 +274,12 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
   build_initc(initc.data());
   std::vector<uint32_t> enc_ops(kEncOpsWords);
   build_enc_ops(enc_ops.data());
-  std::vector<uint32_t> pow2(15 * 128);
+  std::vector<uint32_t> pow2(kPow2Ops * 128);
   {
     uint32_t t0[256], img[32], sq[32];
     byte_table(t0);
     shift_basis(t0, 1, img);  // A_8, then repeated squaring: A_{8*2^(k+1)} = A_{8*2^k} o A_{8*2^k}
-    for (int k = 0; k < 15; ++k) {
+    for (int k = 0; k < kPow2Ops; ++k) {
       nibble_image(img, pow2.data() + k * 128);
       for (int i = 0; i < 32; ++i) sq[i] = apply_basis(img, img[i]);
       memcpy(img, sq, sizeof img);
@@ -816,6 +816,7 @@ int bcw_encode_segment(bcw_ctx* c, const uint8_t* h_src, const bcw_encode_params
 int bcw_compact_segment(bcw_ctx* c, bcw_index* ix, const uint8_t* h_src, const bcw_encode_params* p, uint64_t src_fid,
                         const bcw_encode_out* h, bcw_encode_result* h_result, bcw_index_result* h_filter) {
   if (!c || !ix || !p || !h || !h_result || p->mode != BCW_ENC_COMPACT) return BCW_E_INVAL;
+  if (index_ctx(ix) != c) return BCW_E_INVAL;  // the filter runs on the index's context (stream, fragment table)
   if (p->src_len && !h_src) return BCW_E_INVAL;
   DeviceGuard dg(c->device);
   if (!dg.ok) return BCW_E_HIP;
@@ -836,6 +837,7 @@ int bcw_index_recover_segment(bcw_ctx* c, bcw_index* ix, const uint8_t* h_seg, c
                               uint64_t fid, int use_record_fid, bcw_decode_result* h_dres,
                               bcw_index_result* h_out) {
   if (!c || !ix || !p || !h_out) return BCW_E_INVAL;
+  if (index_ctx(ix) != c) return BCW_E_INVAL;  // the puts run on the index's context (stream, fragment table)
   if (p->seg_len && !h_seg) return BCW_E_INVAL;
   DeviceGuard dg(c->device);
   if (!dg.ok) return BCW_E_HIP;

@@ -13,13 +13,18 @@
 // Layout (HBM): an open-addressing slot table (64 B slots, power-of-two capacity, linear probing from
 // the hash) and a grow-only key arena of {hash, length, key bytes padded to 16} entries.
 // A batch of operations (host-supplied, or every delivered row of a decoded record / hint table) runs
-// as four stream-ordered launches, so every cross-workgroup hand-off is a kernel boundary:
-//   k_ix_keys   one lane per op: the merged key's 16 B chunks (gathered from the WAL segment when the
-//               ops come from a decoded table), murmur3 over them, the arena entry
-//   k_ix_claim  probe from the hash: claim an empty slot with a 64-bit CAS on its key reference, or
-//               find the slot already holding the key (arena compare)
+// as five stream-ordered launches, so every cross-workgroup hand-off is a kernel boundary:
+//   k_ix_keys   one lane per op: murmur3 over the merged key's 16 B chunks (gathered from the WAL segment
+//               when the ops come from a decoded table)
+//   k_ix_claim  probe from the hash: find the slot holding the key (arena compare), or claim an empty
+//               slot with a 64-bit CAS of a provisional reference to the op itself (ops of the batch
+//               compare their keys straight from the source); an op that finds its key records the
+//               value it replaces (WriteStat)
 //   k_ix_seq    atomicMax of the op's sequence number into its slot: the last op of a key wins, as
 //               in the reference's sequential loop
+//   k_ix_commit the op that claimed a slot copies its key into the arena and makes the slot's reference
+//               permanent: only keys new to the index take arena space (a rebuild over existing keys
+//               takes none)
 //   k_ix_write  the winning op writes the value / presence
 // Lookups (Get, the compaction filter) are one launch: hash, probe, compare.
 #include <hip/hip_runtime.h>
@@ -27,6 +32,9 @@
 #include <algorithm>
 #include <cstring>
 #include <new>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
 
 #include "bcw_internal.h"
 
@@ -34,7 +42,7 @@ namespace bcw {
 namespace ix {
 
 struct Slot {
-  uint64_t kref;  // 0: empty; else 1 + arena offset of the key entry (set once, by CAS)
+  uint64_t kref;  // 0: empty; 1 + arena offset of the key entry; kProv | op: claimed by op of the running batch
   uint64_t seq;   // sequence number of the last op applied to this key
   uint64_t hash;  // murmur3 Sum64 of the merged key
   uint64_t fid, off, size;
@@ -43,8 +51,10 @@ struct Slot {
 };
 static_assert(sizeof(Slot) == 64, "Slot layout");
 
-// device counters
-enum { C_ARENA = 0, C_SLOTS = 1, C_LIVE = 2, C_OVERFLOW = 3, C_NIN = 4, C_DONE = 5, C_FAIL = 6, C_NUM = 8 };
+constexpr uint64_t kProv = 1ull << 63;  // provisional slot reference (claim -> commit inside one batch)
+
+// device counters (C_NEED: arena bytes the rows of a decoded table would take, k_ix_need)
+enum { C_ARENA = 0, C_SLOTS = 1, C_LIVE = 2, C_OVERFLOW = 3, C_NIN = 4, C_DONE = 5, C_FAIL = 6, C_NEED = 7, C_NUM = 8 };
 
 // op sources
 enum { SRC_FLAT = 0, SRC_RECORD = 1, SRC_HINT = 2 };
@@ -180,7 +190,14 @@ __device__ __forceinline__ Key make_key(const Src& s, uint64_t i) {
   k.la = s.ns;
   k.pa = s.kind == SRC_RECORD ? 1u : 0u;  // RecordFromBytes: data[1:1+NsSize]; HintRecord: data[0:NsSize]
   k.lb = t.key_len[i];
-  k.pb = t.hdr_size[i];                   // record: headerSize (key offset); hint: key offset
+  k.pb = t.hdr_size[i];                   // record: headerSize (key offset); hint: key offset mod 256
+  if (s.kind == SRC_HINT && s.ns > 245u) {
+    // the hint key offset NsSize + len(uvarint keyLen) (hint.go:62-66) no longer fits the table's u8 column:
+    // count the varint's bytes in the payload (HintRecord.Decode accepted it, so it ends within 10 bytes)
+    uint32_t u = 1;
+    while (u < 10u && (payload_byte(s, k.f0, k.f1, (uint64_t)s.ns + u - 1) & 0x80u)) ++u;
+    k.pb = s.ns + u;
+  }
   k.ca = (uint64_t)k.pa + k.la <= l0;
   k.cb = (uint64_t)k.pb + k.lb <= l0;
   k.a0 = (int64_t)(d0 + k.pa);
@@ -260,11 +277,10 @@ __device__ __forceinline__ uint64_t wave_alloc(uint64_t* ctr, uint64_t v) {
   return base + incl - v;
 }
 
-// ---- batch launch 1: keys into the arena --------------------------------------------------------
+// ---- batch launch 1: key hashes ----------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ix_keys(Src s, uint64_t n, const bcw_decode_result* __restrict__ R,
-                                                 uint64_t gen, uint8_t* __restrict__ arena, uint64_t arena_cap,
-                                                 uint64_t* __restrict__ cnt, uint64_t* __restrict__ op_kref,
-                                                 uint64_t* __restrict__ op_hash) {
+                                                 uint64_t gen, uint64_t* __restrict__ cnt,
+                                                 uint64_t* __restrict__ op_kref, uint64_t* __restrict__ op_hash) {
   const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
   uint64_t nin = n;
   if (s.kind != SRC_FLAT) {
@@ -272,73 +288,78 @@ __global__ __launch_bounds__(256) void k_ix_keys(Src s, uint64_t n, const bcw_de
     nin = fail ? 0 : delivered_rows(R);
     if (i == 0) { cnt[C_NIN] = nin; cnt[C_FAIL] = fail; }
   }
-  const bool act = i < nin;
-  Key k{};
-  if (act) k = make_key(s, i);
-  const uint64_t esz = act ? 16ull + (((uint64_t)k.len() + 15) & ~15ull) : 0;
-  const uint64_t a = wave_alloc(&cnt[C_ARENA], esz);
-  if (!act) return;
-  if (a + esz > arena_cap) {  // the host sizes the arena before the launch; never expected
-    atomicOr(reinterpret_cast<unsigned long long*>(&cnt[C_OVERFLOW]), 1ull);
-    op_kref[i] = 0;
-    return;
-  }
-  uint8_t* e = arena + a;
-  Murmur m;
-  const uint32_t L = k.len(), nb = (L + 15) / 16, t = L & 15u;
-  uint4 v = make_uint4(0, 0, 0, 0);
-  for (uint32_t c = 0; c < nb; ++c) {
-    v = key_chunk(s, k, c);
-    *reinterpret_cast<uint4*>(e + 16 + 16 * c) = v;
-    if (16 * c + 16 <= L) m.block((uint64_t)v.x | ((uint64_t)v.y << 32), (uint64_t)v.z | ((uint64_t)v.w << 32));
-  }
-  if (!t) v = make_uint4(0, 0, 0, 0);
-  const uint64_t h = m.finish((uint64_t)v.x | ((uint64_t)v.y << 32), (uint64_t)v.z | ((uint64_t)v.w << 32), t, L);
-  *reinterpret_cast<uint4*>(e) = make_uint4((uint32_t)h, (uint32_t)(h >> 32), L, 0u);
-  op_kref[i] = a + 1;
-  op_hash[i] = h;
+  if (i >= nin) return;
+  const Key k = make_key(s, i);
+  op_hash[i] = key_hash(s, k);
+  op_kref[i] = kProv | i;  // the op's own provisional reference (its key is read from the source)
 }
 
-// the arena entries at a and b hold the same key (lengths given)
-__device__ __forceinline__ bool arena_equal(const uint8_t* __restrict__ arena, uint64_t a, uint64_t b, uint32_t L) {
-  const uint4* p = reinterpret_cast<const uint4*>(arena + a + 16);
-  const uint4* q = reinterpret_cast<const uint4*>(arena + b + 16);
+// the arena entry at offset a holds op k's key (length L)
+__device__ __forceinline__ bool arena_matches(const Src& s, const Key& k, const uint8_t* __restrict__ arena,
+                                              uint64_t a, uint32_t L) {
+  const uint4* q = reinterpret_cast<const uint4*>(arena + a + 16);
   for (uint32_t c = 0; c < (L + 15) / 16; ++c) {
-    const uint4 x = p[c], y = q[c];
+    const uint4 x = key_chunk(s, k, c), y = q[c];
+    if (x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w) return false;
+  }
+  return true;
+}
+// ops k and kj of the batch have the same key (lengths equal)
+__device__ __forceinline__ bool keys_match(const Src& s, const Key& k, const Key& kj, uint32_t L) {
+  for (uint32_t c = 0; c < (L + 15) / 16; ++c) {
+    const uint4 x = key_chunk(s, k, c), y = key_chunk(s, kj, c);
     if (x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w) return false;
   }
   return true;
 }
 
-// ---- batch launch 2: claim or find each op's slot --------------------------------------------------
-__global__ __launch_bounds__(256) void k_ix_claim(uint64_t n, const uint64_t* __restrict__ cnt_in, int flat,
+// ---- batch launch 2: find or claim each op's slot --------------------------------------------------
+// old_*: per op, the value the slot held before the batch when the key existed (WriteStat of the key's first
+// op in the batch; the host composes the later ones, bcw_index_apply_stat)
+__global__ __launch_bounds__(256) void k_ix_claim(Src s, uint64_t n, const uint64_t* __restrict__ cnt_in,
                                                   Slot* __restrict__ slots, uint64_t mask,
                                                   const uint8_t* __restrict__ arena, uint64_t* __restrict__ cnt,
                                                   const uint64_t* __restrict__ op_kref,
-                                                  const uint64_t* __restrict__ op_hash, uint64_t* __restrict__ op_slot) {
+                                                  const uint64_t* __restrict__ op_hash, uint64_t* __restrict__ op_slot,
+                                                  uint8_t* __restrict__ old_found, uint64_t* __restrict__ old_fid,
+                                                  uint64_t* __restrict__ old_size) {
   const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
-  const uint64_t nin = flat ? n : cnt_in[C_NIN];
+  const uint64_t nin = s.kind == SRC_FLAT ? n : cnt_in[C_NIN];
   bool claimed = false;
   if (i < nin) {
-    const uint64_t kr = op_kref[i];
     uint64_t slot = ~0ull;
-    if (kr) {
+    uint8_t found = 0;
+    uint64_t ofid = 0, osize = 0;
+    if (op_kref[i]) {
       const uint64_t h = op_hash[i];
-      const uint32_t L = *reinterpret_cast<const uint32_t*>(arena + (kr - 1) + 8);
+      const Key k = make_key(s, i);
+      const uint32_t L = k.len();
       uint64_t j = h & mask;
       for (uint64_t probe = 0; probe <= mask; ++probe, j = (j + 1) & mask) {
-        const uint64_t c = atomicCAS(reinterpret_cast<unsigned long long*>(&slots[j].kref), 0ull,
-                                     (unsigned long long)kr);
-        if (c == 0) { slot = j; claimed = true; slots[j].hash = h; break; }
-        const uint4 hd = *reinterpret_cast<const uint4*>(arena + (c - 1));
-        if (((uint64_t)hd.x | ((uint64_t)hd.y << 32)) == h && hd.z == L && arena_equal(arena, kr - 1, c - 1, L)) {
-          slot = j;
-          break;
+        uint64_t c = __hip_atomic_load(&slots[j].kref, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c == 0) {
+          c = atomicCAS(reinterpret_cast<unsigned long long*>(&slots[j].kref), 0ull, (unsigned long long)(kProv | i));
+          if (c == 0) { slot = j; claimed = true; break; }
+        }
+        if (c & kProv) {  // claimed by another op of this batch: compare with its key at the source
+          const uint64_t o = c & ~kProv;
+          if (op_hash[o] != h) continue;
+          const Key ko = make_key(s, o);
+          if (ko.len() == L && keys_match(s, k, ko, L)) { slot = j; break; }
+        } else {
+          const uint4 hd = *reinterpret_cast<const uint4*>(arena + (c - 1));
+          if (((uint64_t)hd.x | ((uint64_t)hd.y << 32)) == h && hd.z == L && arena_matches(s, k, arena, c - 1, L)) {
+            slot = j;
+            const Slot S = slots[j];  // values are only written by k_ix_write, after this launch
+            if (S.live) { found = 1; ofid = S.fid; osize = S.size; }
+            break;
+          }
         }
       }
       if (slot == ~0ull) atomicOr(reinterpret_cast<unsigned long long*>(&cnt[C_OVERFLOW]), 2ull);
     }
     op_slot[i] = slot;
+    if (old_found) { old_found[i] = found; old_fid[i] = ofid; old_size[i] = osize; }
   }
   (void)wave_alloc(&cnt[C_SLOTS], claimed ? 1ull : 0ull);
 }
@@ -355,7 +376,50 @@ __global__ __launch_bounds__(256) void k_ix_seq(uint64_t n, const uint64_t* __re
   atomicMax(reinterpret_cast<unsigned long long*>(&slots[s].seq), (unsigned long long)(seq_base + i));
 }
 
-// ---- batch launch 4: values ---------------------------------------------------------------------------
+// ---- batch launch 4: the claiming op copies its key into the arena ------------------------------------
+__global__ __launch_bounds__(256) void k_ix_commit(Src s, uint64_t n, uint64_t* __restrict__ cnt,
+                                                   Slot* __restrict__ slots, uint8_t* __restrict__ arena,
+                                                   uint64_t arena_cap, const uint64_t* __restrict__ op_hash,
+                                                   const uint64_t* __restrict__ op_slot) {
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  const uint64_t nin = s.kind == SRC_FLAT ? n : cnt[C_NIN];
+  bool own = false;
+  uint64_t sl = ~0ull;
+  Key k{};
+  if (i < nin) {
+    sl = op_slot[i];
+    own = sl != ~0ull && slots[sl].kref == (kProv | i);
+    if (own) k = make_key(s, i);
+  }
+  const uint64_t esz = own ? 16ull + (((uint64_t)k.len() + 15) & ~15ull) : 0;
+  const uint64_t a = wave_alloc(&cnt[C_ARENA], esz);
+  if (!own) return;
+  if (a + esz > arena_cap) {  // the host sizes the arena before the launch; never expected
+    atomicOr(reinterpret_cast<unsigned long long*>(&cnt[C_OVERFLOW]), 1ull);
+    slots[sl].kref = 0;
+    return;
+  }
+  uint8_t* e = arena + a;
+  const uint32_t L = k.len();
+  for (uint32_t c = 0; c < (L + 15) / 16; ++c) *reinterpret_cast<uint4*>(e + 16 + 16 * c) = key_chunk(s, k, c);
+  const uint64_t h = op_hash[i];
+  *reinterpret_cast<uint4*>(e) = make_uint4((uint32_t)h, (uint32_t)(h >> 32), L, 0u);
+  slots[sl].hash = h;
+  slots[sl].kref = a + 1;
+}
+
+// arena bytes the delivered rows of a decoded table would take if every key were new (the exact bound the
+// host reads when its cheap bound does not fit the arena)
+__global__ __launch_bounds__(256) void k_ix_need(Src s, uint64_t rows, const bcw_decode_result* __restrict__ R,
+                                                 uint64_t gen, uint64_t* __restrict__ cnt) {
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  const uint64_t nin = table_fail(R, gen, rows) ? 0 : delivered_rows(R);
+  uint64_t b = 0;
+  if (i < nin) b = 16ull + (((uint64_t)s.ns + s.t.key_len[i] + 15) & ~15ull);
+  (void)wave_alloc(&cnt[C_NEED], b);
+}
+
+// ---- batch launch 5: values ---------------------------------------------------------------------------
 struct OpVals {
   // flat ops (host arrays copied to the device): op code and value per op
   const uint8_t* op;
@@ -601,6 +665,10 @@ struct bcw_index {
   bcw_index_result* d_res = nullptr;
 };
 
+namespace bcw {
+bcw_ctx* index_ctx(const bcw_index* ix) { return ix ? ix->ctx : nullptr; }
+}  // namespace bcw
+
 namespace {
 
 constexpr double kMaxLoad = 0.7;
@@ -692,17 +760,18 @@ int ix_stage(bcw_index* x, uint64_t bytes) {
   return BCW_OK;
 }
 
-// the four launches of a batch (ops [0, n) of src)
-void ix_batch(bcw_index* x, const Src& s, uint64_t n, const bcw_decode_result* R, uint64_t gen, const OpVals& v) {
+// the five launches of a batch (ops [0, n) of src); old_*: optional WriteStat outputs of k_ix_claim
+void ix_batch(bcw_index* x, const Src& s, uint64_t n, const bcw_decode_result* R, uint64_t gen, const OpVals& v,
+              uint8_t* old_found = nullptr, uint64_t* old_fid = nullptr, uint64_t* old_size = nullptr) {
   hipStream_t st = x->ctx->cur;
   const uint32_t grid = (uint32_t)((n + 255) / 256);
-  const int flat = s.kind == SRC_FLAT;
   (void)hipMemsetAsync(x->cnt + C_NIN, 0, 3 * sizeof(uint64_t), st);  // C_NIN, C_DONE, C_FAIL
   if (!grid) return;
-  k_ix_keys<<<grid, 256, 0, st>>>(s, n, R, gen, x->arena, x->arena_cap, x->cnt, x->op_kref, x->op_hash);
-  k_ix_claim<<<grid, 256, 0, st>>>(n, x->cnt, flat, x->slots, x->cap - 1, x->arena, x->cnt, x->op_kref, x->op_hash,
-                                   x->op_slot);
-  k_ix_seq<<<grid, 256, 0, st>>>(n, x->cnt, flat, x->slots, x->op_slot, x->seq_base);
+  k_ix_keys<<<grid, 256, 0, st>>>(s, n, R, gen, x->cnt, x->op_kref, x->op_hash);
+  k_ix_claim<<<grid, 256, 0, st>>>(s, n, x->cnt, x->slots, x->cap - 1, x->arena, x->cnt, x->op_kref, x->op_hash,
+                                   x->op_slot, old_found, old_fid, old_size);
+  k_ix_seq<<<grid, 256, 0, st>>>(n, x->cnt, s.kind == SRC_FLAT, x->slots, x->op_slot, x->seq_base);
+  k_ix_commit<<<grid, 256, 0, st>>>(s, n, x->cnt, x->slots, x->arena, x->arena_cap, x->op_hash, x->op_slot);
   k_ix_write<<<grid, 256, 0, st>>>(s, n, x->cnt, v, x->slots, x->op_slot, x->seq_base);
   x->seq_base += n;
 }
@@ -781,9 +850,12 @@ int bcw_index_stats(bcw_index* x, bcw_index_info* out) {
   return BCW_OK;
 }
 
-int bcw_index_apply(bcw_index* x, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off, const uint8_t* h_ops,
-                    const uint64_t* h_fid, const uint64_t* h_off, const uint64_t* h_size) {
+int bcw_index_apply_stat(bcw_index* x, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off,
+                         const uint8_t* h_ops, const uint64_t* h_fid, const uint64_t* h_off, const uint64_t* h_size,
+                         uint8_t* h_found, uint64_t* h_free_fid, uint64_t* h_free_bytes) {
   if (!x || (n && (!h_key_off || !h_ops || !h_fid || !h_off || !h_size))) return BCW_E_INVAL;
+  const bool stat = h_found || h_free_fid || h_free_bytes;
+  if (stat && !(h_found && h_free_fid && h_free_bytes)) return BCW_E_INVAL;
   if (n == 0) return BCW_OK;
   const uint64_t kb = h_key_off[n] - h_key_off[0];
   if (kb && !h_keys) return BCW_E_INVAL;
@@ -794,9 +866,9 @@ int bcw_index_apply(bcw_index* x, uint64_t n, const uint8_t* h_keys, const uint6
   const uint64_t arena_b = 16 * n + kb + 15 * n;
   int rc = ix_room(x, n, arena_b);
   if (rc != BCW_OK) return rc;
-  // staging: keys | key offsets (rebased) | fid | off | size | ops
+  // staging: keys | key offsets (rebased) | fid | off | size | WriteStat (fid, size) | ops | found
   const uint64_t kbp = (kb + 15) & ~15ull;
-  rc = ix_stage(x, kbp + 8 * (n + 1) + 24 * n + n + 64);
+  rc = ix_stage(x, kbp + 8 * (n + 1) + 40 * n + 2 * n + 64);
   if (rc != BCW_OK) return rc;
   uint8_t* m = (uint8_t*)x->stage;
   uint8_t* d_keys = m;
@@ -804,7 +876,10 @@ int bcw_index_apply(bcw_index* x, uint64_t n, const uint8_t* h_keys, const uint6
   uint64_t* d_fid = d_koff + (n + 1);
   uint64_t* d_off = d_fid + n;
   uint64_t* d_size = d_off + n;
-  uint8_t* d_ops = (uint8_t*)(d_size + n);
+  uint64_t* d_ofid = d_size + n;
+  uint64_t* d_osize = d_ofid + n;
+  uint8_t* d_ops = (uint8_t*)(d_osize + n);
+  uint8_t* d_found = d_ops + n;
   hipStream_t st = x->ctx->cur;
   std::vector<uint64_t> koff(n + 1);
   for (uint64_t i = 0; i <= n; ++i) koff[i] = h_key_off[i] - h_key_off[0];
@@ -821,12 +896,56 @@ int bcw_index_apply(bcw_index* x, uint64_t n, const uint8_t* h_keys, const uint6
   s.koff = d_koff;
   s.keys_len = kb;
   OpVals v{d_ops, d_fid, d_off, d_size, 0, 0};
-  ix_batch(x, s, n, nullptr, 0, v);
-  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return BCW_E_HIP;
+  ix_batch(x, s, n, nullptr, 0, v, stat ? d_found : nullptr, d_ofid, d_osize);
+  if (stat)
+    ok = hipMemcpyAsync(h_found, d_found, n, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(h_free_fid, d_ofid, 8 * n, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(h_free_bytes, d_osize, 8 * n, hipMemcpyDeviceToHost, st) == hipSuccess;
+  if (!ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return BCW_E_HIP;
+  if (stat) {
+    // the device reported, per op, the value the key held before the batch; an op preceded by another op on the
+    // same key in this batch replaces that op's value instead (Put: its fid / size, SoftDelete: IndexValue{} with
+    // fid 0 / size 0, Delete: nothing -- index.go:108-165)
+    std::unordered_map<std::string_view, uint64_t> last;
+    last.reserve(n * 2);
+    const char* kbase = reinterpret_cast<const char*>(h_keys);
+    for (uint64_t i = 0; i < n; ++i) {
+      const std::string_view key(kbase ? kbase + h_key_off[i] : "", h_key_off[i + 1] - h_key_off[i]);
+      auto it = last.find(key);
+      if (it != last.end()) {
+        const uint64_t p = it->second;
+        h_found[i] = h_ops[p] != BCW_IDX_DELETE;
+        h_free_fid[i] = h_ops[p] == BCW_IDX_PUT ? h_fid[p] : 0;
+        h_free_bytes[i] = h_ops[p] == BCW_IDX_PUT ? h_size[p] : 0;
+        it->second = i;
+      } else {
+        last.emplace(key, i);
+      }
+      if (!h_found[i]) h_free_fid[i] = h_free_bytes[i] = 0;
+    }
+  }
   uint64_t c[C_NUM];
   rc = ix_sync_counters(x, c);
   if (rc != BCW_OK) return rc;
   return c[C_OVERFLOW] ? BCW_E_CAPACITY : BCW_OK;
+}
+
+int bcw_index_apply(bcw_index* x, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off, const uint8_t* h_ops,
+                    const uint64_t* h_fid, const uint64_t* h_off, const uint64_t* h_size) {
+  return bcw_index_apply_stat(x, n, h_keys, h_key_off, h_ops, h_fid, h_off, h_size, nullptr, nullptr, nullptr);
+}
+
+int bcw_index_clear(bcw_index* x) {
+  if (!x) return BCW_E_INVAL;
+  DeviceGuard dg(x->ctx->device);
+  if (!dg.ok) return BCW_E_HIP;
+  hipStream_t st = x->ctx->cur;
+  if (hipMemsetAsync(x->slots, 0, x->cap * sizeof(Slot), st) != hipSuccess ||
+      hipMemsetAsync(x->cnt, 0, C_NUM * sizeof(uint64_t), st) != hipSuccess)
+    return BCW_E_HIP;
+  x->slots_ub = 0;
+  x->arena_ub = 0;
+  return BCW_OK;
 }
 
 int bcw_index_get(bcw_index* x, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off, uint64_t* h_fid,
@@ -884,10 +1003,25 @@ int bcw_index_put_decoded_async(bcw_index* x, const uint8_t* d_seg, const bcw_de
   DeviceGuard dg(c->device);
   if (!dg.ok) return BCW_E_HIP;
   const uint64_t rows = d_table->capacity;
-  // arena bound: a merged key is at most its record's payload (ns + key <= size), all payloads fit the segment
-  int rc = ix_room(x, rows, p->seg_len + 32 * rows);
-  if (rc != BCW_OK) return rc;
   const Src s = table_src(c, d_seg, p, d_table, p->mode == BCW_MODE_RECORD ? SRC_RECORD : SRC_HINT);
+  // arena bound: a merged key is at most its record's payload (ns + key <= size), all payloads fit the segment.
+  // When that cheap bound does not fit the arena (a large segment), the exact need of the delivered rows is
+  // read back instead (one small launch and a sync): only keys new to the index take arena space, so an
+  // index rebuilt over keys it already holds does not grow.
+  uint64_t arena_b = p->seg_len + 32 * rows;
+  if (x->arena_ub + arena_b > x->arena_cap && rows) {
+    if (hipMemsetAsync(x->cnt + C_NEED, 0, sizeof(uint64_t), c->cur) != hipSuccess) return BCW_E_HIP;
+    k_ix_need<<<(uint32_t)((rows + 255) / 256), 256, 0, c->cur>>>(s, rows, d_result, c->frag_gen, x->cnt);
+    uint64_t cc[C_NUM];
+    int rc0 = ix_sync_counters(x, cc);
+    if (rc0 != BCW_OK) return rc0;
+    if (cc[C_OVERFLOW]) return BCW_E_CAPACITY;
+    x->arena_ub = cc[C_ARENA];
+    x->slots_ub = cc[C_SLOTS];
+    arena_b = cc[C_NEED];
+  }
+  int rc = ix_room(x, rows, arena_b);
+  if (rc != BCW_OK) return rc;
   OpVals v{nullptr, nullptr, nullptr, nullptr, fid, use_record_fid};
   ix_batch(x, s, rows, d_result, c->frag_gen, v);
   if (d_out) k_ix_result<<<1, 1, 0, c->cur>>>(x->cnt, d_out);

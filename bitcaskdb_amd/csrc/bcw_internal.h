@@ -39,6 +39,9 @@ struct Xf {
 };
 static_assert(sizeof(Xf) == 40, "Xf layout");
 
+// shift operators A_{8 * 2^k} for k < kPow2Ops: any shift below 2^16 bytes (a fragment's u16 length)
+constexpr int kPow2Ops = 16;
+
 // Device-side constant tables, built on the host once per context.
 struct Tables {
   uint32_t* slice;   // [2][256] slice-by-2 CRC-32C tables (T0 = byte table, T1)
@@ -48,7 +51,7 @@ struct Tables {
   uint32_t* initc;   // [kBlock+1] A_{8L}(0xFFFFFFFF)
   uint32_t* lds_image;  // k_crc's LDS table image, laid out exactly as in LDS (see kLdsImage)
   uint32_t* enc_ops;    // [kEncOpsWords] encode shift operators (nibble images, see build_enc_ops)
-  uint32_t* pow2;       // [15][8][16] A_{8 * 2^k} (nibble images), k < 15: shifts by any distance < 32 KiB
+  uint32_t* pow2;       // [kPow2Ops][8][16] A_{8 * 2^k} (nibble images), k < 16: shifts by any distance < 64 KiB
 };
 // enc_ops layout (operators of 128 words): [n] A_{8*16*n}, [16 + n] A_{8*256*n} (n < 16), [32 + n]
 // A_{8*4096*n} (n < 8), [40 + t] A_{8t}^-1 (t < 16), [56 + k] A_{8*2^k} (k < 32), [88 + k] A_{8*2^k}^-1 (k < 15)
@@ -184,6 +187,9 @@ struct DeviceGuard {
   DeviceGuard(const DeviceGuard&) = delete;
   DeviceGuard& operator=(const DeviceGuard&) = delete;
 };
+
+// The context an index was created on (bcw_index.hip): the sync entry points refuse an index of another context.
+bcw_ctx* index_ctx(const bcw_index* ix);
 
 // Host-side table builders (bcw_api.cpp).
 void build_slice_tables(uint32_t* t2x256);

@@ -81,13 +81,13 @@ struct ReadArgs {
   uint8_t* payload;
   uint8_t* rd_status;
   bcw_record_table tab;
-  const uint32_t* pow2;   // [15][8][16] nibble images of A_{8 * 2^k}
+  const uint32_t* pow2;   // [kPow2Ops][8][16] nibble images of A_{8 * 2^k}
   const uint32_t* initc;  // A_{8L}(0xFFFFFFFF)
 };
 
 __global__ __launch_bounds__(64 * kWaves) void k_read_records(ReadArgs A) {
   __shared__ uint32_t t0[256];
-  __shared__ uint32_t sp2[15 * 128];
+  __shared__ uint32_t sp2[kPow2Ops * 128];  // a fragment is < 2^16 bytes: shifts by up to 65535
   __shared__ uint64_t s_fo[kWaves][kMaxF];
   __shared__ uint32_t s_fl[kWaves][kMaxF];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_read_records(ReadArgs A) {
     for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
     t0[i] = c;
   }
-  for (uint32_t i = tid; i < 15 * 128; i += 64 * kWaves) sp2[i] = A.pow2[i];
+  for (uint32_t i = tid; i < kPow2Ops * 128; i += 64 * kWaves) sp2[i] = A.pow2[i];
   __syncthreads();
   const uint64_t r = (uint64_t)blockIdx.x * kWaves + wave;
   if (r >= A.n) return;

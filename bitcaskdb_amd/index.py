@@ -82,22 +82,51 @@ class Index:
             pass
 
     # ---- batches (DBImpl.writeIndex, db_impl.go:433-452) ----
-    def apply(self, ops, keys, fid=None, off=None, size=None):
-        """ops[i] in (IDX_PUT, IDX_DELETE, IDX_SOFT_DELETE) on merged key keys[i], applied in order."""
+    def apply(self, ops, keys, fid=None, off=None, size=None, stats: bool = False):
+        """ops[i] in (IDX_PUT, IDX_DELETE, IDX_SOFT_DELETE) on merged key keys[i], applied in order.
+        stats: also return every op's WriteStat (index.go:100-165) as (found, free_fid, free_bytes) arrays."""
         n = len(keys)
         if n == 0:
-            return
+            return (np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint64)) if stats else None
         flat, koff = _pack(keys)
         ops = np.ascontiguousarray(ops, dtype=np.uint8)
         z = np.zeros(n, dtype=np.uint64)
         fid = np.ascontiguousarray(fid if fid is not None else z, dtype=np.uint64)
         off = np.ascontiguousarray(off if off is not None else z, dtype=np.uint64)
         size = np.ascontiguousarray(size if size is not None else z, dtype=np.uint64)
-        rc = L.lib.bcw_index_apply(self._h, n, flat.ctypes.data_as(C.c_void_p), koff.ctypes.data_as(L.u64p),
-                                   ops.ctypes.data_as(L.u8p), fid.ctypes.data_as(L.u64p), off.ctypes.data_as(L.u64p),
-                                   size.ctypes.data_as(L.u64p))
+        found, ffid, fbytes = np.zeros(n, np.uint8), np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+        rc = L.lib.bcw_index_apply_stat(self._h, n, flat.ctypes.data_as(C.c_void_p), koff.ctypes.data_as(L.u64p),
+                                        ops.ctypes.data_as(L.u8p), fid.ctypes.data_as(L.u64p),
+                                        off.ctypes.data_as(L.u64p), size.ctypes.data_as(L.u64p),
+                                        found.ctypes.data_as(L.u8p) if stats else None,
+                                        ffid.ctypes.data_as(L.u64p) if stats else None,
+                                        fbytes.ctypes.data_as(L.u64p) if stats else None)
         if rc != 0:
             raise RuntimeError(f"bcw_index_apply: {L.lib.bcw_strerror(rc).decode()}")
+        return (found, ffid, fbytes) if stats else None
+
+    def write_index(self, ops, keys, fid=None, off=None, size=None) -> dict:
+        """DBImpl.writeIndex (db_impl.go:433-452): apply the batch, return writeStats {FreeWalFid: FreeBytes}
+        (a not-found Delete adds 0 to fid 0, as the reference's zero WriteStat does)."""
+        found, ffid, fbytes = self.apply(ops, keys, fid, off, size, stats=True)
+        out: dict = {}
+        for f, b in zip(ffid.tolist(), fbytes.tolist()):
+            out[f] = out.get(f, 0) + b
+        return out
+
+    def clear(self):
+        """remove every key (capacity kept): with apply() of a Go index's live entries, a snapshot load"""
+        rc = L.lib.bcw_index_clear(self._h)
+        if rc != 0:
+            raise RuntimeError(f"bcw_index_clear: {L.lib.bcw_strerror(rc).decode()}")
+
+    def load_snapshot(self, entries: dict):
+        """make the device index hold exactly `entries` ({merged key: (fid, off, size)}, e.g. the live entries of
+        a bounded, evicting Go index at compaction start), for the device doFilter"""
+        self.clear()
+        keys = list(entries)
+        vals = np.array([entries[k] for k in keys], dtype=np.uint64).reshape(-1, 3)
+        self.apply([L.IDX_PUT] * len(keys), keys, vals[:, 0], vals[:, 1], vals[:, 2])
 
     def get_many(self, keys):
         """Index.Get of merged keys: (status, fid, off, size) arrays; status IDX_*."""

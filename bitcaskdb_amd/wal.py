@@ -389,7 +389,11 @@ def iterate_hint(hint: Wal, cb, ns_size: int = 20, ctx: Context | None = None):
         if st == L.ST_PANIC:
             raise RefPanic("slice bounds out of range")
         payload = dec.record_bytes(r)
-        ko, kl = int(dec.table["hdr_size"][r]), int(dec.table["key_len"][r])
+        # key offset = NsSize + len(uvarint keyLen) (hint.go:62-66); the table's u8 hdr_size holds it mod 256
+        ko = ns_size + 1
+        while ko - ns_size < 10 and payload[ko - 1] & 0x80:
+            ko += 1
+        kl = int(dec.table["key_len"][r])
         rec = HintRecord(ns=payload[:ns_size], key=payload[ko:ko + kl], fid=int(dec.table["expire"][r]),
                          off=int(dec.table["aux0"][r]), size=int(dec.table["aux1"][r]))
         ret = cb(rec)

@@ -104,7 +104,8 @@ typedef struct bcw_decode_params {
  * Row r describes the r-th record the reference iterator emits (in file order).
  *   record mode: expire = decoded expire incl. baseTime; key/val/meta_len = varint lengths;
  *                hdr_size = data[0]; flags = flag byte; etag_off = offset of the etag field.
- *   hint mode:   key_len, hdr_size = key offset; expire = fid; aux0 = off; aux1 = size.
+ *   hint mode:   key_len, hdr_size = key offset mod 256 (exact when ns_size <= 245; the key starts at
+ *                ns_size + the length of the keyLen varint); expire = fid; aux0 = off; aux1 = size.
  * foff is the iterator offset (data start of the record's first non-empty fragment,
  * wal_iterator.go:70-72); callers subtract BCW_HEADER_SIZE as compaction.go:302 does.
  * first_frag / emit_frag are global fragment indices: the record's bytes are the data of
@@ -306,7 +307,9 @@ int bcw_encode_segment(bcw_ctx* ctx, const uint8_t* h_src, const bcw_encode_para
  * Observable semantics of Index.Get/Put/Delete/SoftDelete (index.go:81-165): a map from MergedKey(ns, key)
  * = ns || key (utils.go:133-139) to (fid, off, size), hashed with murmur3 Sum64 (index.go:15-19). Get
  * reports ErrKeyNotFound, or ErrKeySoftDeleted when off == 0. The reference's sampled approximate-LRU
- * eviction (random, map.go:395-420) is not restated: the device index keeps every key and grows.
+ * eviction (random, map.go:349-371) is not restated: the device index keeps every key and grows. With a bounded
+ * Go index (IndexLimited below the key count) the Go index stays authoritative and the device filter runs
+ * against a snapshot of it (bcw_index_clear + bcw_index_apply of its live entries).
  * Batches keep the reference's sequential order: the last operation on a key wins. An index is bound to
  * the context it was created on (its stream and device; the table-driven calls read that context's
  * fragment table of its latest decode). */
@@ -347,6 +350,19 @@ int bcw_index_stats(bcw_index* ix, bcw_index_info* out);
  * Synchronous. */
 int bcw_index_apply(bcw_index* ix, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off,
                     const uint8_t* h_ops, const uint64_t* h_fid, const uint64_t* h_off, const uint64_t* h_size);
+/* bcw_index_apply plus the WriteStat of every op (index.go:100-165), for DBImpl.writeIndex's freed-bytes map
+ * (db_impl.go:433-452, manifest.Apply db_impl.go:402): h_found[i] = 1 when op i replaced or removed a value
+ * (the key was present before it: a previous op of the same batch counts), h_free_fid[i] / h_free_bytes[i] =
+ * that value's fid / valueSize (0, 0 when h_found[i] = 0). The Go shim sums writeStats[free_fid] += free_bytes
+ * exactly as writeIndex does. The device index never evicts, so a Put of a new key reports nothing -- with a
+ * bounded Go index (IndexLimited below the key count) the reference reports the evicted entry instead: keep the
+ * Go index authoritative then ("bounded index"). Synchronous. */
+int bcw_index_apply_stat(bcw_index* ix, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off,
+                         const uint8_t* h_ops, const uint64_t* h_fid, const uint64_t* h_off, const uint64_t* h_size,
+                         uint8_t* h_found, uint64_t* h_free_fid, uint64_t* h_free_bytes);
+/* Remove every key (capacity kept). With bcw_index_apply of the Go index's live entries this loads a snapshot
+ * of a bounded (evicting) Go index for the device compaction filter ("bounded index"). */
+int bcw_index_clear(bcw_index* ix);
 /* Index.Get of n merged keys (host arrays): status BCW_IDX_* and the value per key. Synchronous. */
 int bcw_index_get(bcw_index* ix, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off, uint64_t* h_fid,
                   uint64_t* h_off, uint64_t* h_size, uint8_t* h_status);
@@ -375,14 +391,14 @@ int bcw_index_export(bcw_index* ix, uint8_t* h_keys, uint64_t keys_cap, uint64_t
 /* Synchronous compaction of one source WAL with the device filter: decode -> doFilter against the index
  * -> Record.Encode + WriteRecord + hint append (compaction.go:294-327 with doFilter compaction.go:329-348
  * and no user CompactionFilter), host in / host out like bcw_encode_segment. h_filter (may be NULL)
- * receives the filter's outcome (n_done = rows kept). */
+ * receives the filter's outcome (n_done = rows kept). ix must belong to ctx (BCW_E_INVAL otherwise). */
 int bcw_compact_segment(bcw_ctx* ctx, bcw_index* ix, const uint8_t* h_src, const bcw_encode_params* p,
                         uint64_t src_fid, const bcw_encode_out* h_out, bcw_encode_result* h_result,
                         bcw_index_result* h_filter);
 /* Synchronous recoverFromWal step (db_impl.go:286-313) for one file: decode h_seg (p->mode: BCW_MODE_HINT for a
  * hint file, BCW_MODE_RECORD for a data WAL) and put every delivered row into the index. h_dres (may be
  * NULL) receives the decode result: a hint file whose iteration failed is followed, as in the reference,
- * by the data WAL of the same fid. */
+ * by the data WAL of the same fid. ix must belong to ctx (BCW_E_INVAL otherwise). */
 int bcw_index_recover_segment(bcw_ctx* ctx, bcw_index* ix, const uint8_t* h_seg, const bcw_decode_params* p,
                               uint64_t fid, int use_record_fid, bcw_decode_result* h_dres, bcw_index_result* h_out);
 /* IndexOperator.Hash (index.go:15-19): murmur3 (spaolacci/murmur3 v1.1.0) New64().Sum64() on the host */

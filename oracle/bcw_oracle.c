@@ -987,6 +987,11 @@ static void rec_ns_key(const oc_rec* r, const uint8_t* payload, uint32_t ns_size
                        const uint8_t** key, uint64_t* kl) {
   *ns = payload + (mode == 0 ? 1 : 0);
   *key = payload + r->hdr_size;
+  if (mode == 1) { /* hint key offset NsSize + len(uvarint keyLen) (hint.go:62-66): hdr_size holds it mod 256 */
+    size_t u = 1;
+    while (u < 10 && (payload[ns_size + u - 1] & 0x80)) ++u;
+    *key = payload + ns_size + u;
+  }
   *kl = r->key_len;
 }
 
@@ -1065,4 +1070,349 @@ int oc_read_record(const uint8_t* seg, uint64_t seg_len, uint64_t offset, uint64
     if (type != OC_FIRST && type != OC_MIDDLE) return OC_RD_TYPE;
     if (blk_size - blk_off <= OC_HEADER_SIZE) return OC_RD_INCOMPLETE; /* break; i++ ends the block loop */
   }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* bounded index: map.go's SimpleMap / ShardMap with the sampled approximate-LRU eviction        */
+/* ------------------------------------------------------------------------------------------ */
+/* Restated operation by operation (map.go:122-428) so that an index whose Limited is below its key count
+ * (IndexCapacity / IndexLimited / IndexEvictionPoolCapacity, db.go:70-72 -> db_impl.go:164-166) has an
+ * oracle: Set evicts before inserting once used + 1 > limited (map.go:185-187) and returns the evicted
+ * value as "old" (so WriteStat reports it, index.go:152-162); the eviction samples SampleKeys entries of
+ * random buckets (Rand(capacity), chains walked from the bucket head, map.go:349-371) into a pool kept in
+ * ascending expire order with upper-bound insertion (map.go:294-316), then deletes the first pool entry
+ * that still exists and drops [0, pos] from the pool while the size shrinks by pos only
+ * (map.go:319-342 -- the last survivor stays duplicated, as in the reference). Rand and WallTime are
+ * the injected MapOperatorBase (map.go:23-29): a scripted value list cycled like map_test.go's
+ * mockSimpleMapOperator (v[i] % n), or a seeded splitmix64 stream; WallTime is a seconds counter the
+ * caller advances (genExpire = seconds since the map's initTime, map.go:149-156). */
+typedef struct oc_bkt {
+  uint8_t* key; /* NULL: empty bucket head */
+  uint32_t klen;
+  uint32_t expire;
+  uint64_t val[3];
+  struct oc_bkt* next;
+} oc_bkt;
+typedef struct oc_pent { uint64_t slot; const uint8_t* key; uint32_t klen, expire; } oc_pent;
+typedef struct oc_shard {
+  uint64_t cap, used, limited, pool_size, pool_cap, sample;
+  oc_bkt* b;
+  oc_pent* pool;
+  uint64_t init;
+} oc_shard;
+struct oc_smap {
+  uint32_t nsh;
+  int hash_mode;
+  oc_shard* sh;
+  uint64_t now;
+  uint64_t* rv;
+  uint64_t nrv, ri, seed;
+  uint8_t** arena; /* pool key copies (the pool may hold stale duplicates: never freed before the map) */
+  uint64_t narena, carena;
+};
+
+static uint64_t sm_rand(oc_smap* m, uint64_t n) {
+  if (m->nrv) {
+    if (m->ri >= m->nrv) m->ri = 0;
+    return m->rv[m->ri++] % n;
+  }
+  uint64_t z = (m->seed += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (z ^ (z >> 31)) % n;
+}
+static uint64_t sm_hash(const oc_smap* m, const uint8_t* k, size_t kl) {
+  if (m->hash_mode == 1) { uint64_t v = 0; oc_memcpy(&v, k, kl < 8 ? kl : 8); return v; }
+  return oc_murmur3_sum64(k, kl);
+}
+static uint32_t sm_expire(const oc_smap* m, const oc_shard* s) {
+  return m->now < s->init ? 0u : (uint32_t)(m->now - s->init);
+}
+static const uint8_t* sm_keep_key(oc_smap* m, const uint8_t* k, uint32_t kl) {
+  if (m->narena == m->carena) {
+    m->carena = m->carena ? 2 * m->carena : 1024;
+    m->arena = (uint8_t**)realloc(m->arena, m->carena * sizeof *m->arena);
+  }
+  uint8_t* c = (uint8_t*)malloc(kl ? kl : 1);
+  oc_memcpy(c, k, kl);
+  m->arena[m->narena++] = c;
+  return c;
+}
+static int sm_eq(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
+  return al == bl && (al == 0 || memcmp(a, b, al) == 0);
+}
+
+oc_smap* oc_smap_new(uint32_t nshards, uint64_t capacity, uint64_t limited, uint64_t pool_cap, uint64_t sample_keys,
+                     int hash_mode, const uint64_t* rand_vals, uint64_t n_rand, uint64_t seed) {
+  if (nshards == 0) return NULL;
+  /* NewShardMap divides Capacity and Limited (map.go:385-390); validate per map (map.go:102-120) */
+  const uint64_t cap = capacity / nshards, lim = limited / nshards;
+  if (lim > cap || pool_cap > lim || sample_keys < 1 || pool_cap < 16 || cap == 0) return NULL;
+  oc_smap* m = (oc_smap*)calloc(1, sizeof *m);
+  m->nsh = nshards;
+  m->hash_mode = hash_mode;
+  m->seed = seed;
+  if (n_rand) {
+    m->rv = (uint64_t*)malloc(n_rand * sizeof(uint64_t));
+    oc_memcpy(m->rv, rand_vals, n_rand * sizeof(uint64_t));
+    m->nrv = n_rand;
+  }
+  m->sh = (oc_shard*)calloc(nshards, sizeof(oc_shard));
+  for (uint32_t i = 0; i < nshards; ++i) {
+    oc_shard* s = &m->sh[i];
+    s->cap = cap; s->limited = lim; s->pool_cap = pool_cap; s->sample = sample_keys;
+    s->b = (oc_bkt*)calloc(cap, sizeof(oc_bkt));
+    s->pool = (oc_pent*)calloc(pool_cap, sizeof(oc_pent));
+    s->init = m->now;
+  }
+  return m;
+}
+void oc_smap_free(oc_smap* m) {
+  if (!m) return;
+  for (uint32_t i = 0; i < m->nsh; ++i) {
+    oc_shard* s = &m->sh[i];
+    for (uint64_t j = 0; j < s->cap; ++j) {
+      oc_bkt* e = s->b[j].next;
+      while (e) { oc_bkt* n = e->next; free(e->key); free(e); e = n; }
+      free(s->b[j].key);
+    }
+    free(s->b);
+    free(s->pool);
+  }
+  for (uint64_t i = 0; i < m->narena; ++i) free(m->arena[i]);
+  free(m->arena);
+  free(m->rv);
+  free(m->sh);
+  free(m);
+}
+void oc_smap_set_now(oc_smap* m, uint64_t seconds) { m->now = seconds; }
+uint64_t oc_smap_size(const oc_smap* m) {
+  uint64_t n = 0;
+  for (uint32_t i = 0; i < m->nsh; ++i) n += m->sh[i].used;
+  return n;
+}
+
+/* getEntryWithSlot (map.go:229-245) */
+static oc_bkt* sm_find(oc_shard* s, const uint8_t* k, uint32_t kl, uint64_t slot) {
+  slot %= s->cap;
+  if (!s->b[slot].key) return NULL;
+  for (oc_bkt* e = &s->b[slot]; e; e = e->next)
+    if (sm_eq(k, kl, e->key, e->klen)) return e;
+  return NULL;
+}
+/* deleteWithSlotInternal (map.go:260-292): 0 deleted (old value out), 1 ErrKeyNotFound */
+static int sm_delete(oc_shard* s, const uint8_t* k, uint32_t kl, uint64_t slot, uint64_t old[3]) {
+  slot %= s->cap;
+  oc_bkt* h = &s->b[slot];
+  if (!h->key) return 1;
+  if (sm_eq(h->key, h->klen, k, kl)) {
+    if (old) oc_memcpy(old, h->val, sizeof h->val);
+    free(h->key);
+    if (h->next) {
+      oc_bkt* n = h->next;
+      *h = *n; /* m.buckets[slot] = *m.buckets[slot].next */
+      free(n);
+    } else {
+      h->key = NULL;
+      h->klen = 0;
+      memset(h->val, 0, sizeof h->val);
+    }
+    s->used--;
+    return 0;
+  }
+  for (oc_bkt* e = h; e->next; e = e->next) {
+    if (sm_eq(e->next->key, e->next->klen, k, kl)) {
+      oc_bkt* d = e->next;
+      if (old) oc_memcpy(old, d->val, sizeof d->val);
+      e->next = d->next;
+      free(d->key);
+      free(d);
+      s->used--;
+      return 0;
+    }
+  }
+  return 1;
+}
+/* insertEvictionEntry (map.go:294-316) */
+static void sm_pool_insert(oc_shard* s, oc_pent en) {
+  uint64_t idx = 0;
+  while (idx < s->pool_size && !(en.expire < s->pool[idx].expire)) ++idx; /* sort.Search upper bound */
+  if (idx == s->pool_size) {
+    idx = s->pool_size - 1; /* size 0 only when pool_cap > 0: then the next line makes it 0 */
+    if (s->pool_size != s->pool_cap) idx = s->pool_size;
+  }
+  if (s->pool_size != s->pool_cap) s->pool_size++;
+  if (s->pool_size - 1 > idx) memmove(&s->pool[idx + 1], &s->pool[idx], (s->pool_size - 1 - idx) * sizeof(oc_pent));
+  s->pool[idx] = en;
+}
+/* evictMinExpireEntry (map.go:319-342); the reference's own argument guarantees a hit */
+static void sm_evict_min(oc_shard* s, uint64_t old[3]) {
+  uint64_t pos = 0;
+  while (pos < s->pool_size) {
+    if (sm_delete(s, s->pool[pos].key, s->pool[pos].klen, s->pool[pos].slot, old) == 0) break;
+    pos++;
+  }
+  if (pos + 1 <= s->pool_size)
+    memmove(&s->pool[0], &s->pool[pos + 1], (s->pool_size - pos - 1) * sizeof(oc_pent));
+  s->pool_size -= pos;
+}
+/* evict (map.go:349-371) */
+static void sm_evict(oc_smap* m, oc_shard* s, uint64_t old[3]) {
+  uint64_t left = s->sample;
+  while (left > 0) {
+    const uint64_t slot = sm_rand(m, s->cap);
+    oc_bkt* e = &s->b[slot];
+    if (!e->key) continue;
+    for (; left > 0 && e; e = e->next, --left) {
+      oc_pent p;
+      p.expire = e->expire;
+      p.key = sm_keep_key(m, e->key, e->klen);
+      p.klen = e->klen;
+      p.slot = slot;
+      sm_pool_insert(s, p);
+    }
+  }
+  sm_evict_min(s, old);
+}
+
+/* Set (map.go:160-210 via ShardMap.Set map.go:414-418): 0 inserted (no old value), 1 replaced (old = the
+ * previous value), 2 inserted after an eviction (old = the evicted value) */
+int oc_smap_set(oc_smap* m, const uint8_t* k, size_t kl, const uint64_t val[3], uint64_t old[3]) {
+  const uint64_t h = sm_hash(m, k, kl);
+  oc_shard* s = &m->sh[h % m->nsh];
+  const uint64_t slot = h % s->cap;
+  oc_bkt* e = sm_find(s, k, (uint32_t)kl, slot);
+  if (e) {
+    if (old) oc_memcpy(old, e->val, sizeof e->val);
+    oc_memcpy(e->val, val, sizeof e->val);
+    e->expire = sm_expire(m, s);
+    return 1;
+  }
+  int ret = 0;
+  if (s->used + 1 > s->limited) { sm_evict(m, s, old); ret = 2; }
+  s->used++;
+  oc_bkt* hd = &s->b[slot];
+  uint8_t* kc = (uint8_t*)malloc(kl ? kl : 1);
+  oc_memcpy(kc, k, kl);
+  if (!hd->key) {
+    hd->key = kc; hd->klen = (uint32_t)kl;
+    oc_memcpy(hd->val, val, sizeof hd->val);
+    hd->expire = sm_expire(m, s);
+    return ret;
+  }
+  oc_bkt* n = (oc_bkt*)calloc(1, sizeof *n);
+  n->key = kc; n->klen = (uint32_t)kl;
+  oc_memcpy(n->val, val, sizeof n->val);
+  n->next = hd->next;
+  n->expire = sm_expire(m, s);
+  hd->next = n;
+  return ret;
+}
+/* Get (map.go:212-227): 0 found, 1 ErrKeyNotFound */
+int oc_smap_get(oc_smap* m, const uint8_t* k, size_t kl, uint64_t val[3]) {
+  const uint64_t h = sm_hash(m, k, kl);
+  oc_shard* s = &m->sh[h % m->nsh];
+  oc_bkt* e = sm_find(s, k, (uint32_t)kl, h);
+  if (!e) return 1;
+  oc_memcpy(val, e->val, sizeof e->val);
+  return 0;
+}
+/* Delete (map.go:248-258): 0 deleted (old out), 1 ErrKeyNotFound */
+int oc_smap_delete(oc_smap* m, const uint8_t* k, size_t kl, uint64_t old[3]) {
+  const uint64_t h = sm_hash(m, k, kl);
+  oc_shard* s = &m->sh[h % m->nsh];
+  return sm_delete(s, k, (uint32_t)kl, h, old);
+}
+/* every live entry, in bucket order: keys concatenated (koff has n + 1 entries), values 3 per entry;
+ * returns the entry count (outputs written only while they fit) */
+uint64_t oc_smap_export(const oc_smap* m, uint8_t* keys, uint64_t keys_cap, uint64_t* koff, uint64_t* vals,
+                        uint64_t cap, uint64_t* key_bytes) {
+  uint64_t n = 0, kb = 0;
+  if (koff && cap) koff[0] = 0;
+  for (uint32_t i = 0; i < m->nsh; ++i)
+    for (uint64_t j = 0; j < m->sh[i].cap; ++j) {
+      if (!m->sh[i].b[j].key) continue;
+      for (const oc_bkt* e = &m->sh[i].b[j]; e; e = e->next) {
+        if (n < cap && kb + e->klen <= keys_cap) {
+          if (e->klen) oc_memcpy(keys + kb, e->key, e->klen);
+          oc_memcpy(vals + 3 * n, e->val, sizeof e->val);
+          koff[n + 1] = kb + e->klen;
+        }
+        kb += e->klen;
+        n++;
+      }
+    }
+  if (key_bytes) *key_bytes = kb;
+  return n;
+}
+
+/* Index over the bounded map (index.go:81-165): op 0 Put, 1 Delete, 2 SoftDelete. Returns the WriteStat
+ * the reference fills (index.go:115-118,134-137,157-160): *free_bytes = old.valueSize and *free_fid =
+ * old.fid when an old value came back (a replaced key, a deleted key, or the entry evicted to make room),
+ * else 0, 0. */
+void oc_bindex_op(oc_smap* m, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, int op, uint64_t fid,
+                  uint64_t off, uint64_t size, uint64_t* free_fid, uint64_t* free_bytes) {
+  uint8_t* mk = merged_key(ns, nsl, key, kl);
+  uint64_t old[3] = {0, 0, 0};
+  int has_old = 0;
+  if (op == 1) {
+    has_old = oc_smap_delete(m, mk, nsl + kl, old) == 0;
+  } else {
+    const uint64_t v[3] = {op == 0 ? fid : 0, op == 0 ? off : 0, op == 0 ? size : 0};
+    has_old = oc_smap_set(m, mk, nsl + kl, v, old) != 0;
+  }
+  free(mk);
+  if (free_fid) *free_fid = has_old ? old[0] : 0;
+  if (free_bytes) *free_bytes = has_old ? old[2] : 0;
+}
+/* Index.Get over the bounded map: 0 found, 1 ErrKeyNotFound, 2 ErrKeySoftDeleted */
+int oc_bindex_get(oc_smap* m, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, uint64_t* fid,
+                  uint64_t* off, uint64_t* size) {
+  uint8_t* mk = merged_key(ns, nsl, key, kl);
+  uint64_t v[3];
+  const int r = oc_smap_get(m, mk, nsl + kl, v);
+  free(mk);
+  if (r) return 1;
+  *fid = v[0]; *off = v[1]; *size = v[2];
+  return v[1] == 0 ? 2 : 0;
+}
+/* recoverFromWal's Put loop (db_impl.go:290-313) into the bounded index, as oc_index_put_segment */
+int oc_bindex_put_segment(oc_smap* m, const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                          uint32_t ns_size, uint32_t etag_size, int mode, uint64_t fid, int use_rec_fid,
+                          uint64_t* n_put) {
+  oc_decode* d = oc_decode_segment(seg, len, start_off, base_time, ns_size, etag_size, mode);
+  int ret = d->err_class;
+  uint64_t r = 0;
+  for (; r < d->n_recs; ++r) {
+    const oc_rec* rc = &d->recs[r];
+    if (rc->status != OC_ST_OK) { ret = 16 + rc->status; break; }
+    const uint8_t *ns, *key;
+    uint64_t kl;
+    rec_ns_key(rc, d->bytes + d->byte_offs[r], ns_size, mode, &ns, &key, &kl);
+    if (mode == 0) oc_bindex_op(m, ns, ns_size, key, kl, 0, fid, rc->foff - OC_HEADER_SIZE, rc->size, NULL, NULL);
+    else oc_bindex_op(m, ns, ns_size, key, kl, 0, use_rec_fid ? rc->expire : fid, rc->val_len, rc->meta_len, NULL, NULL);
+  }
+  *n_put = r;
+  oc_decode_free(d);
+  return ret;
+}
+/* doFilter over every delivered row against the bounded index (compaction.go:329-348: a key evicted from
+ * the index is dropped like a deleted one) */
+uint64_t oc_bindex_compact_filter(oc_smap* m, const uint8_t* seg, uint64_t len, uint32_t start_off,
+                                  uint64_t base_time, uint32_t ns_size, uint32_t etag_size, uint64_t src_fid,
+                                  uint8_t* keep, uint64_t n_keep) {
+  oc_decode* d = oc_decode_segment(seg, len, start_off, base_time, ns_size, etag_size, 0);
+  uint64_t r = 0;
+  for (uint64_t i = 0; i < n_keep; ++i) keep[i] = 0;
+  for (; r < d->n_recs; ++r) {
+    const oc_rec* rc = &d->recs[r];
+    if (rc->status != OC_ST_OK) break;
+    const uint8_t *ns, *key;
+    uint64_t kl, fid = 0, off = 0, size = 0;
+    rec_ns_key(rc, d->bytes + d->byte_offs[r], ns_size, 0, &ns, &key, &kl);
+    const int g = oc_bindex_get(m, ns, ns_size, key, kl, &fid, &off, &size);
+    if (r < n_keep) keep[r] = (g == 0 && fid == src_fid && off == rc->foff - OC_HEADER_SIZE) ? 1 : 0;
+  }
+  oc_decode_free(d);
+  return r;
 }

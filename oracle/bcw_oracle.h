@@ -68,7 +68,7 @@ typedef struct oc_rec {
   uint64_t meta_len;  /* record: metaLen; hint: size */
   uint32_t first_frag;/* first fragment whose data is part of the record */
   uint32_t emit_frag; /* fragment that completed the record (Full or Last) */
-  uint8_t hdr_size;   /* record: data[0]; hint: key offset */
+  uint8_t hdr_size;   /* record: data[0]; hint: key offset mod 256 */
   uint8_t flags;      /* record: flag byte; hint: 0 */
   uint8_t etag_off;   /* record: offset of etag/expire fields; hint: 0 */
   uint8_t status;     /* OC_ST_* */
@@ -190,6 +190,32 @@ int oc_index_put_segment(oc_index* x, const uint8_t* seg, uint64_t len, uint32_t
                          uint64_t* n_put);
 uint64_t oc_compact_filter(oc_index* x, const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
                            uint32_t ns_size, uint32_t etag_size, uint64_t src_fid, uint8_t* keep, uint64_t n_keep);
+
+/* ---- bounded index: map.go SimpleMap (nshards 1) / ShardMap (nshards 16) with eviction ----
+ * hash_mode 0: murmur3 Sum64 (IndexOperator.Hash); 1: the key's first 8 bytes little-endian (map_test.go's
+ * mockSimpleMapOperator, Hash(k) = k). Rand: rand_vals cycled (v[i] % n) or, with n_rand 0, splitmix64(seed).
+ * NULL when NewMap's validate fails (ErrMapOptions). Values are 3 x u64 (IndexValue{fid, off, size}). */
+typedef struct oc_smap oc_smap;
+oc_smap* oc_smap_new(uint32_t nshards, uint64_t capacity, uint64_t limited, uint64_t pool_cap, uint64_t sample_keys,
+                     int hash_mode, const uint64_t* rand_vals, uint64_t n_rand, uint64_t seed);
+void oc_smap_free(oc_smap* m);
+void oc_smap_set_now(oc_smap* m, uint64_t seconds);
+uint64_t oc_smap_size(const oc_smap* m);
+int oc_smap_set(oc_smap* m, const uint8_t* k, size_t kl, const uint64_t val[3], uint64_t old[3]); /* 0 new, 1 replaced, 2 evicted */
+int oc_smap_get(oc_smap* m, const uint8_t* k, size_t kl, uint64_t val[3]);                        /* 0 found, 1 not found */
+int oc_smap_delete(oc_smap* m, const uint8_t* k, size_t kl, uint64_t old[3]);                     /* 0 deleted, 1 not found */
+uint64_t oc_smap_export(const oc_smap* m, uint8_t* keys, uint64_t keys_cap, uint64_t* koff, uint64_t* vals,
+                        uint64_t cap, uint64_t* key_bytes);
+void oc_bindex_op(oc_smap* m, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, int op, uint64_t fid,
+                  uint64_t off, uint64_t size, uint64_t* free_fid, uint64_t* free_bytes);
+int oc_bindex_get(oc_smap* m, const uint8_t* ns, size_t nsl, const uint8_t* key, size_t kl, uint64_t* fid,
+                  uint64_t* off, uint64_t* size);
+int oc_bindex_put_segment(oc_smap* m, const uint8_t* seg, uint64_t len, uint32_t start_off, uint64_t base_time,
+                          uint32_t ns_size, uint32_t etag_size, int mode, uint64_t fid, int use_rec_fid,
+                          uint64_t* n_put);
+uint64_t oc_bindex_compact_filter(oc_smap* m, const uint8_t* seg, uint64_t len, uint32_t start_off,
+                                  uint64_t base_time, uint32_t ns_size, uint32_t etag_size, uint64_t src_fid,
+                                  uint8_t* keep, uint64_t n_keep);
 
 /* ---- point reads: Wal.ReadRecord + WalParseRecord (wal.go:556-573, 121-173) ---- */
 enum { OC_RD_OK = 0, OC_RD_BEYOND = 1, OC_RD_CORRUPTED = 2, OC_RD_CRC = 3, OC_RD_SIZE = 4, OC_RD_TYPE = 5,

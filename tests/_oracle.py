@@ -116,6 +116,33 @@ lib.oc_synth_segment.restype = vp
 lib.oc_synth_segment.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
                                  C.c_uint64]
 
+lib.oc_smap_new.restype = vp
+lib.oc_smap_new.argtypes = [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, vp, C.c_uint64,
+                            C.c_uint64]
+lib.oc_smap_free.argtypes = [vp]
+lib.oc_smap_set_now.argtypes = [vp, C.c_uint64]
+lib.oc_smap_size.restype = C.c_uint64
+lib.oc_smap_size.argtypes = [vp]
+lib.oc_smap_set.restype = C.c_int
+lib.oc_smap_set.argtypes = [vp, vp, C.c_size_t, vp, vp]
+lib.oc_smap_get.restype = C.c_int
+lib.oc_smap_get.argtypes = [vp, vp, C.c_size_t, vp]
+lib.oc_smap_delete.restype = C.c_int
+lib.oc_smap_delete.argtypes = [vp, vp, C.c_size_t, vp]
+lib.oc_smap_export.restype = C.c_uint64
+lib.oc_smap_export.argtypes = [vp, vp, C.c_uint64, vp, vp, C.c_uint64, _u64p]
+lib.oc_bindex_op.restype = None
+lib.oc_bindex_op.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, _u64p,
+                             _u64p]
+lib.oc_bindex_get.restype = C.c_int
+lib.oc_bindex_get.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, _u64p, _u64p, _u64p]
+lib.oc_bindex_put_segment.restype = C.c_int
+lib.oc_bindex_put_segment.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int,
+                                      C.c_uint64, C.c_int, _u64p]
+lib.oc_bindex_compact_filter.restype = C.c_uint64
+lib.oc_bindex_compact_filter.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                                         C.c_uint64, vp, C.c_uint64]
+
 
 def _ptr(a):
     if isinstance(a, (bytes, bytearray)):
@@ -359,4 +386,79 @@ class Index:
         keep = np.zeros(max(n_rows, 1), dtype=np.uint8)
         nv = lib.oc_compact_filter(self.h, _ptr(seg), seg.size, start_off, base_time, ns_size, etag_size, src_fid,
                                    keep.ctypes.data_as(vp), n_rows)
+        return keep[:n_rows], int(nv)
+
+
+class SMap:
+    """oc_smap: map.go's SimpleMap (nshards=1) / ShardMap (nshards=16) with the sampled eviction, Rand and
+    WallTime injected (scripted `rand_vals` cycled as v % n like map_test.go's mock, or a seeded stream)."""
+
+    def __init__(self, capacity, limited, pool_cap, sample_keys, nshards=16, hash_mode=0, rand_vals=(), seed=1):
+        rv = np.asarray(rand_vals, dtype=np.uint64)
+        self.h = lib.oc_smap_new(nshards, capacity, limited, pool_cap, sample_keys, hash_mode,
+                                 rv.ctypes.data_as(vp) if rv.size else None, rv.size, seed)
+        if not self.h:
+            raise ValueError("ErrMapOptions")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib.oc_smap_free(self.h)
+            self.h = None
+
+    def set_now(self, seconds: int):
+        lib.oc_smap_set_now(self.h, seconds)
+
+    def size(self) -> int:
+        return int(lib.oc_smap_size(self.h))
+
+    def set(self, key: bytes, val):
+        v = (C.c_uint64 * 3)(*(list(val) + [0, 0, 0])[:3])
+        old = (C.c_uint64 * 3)()
+        r = lib.oc_smap_set(self.h, _ptr(key), len(key), v, old)
+        return int(r), tuple(int(x) for x in old)
+
+    def get(self, key: bytes):
+        v = (C.c_uint64 * 3)()
+        r = lib.oc_smap_get(self.h, _ptr(key), len(key), v)
+        return (None if r else tuple(int(x) for x in v))
+
+    def delete(self, key: bytes):
+        old = (C.c_uint64 * 3)()
+        r = lib.oc_smap_delete(self.h, _ptr(key), len(key), old)
+        return (None if r else tuple(int(x) for x in old))
+
+    def export(self):
+        kb = C.c_uint64()
+        n = int(lib.oc_smap_export(self.h, None, 0, None, None, 0, C.byref(kb)))
+        keys = np.zeros(max(int(kb.value), 1), dtype=np.uint8)
+        koff = np.zeros(n + 1, dtype=np.uint64)
+        vals = np.zeros(3 * max(n, 1), dtype=np.uint64)
+        lib.oc_smap_export(self.h, keys.ctypes.data_as(vp), keys.size, koff.ctypes.data_as(vp),
+                           vals.ctypes.data_as(vp), n, C.byref(kb))
+        kbytes = keys.tobytes()
+        return {kbytes[int(koff[i]):int(koff[i + 1])]: tuple(int(x) for x in vals[3 * i:3 * i + 3]) for i in range(n)}
+
+    # Index over the bounded map (index.go:81-165)
+    def index_op(self, ns: bytes, key: bytes, op: int, fid=0, off=0, size=0):
+        ff, fb = C.c_uint64(), C.c_uint64()
+        lib.oc_bindex_op(self.h, _ptr(ns), len(ns), _ptr(key), len(key), op, fid, off, size, C.byref(ff), C.byref(fb))
+        return int(ff.value), int(fb.value)  # WriteStat{FreeWalFid, FreeBytes}
+
+    def index_get(self, ns: bytes, key: bytes):
+        f, o, z = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        st = lib.oc_bindex_get(self.h, _ptr(ns), len(ns), _ptr(key), len(key), C.byref(f), C.byref(o), C.byref(z))
+        return int(st), (int(f.value), int(o.value), int(z.value))
+
+    def put_segment(self, seg, start_off, base_time, ns_size, etag_size, mode, fid, use_rec_fid=False):
+        seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+        n = C.c_uint64()
+        ec = lib.oc_bindex_put_segment(self.h, _ptr(seg), seg.size, start_off, base_time, ns_size, etag_size, mode,
+                                       fid, int(use_rec_fid), C.byref(n))
+        return int(ec), int(n.value)
+
+    def compact_filter(self, seg, start_off, base_time, ns_size, etag_size, src_fid, n_rows):
+        seg = np.frombuffer(seg, dtype=np.uint8) if isinstance(seg, (bytes, bytearray)) else seg
+        keep = np.zeros(max(n_rows, 1), dtype=np.uint8)
+        nv = lib.oc_bindex_compact_filter(self.h, _ptr(seg), seg.size, start_off, base_time, ns_size, etag_size,
+                                          src_fid, keep.ctypes.data_as(vp), n_rows)
         return keep[:n_rows], int(nv)

@@ -196,3 +196,116 @@ def test_index_config_b_scale(ctx):
     _, kept = IX.compact_one_wal_filtered(dst, hint_w, W.load_wal(data, 1), ix)
     assert kept == n
     assert bytes(dst.data)[40:] == data[40:]  # every record kept, same base time: the same bytes
+
+
+def test_write_stats_vs_oracle(ctx):
+    """bcw_index_apply_stat: every op's WriteStat (index.go:100-165) equals the reference index's -- the oracle's
+    SimpleMap/ShardMap restatement with a Limited above the key count (no eviction, the device's regime) --
+    including ops on keys an earlier op of the same batch touched; writeIndex's per-fid sums follow."""
+    rng = random.Random(11)
+    keys = _keyset(rng, 400)
+    ix = IX.Index(ctx, keys=1024, arena_bytes=1 << 16)
+    om = O.SMap(1 << 20, 1 << 19, 32, 5)
+    for batch in range(8):
+        n = rng.choice([1, 64, 700, 3000])
+        ops, ks, fids, offs, sizes, want = [], [], [], [], [], []
+        for _ in range(n):
+            ns, k = rng.choice(keys)
+            op = rng.choice([0, 0, 0, 1, 2])
+            f, o, z = rng.randrange(1, 9), rng.randrange(40, 1 << 40), rng.randrange(5, 1 << 20)
+            ops.append(op)
+            ks.append(ns + k)
+            fids.append(f)
+            offs.append(o)
+            sizes.append(z)
+            want.append(om.index_op(ns, k, op, f, o, z))
+        if batch % 2:
+            ref = {}
+            for wf, wb in want:  # writeStats[stat.FreeWalFid] += stat.FreeBytes (db_impl.go:450)
+                ref[wf] = ref.get(wf, 0) + wb
+            assert ix.write_index(ops, ks, fids, offs, sizes) == ref
+            continue
+        found, ffid, fbytes = ix.apply(ops, ks, fids, offs, sizes, stats=True)
+        for i, (wf, wb) in enumerate(want):
+            assert (int(ffid[i]), int(fbytes[i])) == (wf, wb), (batch, i, ops[i])
+            if found[i] == 0:
+                assert wb == 0 and wf == 0
+    # the device agrees with the oracle map on every key afterwards
+    st, fid, off, size = ix.get_many([ns + k for ns, k in keys])
+    for j, (ns, k) in enumerate(keys):
+        ost, ov = om.index_get(ns, k)
+        assert st[j] == ost and (ost == 1 or (int(fid[j]), int(off[j]), int(size[j])) == ov), j
+    ix.close()
+
+
+def test_rebuild_over_existing_keys_takes_no_arena(ctx):
+    """only keys new to the index take arena space: a rebuild over the same keys (recovery of a WAL whose keys
+    are indexed) leaves the arena as it was (round-2 rebuild regression: every op appended its key)"""
+    data, _ = cases.wal_of([cases.rec(i, vlen=100) for i in range(3000)])
+    ix = IX.Index(ctx, keys=4096, arena_bytes=1 << 20)
+    ix.recover_segment(data, L.MODE_RECORD, 1, 40, BASE, 20, 20)
+    a0 = ix.stats().arena_used
+    assert a0 > 0
+    for _ in range(4):
+        dres, ires = ix.recover_segment(data, L.MODE_RECORD, 2, 40, BASE, 20, 20)
+        assert ires.n_done == 3000
+    s = ix.stats()
+    assert s.arena_used == a0 and s.live == 3000
+    assert {v[0] for v in ix.export().values()} == {2}
+    ix.close()
+
+
+def test_bounded_index_snapshot_filter(ctx):
+    """A bounded Go index (IndexLimited below the key count, db.go:70-72): recovery evicts keys
+    (map.go:185-187), doFilter drops their records ("deleted or evicted", compaction.go:330-333). The device
+    filter runs against a snapshot of the Go index's live entries (bcw_index_clear + apply): keep masks and
+    the re-encoded dst / hint bytes equal the oracle's over the evicting map."""
+    files = _wal_set(5, nfiles=3, n=500, nkeys=1500, vlens=(10, 300, 5000))
+    om = O.SMap(1024, 512, 32, 5, seed=9)  # 16 shards of 64 buckets / 32 entries
+    for fid in sorted(files):
+        om.set_now(fid)
+        data, hint = files[fid]
+        ec, n = om.put_segment(hint, 40, BASE, 20, 0, 1, fid)
+        assert ec == 0 and n == 500
+    assert om.size() == 512
+    snap = om.export()
+    assert len(snap) == 512
+    ix = IX.Index(ctx)
+    ix.apply([L.IDX_PUT], [b"x" * 20 + b"stale"], [9], [99], [9])  # cleared by the snapshot load
+    ix.load_snapshot(snap)
+    assert ix.stats().live == 512 and ix.export() == snap
+    for src_fid in (1, 3):
+        src = files[src_fid][0]
+        keep_ref, nv = om.compact_filter(src, 40, BASE, 20, 20, src_fid, 500)
+        assert nv == 500 and 0 < int(keep_ref.sum()) < 500
+        dst, hint = W.WalFile(9, BASE), W.WalFile(9, BASE)
+        offs, kept = IX.compact_one_wal_filtered(dst, hint, W.load_wal(src, src_fid), ix)
+        assert kept == int(keep_ref.sum())
+        rd, rh = O.Writer(BASE, BASE), O.Writer(BASE, BASE)
+        ec, _, nin, roffs = O.compact_append(rd, rh, 9, src, 40, BASE, BASE, 20, 20, keep_ref)
+        assert ec == 0 and bytes(dst.data) == rd.data() and bytes(hint.data) == rh.data()
+        np.testing.assert_array_equal(offs[:nin], roffs[:nin])
+    ix.close()
+
+
+def test_hint_recovery_wide_namespace(ctx):
+    """NsSize 300: the hint key offset (NsSize + len(uvarint keyLen), hint.go:62-66) exceeds the table's u8
+    column; the device index recomputes it from the payload"""
+    ns = bytes(i % 256 for i in range(300))
+    w = O.Writer(BASE, BASE)
+    offs = [1000 + 37 * i for i in range(300)]
+    for i in range(300):  # HintRecord.Encode (hint.go:32-48); a data WAL cannot carry NsSize 300 (byte(headerSize))
+        w.write(O.hint_encode(ns, b"k%05d" % i + bytes(i % 200), 4, offs[i], 60 + i))
+    hint = w.data()
+    oc = O.Index()
+    assert oc.put_segment(hint, 40, BASE, 300, 0, 1, 4)[0] == 0
+    ix = IX.Index(ctx)
+    dres, ires = ix.recover_segment(hint, L.MODE_HINT, 4, 40, BASE, 300, 0)
+    assert ires.err_class == 0 and ires.n_done == 300
+    exp = ix.export()
+    assert len(exp) == oc.live() == 300
+    for mk, v in exp.items():
+        assert oc.get(mk[:300], mk[300:]) == (0, v)
+    got = []
+    W.iterate_hint(W.load_wal(hint, 4), lambda h: got.append((h.ns, h.key, h.off)), ns_size=300)
+    assert got == [(ns, b"k%05d" % i + bytes(i % 200), offs[i]) for i in range(300)]

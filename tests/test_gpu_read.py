@@ -100,3 +100,23 @@ def test_read_fuzz(ctx, seed):
     for verify in (True, False):
         st = check(ctx, data, ro, rs, verify)
         assert (st == 0).sum() > 1000
+
+
+@pytest.mark.parametrize("vlen", [32761 - 60, 33000, 40000, 65400])
+def test_read_crafted_long_full_fragment(ctx, vlen):
+    """A crafted single Full fragment longer than a block's data area (u16 length up to 65535): WalParseRecord
+    accepts it when it fits the span WalRecordSize computes. The verify path shifts lane chunks by up to the
+    fragment length, so it needs the 2^15 shift operator (shifts of 32 KiB and more)."""
+    payload = cases.rec(5, vlen=vlen)
+    assert len(payload) < 65536
+    sb = bytearray(40)
+    sb[:] = O.Writer(BASE, BASE).data()[:40]
+    hdr = O.compute_crc32(payload).to_bytes(4, "little") + len(payload).to_bytes(2, "little") + bytes([1])
+    rs = O.wal_record_size(40, len(payload))
+    data = bytes(sb) + hdr + payload
+    data += bytes(40 + rs - len(data) + 16)
+    bad = bytearray(data)
+    bad[40 + 7 + len(payload) - 3] ^= 0x10  # flips a byte near the end: only the high lanes' chunks change
+    for img in (data, bytes(bad)):
+        st = check(ctx, img, [40, 40, 40], [len(payload), len(payload) - 1, len(payload) + 1], verify=True)
+        assert st[0] == (L.RD_OK if img is data else L.RD_CRC), st
