@@ -50,6 +50,7 @@ def parse():
                          "(own stream, segment, record table); the headline value is one segment at a time")
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events bracket every N-th k_crc launch of the timed region")
+    ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_v6_k_crc_pmc.json"),
                     help="PMC traffic summary (rocprofv3 --pmc of this command) to report as roofline.traffic")
     return ap.parse_args()
@@ -175,22 +176,38 @@ def end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec, 
 
 def main():
     args = parse()
+    from bitcaskdb_amd import shard
+    # --gpus N without a launcher: start the N rank processes here (before anything touches a GPU) and exit with
+    # their status; under torch.distributed.run WORLD_SIZE must equal N
+    try:
+        plans = shard.launch_plan(args.gpus, os.environ)
+    except ValueError as e:
+        raise SystemExit(f"bench.py: {e}")
+    if plans is not None:
+        sys.exit(shard.spawn_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], plans))
+    if args.launcher_selftest:  # CPU test of the launcher: report the rank environment, touch no GPU
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}),
+              flush=True)
+        return
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    share = world > ndev  # more ranks than GPUs (the 1-GPU box's two-rank test): RCCL needs one GPU per rank
+    torch.cuda.set_device(shard.rank_device(local, ndev))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
     dev = torch.device("cuda", torch.cuda.current_device())
+    red_dev = None if share else dev  # max-over-ranks tensor: host memory under gloo
 
     from bitcaskdb_amd import _lib as L
     from bitcaskdb_amd import Context
-    from bitcaskdb_amd import shard
 
     # ---- this rank's segments: built on the host with the product writer, then copied to HBM ----
     # A scan over many WAL files (recovery, compaction of every wal, config D) keeps `inflight` segments in
@@ -315,7 +332,7 @@ def main():
             L.lib.bcw_ctx_set_profiling(cx.handle, 0)
         wall_p = shard.timed_steps(step_rot, args.steps, 0, torch.cuda.synchronize,
                                    dist.barrier if world > 1 else None)
-        wall_p = shard.max_over_ranks(wall_p, dist, dev)
+        wall_p = shard.max_over_ranks(wall_p, dist, red_dev)
         bytes_p = sum(slots[i % nslot]["seg_len"] for i in range(args.steps))
         pipelined = {"inflight": nslot, "value": round(shard.aggregate_gib_s([bytes_p / args.steps] * world, wall_p,
                                                                                args.steps), 2),
@@ -332,7 +349,7 @@ def main():
     for cx in all_ctx:
         L.lib.bcw_ctx_set_profiling(cx.handle, 0)
 
-    wall_max = shard.max_over_ranks(wall, dist, dev)
+    wall_max = shard.max_over_ranks(wall, dist, red_dev)
     ms_per_step = wall_max / args.steps * 1e3
     # whole job: this rank's bytes per step (segments of equal size on every rank, to a record) x ranks
     value = shard.aggregate_gib_s([bytes_total / args.steps] * world, wall_max, args.steps)
@@ -415,7 +432,7 @@ def main():
                                + ("4 KiB values" if args.config == "B" else "Zipf(1.1) 128 B-64 KiB values")
                                + ", device-resident decode+CRC+record parse",
                    "seg_bytes": seg_len, "records": n_rec, "fragments": n_frags,
-                   "parallelism": f"one independent segment per GPU x{world}",
+                   "parallelism": f"one independent segment per GPU x{world}" + (" (ranks sharing GPUs)" if share else ""),
                    },
         "roofline": roofline, "cpu_baseline": cpu,
         "pcie_inclusive_GiBs": round(pcie, 2) if pcie else None,

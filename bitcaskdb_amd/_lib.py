@@ -92,6 +92,7 @@ ST_OK, ST_INVALID, ST_PANIC, ST_UNSUPPORTED = 0, 1, 2, 3
 ERR_NONE, ERR_CRC, ERR_TYPE, ERR_PANIC = 0, 1, 2, 3
 SB_OK, SB_SHORT, SB_CRC, SB_MAGIC, SB_BLOCKSIZE = 0, 1, 2, 3, 4
 E_CAPACITY = -4
+OPT_CHASE_DIRECT = 1  # bcw_ctx_set_option: k_chase direct-sum workgroup limit (0 forces the look-back)
 E_IO = -6
 ENC_COMPACT, ENC_HINT = 0, 1
 ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC, ENC_ERR_TABLE, ENC_ERR_STALE = 0, 1, 2, 3, 4, 5
@@ -121,6 +122,7 @@ def _load():
         "bcw_ctx_kernel_times": (C.c_int, [vp, C.POINTER(C.c_double), u64p, C.c_int]),
         "bcw_kernel_name": (C.c_char_p, [C.c_int]),
         "bcw_ctx_reserve_fragments": (C.c_int, [vp, C.c_uint64]),
+        "bcw_ctx_set_option": (C.c_int, [vp, C.c_int, C.c_uint64]),
         "bcw_wal_record_size": (C.c_uint64, [C.c_uint64, C.c_uint64]),
         "bcw_wal_block_index_range": (None, [C.c_uint64, C.c_uint64, u64p, u64p, u64p]),
         "bcw_crc32c_masked": (C.c_uint32, [vp, C.c_uint64]),

@@ -416,6 +416,7 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   s.nlb = nwg;
   s.tickets = 0;
   s.epoch = 1;
+  s.chase_direct = c->chase_direct;
   // on the codec's stream: a null-stream hipMemset is not ordered before kernels on a non-blocking
   // stream, and a look-back word zeroed after k_chase published it would never be seen again
   if (hipMemsetAsync(s.lb, 0, nwg * 8, c->cur) != hipSuccess ||
@@ -489,6 +490,19 @@ int bcw_ctx_reserve_fragments(bcw_ctx* c, uint64_t n) {
   if (!c || n >= 0xfffffff0ull) return BCW_E_INVAL;
   c->frag_hint = std::max(c->frag_hint, n);
   return BCW_OK;
+}
+
+int bcw_ctx_set_option(bcw_ctx* c, int option, uint64_t value) {
+  if (!c) return BCW_E_INVAL;
+  switch (option) {
+    case BCW_OPT_CHASE_DIRECT:
+      if (value > BCW_CHASE_DIRECT_MAX) return BCW_E_INVAL;
+      c->s.chase_direct = (uint32_t)value;
+      c->chase_direct = (uint32_t)value;
+      return BCW_OK;
+    default:
+      return BCW_E_INVAL;
+  }
 }
 
 int bcw_ctx_set_profiling(bcw_ctx* c, int mask) {

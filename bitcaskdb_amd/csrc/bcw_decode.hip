@@ -125,7 +125,7 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 constexpr int kSpec = 8;
 constexpr int kChaseHold = 16;
 constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
-constexpr int kDirect = 1024;  // k_chase workgroups up to which each sums all predecessors' aggregates
+constexpr int kDirect = BCW_CHASE_DIRECT_MAX;  // k_chase workgroups up to which each sums all predecessors' aggregates
 
 // visit(k, start, len, crc, type) for every header of the block; returns the fragment count
 template <typename V>
@@ -183,7 +183,8 @@ __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, u
 __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
                                               uint64_t nblocks, uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
                                               uint64_t frag_cap, uint64_t* __restrict__ lb, uint64_t* __restrict__ misc,
-                                              uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc) {
+                                              uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc,
+                                              uint32_t direct_max) {
   // {crc, start | len << 16} and type of each lane's headers: 9 KiB, so a k_chase workgroup fits beside a k_crc
   // workgroup (which leaves 11 KiB of the CU's LDS) when another segment's decode is in flight
   __shared__ uint32_t s_hold[kChaseHold][2][64];
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   const uint64_t tag = epoch << 40;
   const uint64_t nwg_all = (nblocks + 63) / 64;
   uint64_t excl = 0;
-  if (nwg_all <= (uint64_t)kDirect) {
+  if (nwg_all <= (uint64_t)direct_max) {  // direct_max <= kDirect (bcw_ctx_set_option)
     if (lane == 0) __hip_atomic_store(&lb[wg], tag | (kLbAgg << 38) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t v[kDirect / 64];
 #pragma unroll
@@ -1138,11 +1139,22 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
     r.g1 = fbase[be];
     return r;
   };
+  // the first fragment chunk of an item, loaded with the item one item ahead (fbase -> frags is a dependent pair,
+  // so it trails the item's own loads by one round trip but is in flight during the current item's emission)
+  auto fetch_chunk = [&](uint32_t g0) -> uint4 {
+    const uint64_t g = (uint64_t)g0 + lane;
+    return reinterpret_cast<const uint4*>(frags)[g < frag_cap ? g : frag_cap - 1];
+  };
+  // the first failing fragment (written by k_crc's final scan): nothing at or after it is emitted
+  const uint64_t err_frag = misc[M_ERR_FRAG];
   ItemIn nxt_in = fetch_item((uint64_t)blockIdx.x * kRecWaves + wave);
+  uint4 nxt_chunk = fetch_chunk(nxt_in.g0);
   for (uint64_t item = (uint64_t)blockIdx.x * kRecWaves + wave; item < nitems; item += stride) {
   const uint64_t b = item * bpw;
   const ItemIn cur_in = nxt_in;
+  const uint4 cur_chunk = nxt_chunk;
   nxt_in = fetch_item(item + stride);
+  nxt_chunk = fetch_chunk(nxt_in.g0);
   do {  // this item's record emission
   if (b >= nblocks) break;
   const Xf in = xf_compose(xf_compose(cur_in.w, cur_in.p), cur_in.l);
@@ -1152,14 +1164,15 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
   uint64_t rec = in.n_emit;
   uint64_t g0 = cur_in.g0, g1 = cur_in.g1;
   if (g1 > frag_cap) g1 = frag_cap;
-  const uint64_t err_frag = misc[M_ERR_FRAG];
   if (g1 > err_frag) g1 = err_frag;  // nothing at or after the first failing fragment is emitted
   uint8_t* st = s_stage[wave][lane];
   for (uint64_t c0 = g0; c0 < g1; c0 += 64) {
     const uint64_t g = c0 + lane;
     const bool valid = g < g1;
     Frag f{};
-    if (valid) f = frags[g];
+    if (c0 == g0) __builtin_memcpy(&f, &cur_chunk, sizeof f);  // prefetched with the item
+    else if (valid) f = frags[g];
+    if (!valid) f = Frag{};
     const uint32_t len = valid ? f.len : 0u;
     const uint64_t D = (uint64_t)p.start_off + (uint64_t)f.blk * kBlock + f.start;
     const bool isE = valid && (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST);
@@ -1199,18 +1212,28 @@ __global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg
         else { off2 = D_fa; first2 = (uint32_t)(c0 + fa); }
       }
     }
+    // the record each emitting lane completes (evaluated by every lane: the shuffle below needs all lanes)
+    uint64_t foff;
+    uint32_t ffrag;
+    if (acc_before == 0) { foff = D; ffrag = (uint32_t)g; }
+    else if (prev < 0 && acc > 0) { foff = off; ffrag = first; }
+    else { foff = D_fnz; ffrag = (uint32_t)(c0 + fnz); }
+    const bool full = f.type == BCW_RECORD_FULL;
+    const uint32_t src = full ? (uint32_t)g : ffrag;  // the record's bytes start in fragment src
+    // its first fragment: this lane's (Full), another lane's of this chunk (shuffled), else loaded below
+    const bool src_here = src >= c0 && src < c0 + 64;
+    const uint32_t sw0 = (uint32_t)__shfl((int)f.blk, src_here ? (int)(src - c0) : (int)lane, 64);
+    const uint32_t sw1 = (uint32_t)__shfl((int)((uint32_t)f.start | ((uint32_t)f.len << 16)),
+                                          src_here ? (int)(src - c0) : (int)lane, 64);
     if (isE) {
-      uint64_t foff;
-      uint32_t ffrag;
-      if (acc_before == 0) { foff = D; ffrag = (uint32_t)g; }
-      else if (prev < 0 && acc > 0) { foff = off; ffrag = first; }
-      else { foff = D_fnz; ffrag = (uint32_t)(c0 + fnz); }
-      const bool full = f.type == BCW_RECORD_FULL;
       const uint64_t size = full ? (uint64_t)len : acc_before + len;
-      const uint32_t src = full ? (uint32_t)g : ffrag;  // the record's bytes start in fragment src
       const uint64_t r = rec + __builtin_popcountll(E & below);
+      Frag f0 = f;
+      if (!full) {
+        if (src_here) { f0.blk = sw0; f0.start = (uint16_t)sw1; f0.len = (uint16_t)(sw1 >> 16); }
+        else f0 = frags[src];
+      }
       // stage the record prefix (when its first fragment holds it) with aligned 16 B loads
-      const Frag f0 = full ? f : frags[src];
       const uint64_t a0 = (uint64_t)p.start_off + (uint64_t)f0.blk * kBlock + f0.start;
       uint64_t want = size < kStage ? size : kStage;
       if (want > f0.len) want = f0.len;
@@ -1307,7 +1330,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   const uint32_t nb_grid = (uint32_t)((nblocks + 63) / 64);
   pr.begin(K_CHASE, stream, ev);
   k_chase<<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags, s.frag_cap, s.lb,
-                                       s.misc, s.tickets, s.epoch, tabs.initc);
+                                       s.misc, s.tickets, s.epoch, tabs.initc, s.chase_direct);
   pr.end(K_CHASE, stream, ev);
   s.tickets += nb_grid;
   if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse

@@ -84,6 +84,7 @@ struct Scratch {
   Xf* wgx = nullptr;           // [k_crc workgroups] workgroup aggregates -> exclusive prefixes
   uint64_t nwave_cap = 0;
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
+  uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
 };
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
@@ -228,6 +229,7 @@ struct bcw_ctx {
   bcw_decode_result* d_result = nullptr;
   bcw_index_result* d_ires = nullptr;  // sync index calls
   uint32_t last_start_off = 0;
+  uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // BCW_OPT_CHASE_DIRECT
   uint64_t last_nfrag_cap = 0;
   bcw::Prof prof;
 };

@@ -10,8 +10,11 @@ code the GPU benchmark runs.
 """
 from __future__ import annotations
 
+import os
+import socket
+import subprocess
 import time
-from typing import Callable, Optional, Sequence
+from typing import Callable, Mapping, Optional, Sequence
 
 
 def segment_seed(base: int, rank: int) -> int:
@@ -60,3 +63,64 @@ def aggregate_gib_s(bytes_per_rank: Sequence[int], wall_max_s: float, steps: int
     if wall_max_s <= 0 or steps <= 0:
         raise ValueError("empty timing")
     return sum(bytes_per_rank) / 2 ** 30 / (wall_max_s / steps)
+
+
+def launch_plan(gpus: int, env: Mapping[str, str]) -> Optional[list[dict]]:
+    """How `bench.py --gpus N` runs: None when this process is already the job (N = 1, or a rank started by
+    torch.distributed.run with WORLD_SIZE = N); otherwise the environments of the N rank processes to start,
+    one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1). A WORLD_SIZE that disagrees
+    with --gpus is an error: the job would silently run on the wrong number of GPUs."""
+    if gpus < 1:
+        raise ValueError(f"--gpus {gpus}: need at least one GPU")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise ValueError(f"--gpus {gpus} but WORLD_SIZE={world}: launch with --nproc-per-node {gpus} "
+                             f"or drop the launcher")
+        return None
+    if gpus == 1:
+        return None
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    plans = []
+    for r in range(gpus):
+        e = dict(env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        plans.append(e)
+    return plans
+
+
+def spawn_ranks(argv: Sequence[str], plans: Sequence[Mapping[str, str]], timeout: Optional[float] = None) -> int:
+    """Start one child process per plan (never an exec of this process: the children are new programs, started
+    before this process touches a GPU) and wait for all of them; returns the first nonzero exit code, else 0.
+    A rank that fails takes the others down (they would wait at the rendezvous or a barrier)."""
+    procs = [subprocess.Popen(list(argv), env=dict(e)) for e in plans]
+    rc = 0
+    deadline = None if timeout is None else time.monotonic() + timeout
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:
+                    q.terminate()
+        if deadline is not None and time.monotonic() > deadline:
+            for q in pending:
+                q.kill()
+            return rc or 124
+        time.sleep(0.05)
+    return rc
+
+
+def rank_device(local_rank: int, device_count: int) -> int:
+    """The GPU of a local rank: its own when the node has enough, else ranks share devices round-robin (the
+    1-GPU box's multi-rank test)."""
+    if device_count <= 0:
+        raise RuntimeError("no GPU")
+    return local_rank % device_count

@@ -117,6 +117,12 @@ class Context:
     def set_stream(self, stream_ptr: int | None):
         L.lib.bcw_ctx_set_stream(self._h, C.c_void_p(stream_ptr or 0))
 
+    def set_option(self, option: int, value: int):
+        """bcw_ctx_set_option (L.OPT_*)"""
+        rc = L.lib.bcw_ctx_set_option(self._h, option, value)
+        if rc != 0:
+            raise ValueError(f"bcw_ctx_set_option({option}, {value}): {L.lib.bcw_strerror(rc).decode()}")
+
     def sync(self):
         rc = L.lib.bcw_ctx_sync(self._h)
         if rc != 0:

@@ -185,6 +185,14 @@ int bcw_ctx_set_profiling(bcw_ctx* ctx, int mask);
 int bcw_ctx_set_profiling_sample(bcw_ctx* ctx, int every);
 int bcw_ctx_kernel_times(bcw_ctx* ctx, double* total_ms, uint64_t* launches, int n);
 const char* bcw_kernel_name(int kernel_id);
+/* Tuning / diagnostic options (bcw_ctx_set_option; BCW_E_INVAL for an unknown option or value):
+ *   BCW_OPT_CHASE_DIRECT  k_chase workgroups (64 blocks = 2 MiB each) up to which every workgroup sums all of its
+ *                         predecessors' fragment counts directly; larger segments use the decoupled look-back.
+ *                         0..BCW_CHASE_DIRECT_MAX (default BCW_CHASE_DIRECT_MAX); 0 forces the look-back at
+ *                         every size (the tests drive that branch on small segments with it). */
+#define BCW_OPT_CHASE_DIRECT 1
+#define BCW_CHASE_DIRECT_MAX 1024
+int bcw_ctx_set_option(bcw_ctx* ctx, int option, uint64_t value);
 /* Size the context's fragment scratch for at least n fragments on the next decode (after a decode
  * reported retry_frag_capacity). n must be < 2^32 - 16 (BCW_E_INVAL otherwise, nothing stored). */
 int bcw_ctx_reserve_fragments(bcw_ctx* ctx, uint64_t n);

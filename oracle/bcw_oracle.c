@@ -709,7 +709,8 @@ oc_writer* oc_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_
   }
   uint8_t* ns = (uint8_t*)malloc(ns_size + 1);
   for (uint32_t i = 0; i < ns_size; ++i) ns[i] = (uint8_t)('A' + i % 26);
-  size_t vmax = value_mode == 1 ? 128 * 512 : value_len;
+  size_t vmax = value_mode == 1 ? 128 * 512 : value_mode == 2 ? 1400 : value_len;
+  uint8_t etag[20];
   uint8_t* key = (uint8_t*)malloc(key_len + 8);
   uint8_t* val = (uint8_t*)malloc(vmax + 8);
   uint8_t* rec = (uint8_t*)malloc(vmax + key_len + ns_size + 64);
@@ -720,6 +721,20 @@ oc_writer* oc_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_
       int lo = 0, hi = 511;
       while (lo < hi) { int mid = (lo + hi) / 2; if (cdf[mid] < u) lo = mid + 1; else hi = mid; }
       vl = 128u * (size_t)(lo + 1);
+    }
+    if (value_mode == 2) {
+      /* value_mode 2 (compaction tests): 200-1399 B values, every record with an expire (baseTime + 1 h + up to
+       * ~2 days), a 20 B etag on every third, a tombstone on every 17th */
+      vl = 200 + (size_t)(splitmix64(&s) % 1200);
+      fill_rand(&s, key, key_len);
+      if (key_len >= 8) oc_memcpy(key, &i, 8);
+      fill_rand(&s, val, vl);
+      fill_rand(&s, etag, sizeof etag);
+      const uint64_t expire = base_time + 3600 + splitmix64(&s) % 170000;
+      int64_t n = oc_record_encode(rec, ns, ns_size, key, key_len, val, vl, i % 3 == 0 ? etag : NULL,
+                                   i % 3 == 0 ? sizeof etag : 0, expire, i % 17 == 0, NULL, 0, base_time);
+      oc_writer_write(w, rec, (size_t)n);
+      continue;
     }
     fill_rand(&s, key, key_len);
     if (key_len >= 8) oc_memcpy(key, &i, 8);

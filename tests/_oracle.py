@@ -144,6 +144,11 @@ lib.oc_bindex_compact_filter.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uin
                                          C.c_uint64, vp, C.c_uint64]
 
 
+def _bytes_at(ptr, n: int) -> bytes:
+    """n bytes at ptr (ctypes.string_at takes a C int size: images of 2 GiB and more need the buffer protocol)"""
+    return bytes((C.c_uint8 * n).from_address(ptr)) if n else b""
+
+
 def _ptr(a):
     if isinstance(a, (bytes, bytearray)):
         a = np.frombuffer(a, dtype=np.uint8)
@@ -187,8 +192,7 @@ class Writer:
         return int(lib.oc_writer_size(self.h))
 
     def data(self) -> bytes:
-        n = self.size()
-        return C.string_at(lib.oc_writer_data(self.h), n)
+        return _bytes_at(lib.oc_writer_data(self.h), self.size())
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -304,8 +308,7 @@ def decode_fast_pread(fd: int, length: int, start_off, base_time, ns_size, etag_
 def synth(target_bytes: int, max_records: int, seed: int, ns_size: int = 20, key_len: int = 100,
           value_len: int = 4096, value_mode: int = 0, base_time: int = 1_700_000_000) -> bytes:
     h = lib.oc_synth_segment(target_bytes, max_records, seed, ns_size, key_len, value_len, value_mode, base_time)
-    n = int(lib.oc_writer_size(h))
-    out = C.string_at(lib.oc_writer_data(h), n)
+    out = _bytes_at(lib.oc_writer_data(h), int(lib.oc_writer_size(h)))
     lib.oc_writer_free(h)
     return out
 

@@ -126,3 +126,75 @@ def test_config_e_compaction_200k(ctx):
     res2, _, hb2, _ = ctx.encode(src, L.ENC_HINT, 40, BASE, 5, 40, 40, 20, 20)
     assert res2.err_class == ec2 == 0 and res2.n_in == nin2 == n
     assert hb2 == ref_hint[40:], "hint-by-wal bytes differ"
+
+
+@pytest.fixture
+def lookback_ctx():
+    """a context whose k_chase takes the decoupled look-back at every size (BCW_OPT_CHASE_DIRECT 0)"""
+    from bitcaskdb_amd import Context
+    c = Context(0)
+    c.set_option(L.OPT_CHASE_DIRECT, 0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("where", [None, 0.3, 0.999])
+def test_chase_lookback_branch_256mib(lookback_ctx, where):
+    """k_chase's decoupled look-back (the > 1024-workgroup branch, bcw_decode.hip k_chase) forced on a 256 MiB
+    config-B shape (128 workgroups chaining inclusive prefixes), clean and with a flipped byte: every column
+    equals the oracle's."""
+    data = bytearray(O.synth(256 << 20, 0, 44))
+    if where is not None:
+        data[int(len(data) * where)] ^= 0x11
+    got, ref = full_parity(lookback_ctx, bytes(data), cases.params(), f"lookback flip@{where}")
+    assert (got.result.err_class == 0) == (where is None)
+
+
+def test_chase_lookback_config_c(lookback_ctx):
+    """the look-back over config C's divergent per-block fragment counts (256 MiB Zipf)"""
+    data = O.synth(256 << 20, 0, 45, value_mode=1)
+    got, _ = full_parity(lookback_ctx, data, cases.params(), "lookback C")
+    assert got.result.err_class == 0
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_segment_beyond_2gib(ctx, flip):
+    """a 2.25 GiB config-B-shape segment: 1,153 k_chase workgroups, past the direct-sum limit (1024), so the
+    product's default path takes the decoupled look-back; with a flipped byte beyond workgroup 1024 (past
+    2 GiB) the first failing fragment, delivered records and payloads still equal the oracle's."""
+    data = O.synth(9 << 28, 0, 46)
+    nwg = ((len(data) - 40 + 32767) // 32768 + 63) // 64
+    assert nwg > 1024
+    if flip:
+        b = bytearray(data)
+        pos = (2 << 30) + 40 + 12345 * 7
+        assert (pos - 40) // 32768 // 64 >= 1024
+        b[pos] ^= 0x40
+        data = bytes(b)
+    got, ref = full_parity(ctx, data, cases.params(), f"2.25GiB flip={flip}")
+    assert (got.result.err_class != 0) == flip
+    assert got.n_records > 500000
+
+
+def test_config_e_compaction_2m_rebase(ctx):
+    """config-E-scale compaction: 2,000,000 records carrying expires (a third with etags, every 17th a
+    tombstone), a random keep mask (70 %), and a dst baseTime 500,000 s below the source's, so every kept
+    record's expire delta grows and its varint lengthens (Record.Encode, record.go:57-138): the dst WAL, the
+    hint WAL and every returned offset equal oc_compact_append's (compaction.go:294-327)."""
+    n = 2_000_000
+    src = O.synth(1 << 40, n, 77, 20, 24, 0, 2)
+    rng = np.random.default_rng(5)
+    keep = (rng.random(n) < 0.7).astype(np.uint8)
+    dst_base = BASE - 500_000
+    dst, hint = O.Writer(dst_base, dst_base), O.Writer(dst_base, dst_base)
+    ec, er, nin, offs = O.compact_append(dst, hint, 11, src, 40, BASE, dst_base, 20, 20, keep)
+    assert ec == 0 and nin == n
+    res, wal, hb, goffs = ctx.encode(src, L.ENC_COMPACT, 40, dst_base, 11, 40, 40, 20, 20, keep)
+    assert res.err_class == 0 and res.n_in == n and res.n_written == int(keep.sum())
+    ref_wal, ref_hint = dst.data()[40:], hint.data()[40:]
+    assert len(wal) == len(ref_wal) and len(hb) == len(ref_hint)
+    w, rw = np.frombuffer(wal, np.uint8), np.frombuffer(ref_wal, np.uint8)
+    bad = np.nonzero(w != rw)[0]
+    assert bad.size == 0, f"dst WAL differs from byte {bad[:1]}"
+    assert hb == ref_hint, "hint WAL differs"
+    np.testing.assert_array_equal(goffs[:n], offs[:n])

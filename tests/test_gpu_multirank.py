@@ -1,0 +1,44 @@
+"""The multi-rank path on the GPU: libbcw driven from two rank processes at once (on a 1-GPU box both share
+device 0), each decoding its own segment against the oracle, and bench.py --gpus 2 starting its own ranks."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from bitcaskdb_amd import shard
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _clean_env():
+    return {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+
+
+def test_two_ranks_decode_vs_oracle():
+    plans = shard.launch_plan(2, _clean_env())
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "_rank_decode.py")], env=e,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for e in plans]
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+    got = json.loads([ln for ln in outs[0][0].splitlines() if ln.startswith("[")][-1])
+    assert [g["rank"] for g in got] == [0, 1] and [g["seed"] for g in got] == [42, 43]
+    assert all(g["ok"] and g["n"] > 0 for g in got), got
+    assert len({g["wall_max"] for g in got}) == 1
+
+
+def test_bench_gpus2_self_launch():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--seg-bytes", str(64 << 20),
+                          "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-extras", "--inflight", "1"],
+                         env=_clean_env(), capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 alone prints
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["value"] > 0 and ln["scaling"] == "weak"

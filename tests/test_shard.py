@@ -86,3 +86,38 @@ def test_gloo_world2_independent_segments():
     assert all(g["wall"] <= wall_max + 1e-9 for g in gathered)
     value = shard.aggregate_gib_s([g["seg"] for g in gathered], wall_max, 2)
     assert value > 0
+
+
+def test_launch_plan():
+    """bench.py --gpus N: N rank environments when no launcher started it, none under torchrun (WORLD_SIZE = N),
+    and an error when WORLD_SIZE disagrees with --gpus"""
+    assert shard.launch_plan(1, {}) is None
+    assert shard.launch_plan(4, {"WORLD_SIZE": "4", "RANK": "2"}) is None
+    plans = shard.launch_plan(4, {"PATH": "/bin"})
+    assert [p["RANK"] for p in plans] == ["0", "1", "2", "3"] == [p["LOCAL_RANK"] for p in plans]
+    assert {p["WORLD_SIZE"] for p in plans} == {"4"} and {p["MASTER_ADDR"] for p in plans} == {"127.0.0.1"}
+    assert len({p["MASTER_PORT"] for p in plans}) == 1 and all(p["PATH"] == "/bin" for p in plans)
+    with pytest.raises(ValueError):
+        shard.launch_plan(8, {"WORLD_SIZE": "2"})
+    with pytest.raises(ValueError):
+        shard.launch_plan(0, {})
+    assert [shard.rank_device(r, 1) for r in range(3)] == [0, 0, 0]
+    assert [shard.rank_device(r, 8) for r in range(8)] == list(range(8))
+
+
+def test_bench_launcher_starts_n_ranks():
+    """`python bench.py --gpus 3` with no launcher starts three rank processes itself (the driver's scaling run
+    can call bench.py --gpus 8 directly); the self-test mode reports each rank's environment without a GPU"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--launcher-selftest"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    ranks = sorted((json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith("{")), key=lambda d: d["RANK"])
+    assert [r["RANK"] for r in ranks] == ["0", "1", "2"] and {r["WORLD_SIZE"] for r in ranks} == {"3"}
+    bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--launcher-selftest"],
+                         env=dict(env, WORLD_SIZE="2"), capture_output=True, text=True, timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE=2" in bad.stderr

@@ -464,7 +464,7 @@ int main(int argc, char** argv) {
            rrun(k_records<2>, g4), rrun(k_records<4>, g4), rrun(k_records<8>, g4), rrun(k_records<15>, g4));
     const float ck = timeit([&] {
       k_chase<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, s.lb,
-                                                               s.misc, s.tickets, s.epoch, ctx->tabs.initc);
+                                                               s.misc, s.tickets, s.epoch, ctx->tabs.initc, s.chase_direct);
       s.tickets += (nblocks + 63) / 64;
       ++s.epoch;
     }, reps, st);
