@@ -6,6 +6,15 @@ import ctypes as C
 import os
 import re
 
+# One HIP runtime per process. PyTorch (device memory, streams and torch.distributed in bench.py and the tests) ships
+# its own libamdhip64 with the soname libamdhip64.so.7; loaded first, it is the runtime libbcw.so binds to. Loaded
+# after libbcw.so it would be a second runtime in the process, and with two processes sharing a GPU the second
+# runtime of each finds no device (measured: tools/probe/runtimes.py). Without PyTorch libbcw.so uses /opt/rocm's.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # BCW_LIB: an alternative build of the same library (A/B measurements of kernel variants only)
 LIB_PATH = os.environ.get("BCW_LIB") or os.path.join(_HERE, "libbcw.so")

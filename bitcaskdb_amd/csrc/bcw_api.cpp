@@ -326,11 +326,11 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
 
 static void free_scratch(Scratch& s) {
   (void)hipFree(s.fbase);
+  (void)hipFree(s.rbase);
+  (void)hipFree(s.bsum);
   (void)hipFree(s.lb);
+  (void)hipFree(s.lbe);
   (void)hipFree(s.frags);
-  (void)hipFree(s.pre);
-  (void)hipFree(s.wgagg);
-  (void)hipFree(s.wgx);
   (void)hipFree(s.misc);
   s = Scratch{};
 }
@@ -396,31 +396,30 @@ int bcw_ctx_sync(bcw_ctx* c) {
 
 static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   Scratch& s = c->s;
-  const uint64_t nwave = (uint64_t)c->num_cus * kCrcWaves;
-  if (nblocks <= s.nblocks_cap && frag_cap <= s.frag_cap && nwave <= s.nwave_cap && s.misc) return BCW_OK;
+  if (nblocks <= s.nblocks_cap && frag_cap <= s.frag_cap && s.misc) return BCW_OK;
   (void)hipStreamSynchronize(c->cur);
   const uint64_t nb = std::max(nblocks, s.nblocks_cap);
   const uint64_t fc = std::max(frag_cap, s.frag_cap);
   free_scratch(s);
   const uint64_t nwg = nb / 64 + 2;  // k_chase look-back words: one per 64-block workgroup
-  bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
-            hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
-            hipMalloc(&s.pre, (nb + 1) * sizeof(Xf)) == hipSuccess &&
-            hipMalloc(&s.wgagg, nwave * sizeof(Xf)) == hipSuccess &&
-            hipMalloc(&s.wgx, (nwave / kCrcWaves + 1) * sizeof(Xf)) == hipSuccess &&
+  bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.rbase, (nb + 1) * 4) == hipSuccess &&
+            hipMalloc(&s.bsum, (nb + 1) * sizeof(uint2)) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
+            hipMalloc(&s.lbe, nwg * 8) == hipSuccess && hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
             hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;
   s.frag_cap = fc;
-  s.nwave_cap = nwave;
   s.nlb = nwg;
   s.tickets = 0;
   s.epoch = 1;
   s.chase_direct = c->chase_direct;
   // on the codec's stream: a null-stream hipMemset is not ordered before kernels on a non-blocking
   // stream, and a look-back word zeroed after k_chase published it would never be seen again
-  if (hipMemsetAsync(s.lb, 0, nwg * 8, c->cur) != hipSuccess ||
-      hipMemsetAsync(s.misc, 0, 16 * sizeof(uint64_t), c->cur) != hipSuccess) {
+  // misc[15] (the first unknown-type fragment, an atomicMin in k_chase) starts at UINT64_MAX; every decode's
+  // finalizer resets it for the next one
+  if (hipMemsetAsync(s.lb, 0, nwg * 8, c->cur) != hipSuccess || hipMemsetAsync(s.lbe, 0, nwg * 8, c->cur) != hipSuccess ||
+      hipMemsetAsync(s.misc, 0, 15 * sizeof(uint64_t), c->cur) != hipSuccess ||
+      hipMemsetAsync(s.misc + 15, 0xff, sizeof(uint64_t), c->cur) != hipSuccess) {
     free_scratch(s);
     return BCW_E_HIP;
   }

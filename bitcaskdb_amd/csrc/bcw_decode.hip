@@ -20,9 +20,13 @@ namespace bcw {
 
 // ------------------------------------------------------------------------------------------
 // misc counters (Scratch::misc)
-enum { M_FIRST_BAD = 0, M_NREC = 1, M_ERR_FRAG = 2, M_ERR_CLASS = 3, M_NFRAGS = 4, M_DONE_CRC = 5, M_DONE_REC = 6,
-       M_T_CRC0 = 10, M_T_SCAN0 = 11, M_T_SCAN1 = 12,  // wall_clock64 stamps (diagnostics)
-       M_TICKET = 13 };  // k_chase workgroup tickets (monotonic across launches)
+enum { M_FIRST_BAD = 0,  // first record whose parse fails (atomicMin in k_crc's emission)
+       M_NE = 1,         // Full/Last fragments of the whole segment (k_chase)
+       M_NFRAGS = 4, M_DONE_CRC = 5,
+       M_T_CRC0 = 10, M_T_FIN = 11,  // wall_clock64 stamps (diagnostics)
+       M_TICKET = 13,    // k_chase workgroup tickets (monotonic across launches)
+       M_BAD_CRC = 14,   // first fragment failing its CRC (atomicMin in k_crc; reset by k_chase)
+       M_BAD_TYPE = 15 };  // first fragment of an unknown type (atomicMin in k_chase; reset by k_crc's finalize)
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
@@ -180,9 +184,22 @@ __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, u
   frags[g] = f;
 }
 
+// Block summary for the record state machine (wal_iterator.go:69-96), written by k_chase from the headers alone:
+// the state of the iterator after a block depends only on the fragment types and lengths before it (a CRC
+// failure or unknown type ends the iteration, and nothing after the first failing fragment is emitted), so
+// record emission needs no CRC verdict. x = tail length | tail first non-empty fragment (block-local index,
+// 0xffff: none) << 16; y = that fragment's block-relative start | has-Full/Last << 16. The tail is the part
+// after the block's last Full/Last fragment (the whole block when it has none).
+constexpr uint32_t kSumHasE = 1u << 16;
+
+// ABL: ablation bits for tools/kbench only (0 in the product): 1 no predecessor sum, 2 no table writes,
+// 16 phase cycles (chase, sum, writes; s_memtime) summed into misc[7..9]
+template <int ABL = 0>
 __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
-                                              uint64_t nblocks, uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
-                                              uint64_t frag_cap, uint64_t* __restrict__ lb, uint64_t* __restrict__ misc,
+                                              uint64_t nblocks, uint32_t* __restrict__ fbase,
+                                              uint32_t* __restrict__ rbase, uint2* __restrict__ bsum,
+                                              Frag* __restrict__ frags, uint64_t frag_cap, uint64_t* __restrict__ lb,
+                                              uint64_t* __restrict__ lbe, uint64_t* __restrict__ misc,
                                               uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc,
                                               uint32_t direct_max) {
   // {crc, start | len << 16} and type of each lane's headers: 9 KiB, so a k_chase workgroup fits beside a k_crc
@@ -190,6 +207,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   __shared__ uint32_t s_hold[kChaseHold][2][64];
   __shared__ uint8_t s_type[kChaseHold][64];
   const uint32_t lane = threadIdx.x;
+  const uint64_t tc0 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t wg = 0;
   if (lane == 0) wg = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_TICKET]), 1ull) - ticket_base;
   wg = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)wg) |
@@ -201,6 +219,8 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     boff = (uint64_t)start_off + b * kBlock;
     bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
   }
+  // record-state summary of the block (see kSumHasE) and its first unknown-type fragment
+  uint32_t ne = 0, tacc = 0, tnz = 0xffffu, tst = 0, badk = 0xffffffffu;
   const uint32_t n = chase_block(seg, seg_len, boff, bufsize,
                                  [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
                                    if (k < (uint32_t)kChaseHold) {
@@ -208,25 +228,41 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                      s_hold[k][1][lane] = start | (len << 16);
                                      s_type[k][lane] = (uint8_t)type;
                                    }
+                                   if (type == BCW_RECORD_FULL || type == BCW_RECORD_LAST) {
+                                     ++ne;
+                                     tacc = 0;
+                                     tnz = 0xffffu;
+                                   } else {
+                                     if (len > 0 && tnz == 0xffffu) { tnz = k; tst = start; }
+                                     tacc += len;
+                                     if ((type < BCW_RECORD_FULL || type > BCW_RECORD_LAST) && badk == 0xffffffffu) badk = k;
+                                   }
                                  });
+  const uint64_t tc1 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
   const uint32_t incl = wave_add_scan(n, lane);
   const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+  const uint32_t incl_e = wave_add_scan(ne, lane);
+  const uint32_t tot_e = __builtin_amdgcn_readlane(incl_e, 63);
   // publish, then sum the predecessors. Up to kDirect workgroups (a 2 GiB segment) every workgroup publishes
-  // only its aggregate and sums all of its predecessors' at once (up to kDirect / 64 loads per lane, all in
-  // flight); beyond that, the decoupled look-back (64 predecessors per step, stopping at the nearest
-  // inclusive prefix), whose chain of inclusive prefixes would otherwise serialize the workgroups.
+  // only its aggregate (fragment and Full/Last counts packed: at most 64 * 4681 < 2^19 each) and sums all of its
+  // predecessors' at once (up to kDirect / 64 loads per lane, all in flight); beyond that, the decoupled look-back
+  // (64 predecessors per step, stopping at the nearest inclusive prefix, one word array per count), whose chain of
+  // inclusive prefixes would otherwise serialize the workgroups.
   const uint64_t tag = epoch << 40;
   const uint64_t nwg_all = (nblocks + 63) / 64;
-  uint64_t excl = 0;
-  if (nwg_all <= (uint64_t)direct_max) {  // direct_max <= kDirect (bcw_ctx_set_option)
-    if (lane == 0) __hip_atomic_store(&lb[wg], tag | (kLbAgg << 38) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t excl = 0, excl_e = 0;
+  if (ABL & 1) {
+  } else if (nwg_all <= (uint64_t)direct_max) {  // direct_max <= kDirect (bcw_ctx_set_option)
+    if (lane == 0)
+      __hip_atomic_store(&lb[wg], tag | (kLbAgg << 38) | tot | ((uint64_t)tot_e << 19), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     uint64_t v[kDirect / 64];
 #pragma unroll
     for (int k = 0; k < kDirect / 64; ++k) {
       const uint64_t q = lane + 64u * k;
       v[k] = q < wg ? __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
     }
-    uint64_t c = 0;
+    uint64_t c = 0, ce = 0;
 #pragma unroll
     for (int k = 0; k < kDirect / 64; ++k) {
       const uint64_t q = lane + 64u * k;
@@ -234,38 +270,68 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
         __builtin_amdgcn_s_sleep(1);
         v[k] = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (q < wg) c += v[k] & kLbMask;
+      if (q < wg) {
+        c += v[k] & 0x7ffffu;
+        ce += (v[k] >> 19) & 0x7ffffu;
+      }
     }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) c += (uint64_t)__shfl_xor((long long)c, d, 64);
+    for (int d = 32; d >= 1; d >>= 1) {
+      c += (uint64_t)__shfl_xor((long long)c, d, 64);
+      ce += (uint64_t)__shfl_xor((long long)ce, d, 64);
+    }
     excl = c;
+    excl_e = ce;
   } else {
-    if (lane == 0)
-      __hip_atomic_store(&lb[wg], tag | ((wg == 0 ? kLbInc : kLbAgg) << 38) | tot, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    for (uint64_t top = wg; top > 0;) {  // predecessors [top - 64, top)
+    const uint64_t fl = (wg == 0 ? kLbInc : kLbAgg) << 38;
+    if (lane == 0) {
+      __hip_atomic_store(&lb[wg], tag | fl | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&lbe[wg], tag | fl | tot_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // both counts walk back together; each stops at its own nearest inclusive prefix (the two words of a
+    // predecessor turn inclusive one after the other)
+    bool dn = false, de = false;
+    for (uint64_t top = wg; top > 0 && !(dn && de);) {  // predecessors [top - 64, top)
       const uint64_t q = top - 1 - lane;  // lane 0: the nearest
-      uint64_t v = 0;
+      uint64_t vn = 0, ve = 0;
       if (top > lane) {
-        while (((v = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
-          __builtin_amdgcn_s_sleep(1);
+        if (!dn)
+          while (((vn = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
+            __builtin_amdgcn_s_sleep(1);
+        if (!de)
+          while (((ve = __hip_atomic_load(&lbe[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
+            __builtin_amdgcn_s_sleep(1);
       }
-      const uint64_t inc = __ballot(top > lane && ((v >> 38) & 3u) == kLbInc);
-      const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive prefix
-      uint64_t c = (lane <= stop && top > lane) ? (v & kLbMask) : 0ull;
+      auto step = [&](uint64_t v, bool& done, uint64_t& acc) {
+        if (done) return;
+        const uint64_t inc = __ballot(top > lane && ((v >> 38) & 3u) == kLbInc);
+        const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive prefix
+        uint64_t c = (lane <= stop && top > lane) ? (v & kLbMask) : 0ull;
 #pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) c += (uint64_t)__shfl_xor((long long)c, d, 64);
-      excl += c;
-      if (inc) break;
+        for (int d = 32; d >= 1; d >>= 1) c += (uint64_t)__shfl_xor((long long)c, d, 64);
+        acc += c;
+        done = inc != 0;
+      };
+      step(vn, dn, excl);
+      step(ve, de, excl_e);
       top = top > 64 ? top - 64 : 0;
     }
-    if (lane == 0 && wg != 0)
+    if (lane == 0 && wg != 0) {
       __hip_atomic_store(&lb[wg], tag | (kLbInc << 38) | ((excl + tot) & kLbMask), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&lbe[wg], tag | (kLbInc << 38) | ((excl_e + tot_e) & kLbMask), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   const uint64_t g0 = excl + incl - n;
-  if (b < nblocks) {
+  const uint64_t tc2 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
+  if (b < nblocks && !(ABL & 2)) {
     fbase[b] = (uint32_t)(g0 < 0xffffffffull ? g0 : 0xffffffffull);
+    const uint64_t r0 = excl_e + incl_e - ne;
+    rbase[b] = (uint32_t)(r0 < 0xffffffffull ? r0 : 0xffffffffull);
+    bsum[b] = make_uint2(tacc | (tnz << 16), tst | (ne ? kSumHasE : 0u));
+    if (badk != 0xffffffffu)  // the first unknown-type fragment of the segment (reset by the previous finalize)
+      atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_TYPE]), (unsigned long long)(g0 + badk));
     const uint32_t nh = n < (uint32_t)kChaseHold ? n : (uint32_t)kChaseHold;
     for (uint32_t k = 0; k < nh; ++k) {
       const uint32_t sl = s_hold[k][1][lane];
@@ -277,229 +343,25 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
         if (k >= (uint32_t)kChaseHold) put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, initc);
       });
   }
+  if (ABL & 16) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t tc3 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&misc[7]), (unsigned long long)(tc1 - tc0));
+      atomicAdd(reinterpret_cast<unsigned long long*>(&misc[8]), (unsigned long long)(tc2 - tc1));
+      atomicAdd(reinterpret_cast<unsigned long long*>(&misc[9]), (unsigned long long)(tc3 - tc2));
+    }
+  }
   const uint64_t nwg = (nblocks + 63) / 64;
   if (wg == nwg - 1 && lane == 63) {
-    const uint64_t total = excl + tot;
+    const uint64_t total = excl + tot, total_e = excl_e + tot_e;
     fbase[nblocks] = (uint32_t)(total < 0xffffffffull ? total : 0xffffffffull);
+    rbase[nblocks] = (uint32_t)(total_e < 0xffffffffull ? total_e : 0xffffffffull);
     misc[M_NFRAGS] = total;
-    misc[M_DONE_CRC] = 0;  // k_crc's workgroup completion counter
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Record assembly. The iterator's per-fragment state machine (wal_iterator.go:69-96: `off` is
-// captured while the accumulated record is empty; Full emits the Full's data with that offset;
-// First/Middle append; Last appends and emits; any other type is an error) is summarised per block
-// as a transform Xf of the incoming state (acc_len, off, first). Transforms compose associatively:
-// each k_crc wave builds its blocks' transforms and their wave-local exclusive prefixes once its
-// fragments are verified, the last k_crc workgroup scans the wave aggregates, and k_records
-// composes the two for the incoming state of any block.
-
-__device__ __forceinline__ Xf xf_identity() {
-  Xf x{};
-  x.err_frag = 0xffffffffu;
-  return x;
-}
-// A then B
-__device__ __forceinline__ Xf xf_compose(const Xf& A, const Xf& B) {
-  if (A.err) return A;
-  Xf R;
-  R.pad = 0;
-  R.n_emit = A.n_emit + B.n_emit;
-  R.err = B.err;
-  R.err_class = B.err_class;
-  R.err_frag = B.err_frag;
-  if (B.has_emit) {
-    R.has_emit = 1; R.a = B.a; R.off = B.off; R.first = B.first; R.nz = 0;
-  } else if (A.has_emit) {
-    R.has_emit = 1; R.nz = 0;
-    R.a = A.a + B.a;
-    if (A.a > 0 || !B.nz) { R.off = A.off; R.first = A.first; }
-    else { R.off = B.off; R.first = B.first; }
-  } else {
-    R.has_emit = 0;
-    R.a = A.a + B.a;
-    R.nz = A.nz | B.nz;
-    if (A.nz) { R.off = A.off; R.first = A.first; } else { R.off = B.off; R.first = B.first; }
-  }
-  return R;
-}
-
-
-// Xf published to / read from other workgroups of the same launch: agent-scope atomic 8-byte
-// words, so no L2 writeback/invalidate fence is needed (the per-XCD L2s are not coherent)
-__device__ __forceinline__ void xf_store_agent(Xf* dst, const Xf& x) {
-  const uint64_t* w = reinterpret_cast<const uint64_t*>(&x);
-  uint64_t* d = reinterpret_cast<uint64_t*>(dst);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ Xf xf_load_agent(const Xf* src) {
-  Xf x;
-  uint64_t* w = reinterpret_cast<uint64_t*>(&x);
-  const uint64_t* s = reinterpret_cast<const uint64_t*>(src);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) w[i] = __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return x;
-}
-
-// contiguous lane mask [i, j], i <= j < 64
-__device__ __forceinline__ uint64_t lane_range(uint32_t i, uint32_t j) { return (~0ull >> (63u - j)) & (~0ull << i); }
-
-// Per-chunk view of 64 consecutive fragments (lane = fragment) for the record state machine.
-struct FragChunk {
-  uint64_t c0;                   // global index of lane 0's fragment
-  uint64_t bad, crcbad, E, NZ;   // ballots: failing (CRC or type), CRC failing, Full/Last, non-empty
-  uint32_t S, len;               // per lane: inclusive prefix of lengths, own length
-  uint64_t D;                    // per lane: data offset
-  __device__ __forceinline__ uint64_t sum(uint64_t m) const {  // lengths over a contiguous mask
-    if (!m) return 0;
-    const uint32_t i = __builtin_ctzll(m), j = 63u - __builtin_clzll(m);
-    return (uint64_t)(__builtin_amdgcn_readlane(S, j) - __builtin_amdgcn_readlane(S, i) +
-                      __builtin_amdgcn_readlane(len, i));
-  }
-  __device__ __forceinline__ uint64_t doff(uint32_t i) const {
-    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)D, i) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(D >> 32), i) << 32);
-  }
-  // transform of the contiguous run of fragments M (wal_iterator.go:69-96, stops at the run's
-  // first CRC (:79-82) or type (:94-95) failure)
-  __device__ __forceinline__ Xf run(uint64_t M) const {
-    Xf x = xf_identity();
-    uint64_t Mv = M;
-    const uint64_t b = bad & M;
-    if (b) {
-      const uint32_t fb = __builtin_ctzll(b);
-      Mv = M & ((1ull << fb) - 1ull);
-      x.err = 1;
-      x.err_class = ((crcbad >> fb) & 1ull) ? BCW_ERR_CRC : BCW_ERR_TYPE;
-      x.err_frag = (uint32_t)(c0 + fb);
-    }
-    const uint64_t Em = E & Mv;
-    uint64_t rest = Mv;  // fragments whose lengths are pending at the end of the run
-    if (Em) {
-      const uint32_t lastE = 63u - __builtin_clzll(Em);
-      rest = lastE == 63u ? 0ull : (Mv & (~0ull << (lastE + 1u)));
-      x.has_emit = 1;
-      x.n_emit = (uint64_t)__builtin_popcountll(Em);
-    }
-    x.a = sum(rest);
-    const uint64_t nzr = NZ & rest;
-    x.nz = (!Em && nzr) ? 1 : 0;
-    if (nzr) {
-      const uint32_t i = __builtin_ctzll(nzr);
-      x.off = doff(i);
-      x.first = (uint32_t)(c0 + i);
-    }
-    return x;
-  }
-};
-
-// One k_crc wave, after verifying fragments [f0, f1) of blocks [b0, b1): the record-state
-// transform of each block, written as the wave-exclusive prefix lpre[b]; returns the wave aggregate.
-__device__ Xf wave_block_xf(const Frag* __restrict__ frags, uint64_t f0, uint64_t f1, uint64_t b0, uint64_t b1,
-                            uint32_t start_off, uint32_t lane, Xf* __restrict__ lpre) {
-  Xf R = xf_identity();    // closed blocks
-  Xf cur = xf_identity();  // the open block
-  if (b0 >= b1) return R;
-  uint64_t ob = b0;
-  if (lane == 0) lpre[b0] = R;
-  for (uint64_t c0 = f0; c0 < f1; c0 += 64) {
-    const uint64_t g = c0 + lane;
-    const bool valid = g < f1;
-    Frag f{};
-    if (valid) f = frags[g];
-    FragChunk ch;
-    ch.c0 = c0;
-    ch.crcbad = __ballot(valid && !f.ok);
-    ch.bad = __ballot(valid && (!f.ok || f.type < BCW_RECORD_FULL || f.type > BCW_RECORD_LAST));
-    ch.E = __ballot(valid && (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST));
-    ch.NZ = __ballot(valid && f.len > 0);
-    ch.len = valid ? f.len : 0u;
-    ch.S = wave_add_scan(ch.len, lane);
-    ch.D = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
-    const uint64_t V = __ballot(valid);
-    const uint32_t blk = f.blk;
-    const uint32_t pblk = __shfl_up(blk, 1, 64);
-    uint64_t starts = __ballot(valid && (lane == 0 || blk != pblk));
-    const uint32_t last = 63u - __builtin_clzll(V);
-    while (starts) {
-      const uint32_t s = __builtin_ctzll(starts);
-      starts &= starts - 1ull;
-      const uint32_t e = starts ? __builtin_ctzll(starts) - 1u : last;
-      const uint64_t bb = (uint32_t)__builtin_amdgcn_readlane(blk, s);
-      const Xf x = ch.run(lane_range(s, e));
-      if (bb != ob) {
-        R = xf_compose(R, cur);
-        for (uint64_t q = ob + 1 + lane; q < bb; q += 64) lpre[q] = R;  // blocks without fragments
-        ob = bb;
-        cur = x;
-        if (lane == 0) lpre[bb] = R;
-      } else {
-        cur = xf_compose(cur, x);
-      }
-    }
-  }
-  R = xf_compose(R, cur);
-  for (uint64_t q = ob + 1 + lane; q < b1; q += 64) lpre[q] = R;
-  return R;
-}
-
-// Xf moved between lanes (10 dwords)
-__device__ __forceinline__ Xf xf_shfl(const Xf& x, int src) {
-  Xf r;
-  const uint32_t* a = reinterpret_cast<const uint32_t*>(&x);
-  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
-#pragma unroll
-  for (int i = 0; i < 10; ++i) o[i] = (uint32_t)__shfl((int)a[i], src, 64);
-  return r;
-}
-__device__ __forceinline__ Xf xf_readlane(const Xf& x, uint32_t src) {
-  Xf r;
-  const uint32_t* a = reinterpret_cast<const uint32_t*>(&x);
-  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
-#pragma unroll
-  for (int i = 0; i < 10; ++i) o[i] = (uint32_t)__builtin_amdgcn_readlane((int)a[i], src);
-  return r;
-}
-// inclusive wave scan of Xf over lanes [0, n) (n a power of two <= 64), lane-order composition
-__device__ __forceinline__ Xf wave_xf_scan(Xf x, uint32_t lane, uint32_t n) {
-  for (uint32_t d = 1; d < n; d <<= 1) {
-    const Xf y = xf_shfl(x, (int)(lane >= d ? lane - d : lane));
-    if (lane >= d) x = xf_compose(y, x);
-  }
-  return x;
-}
-
-// Exclusive scan of the k_crc workgroup aggregates by the last wave to finish (one wave,
-// kAggPer consecutive aggregates per lane per round, loaded back to back); totals -> misc.
-constexpr int kAggPer = 4;
-__device__ void scan_wg_aggregates(Xf* __restrict__ wgx, uint64_t n, uint64_t* __restrict__ misc, uint32_t lane) {
-  Xf carry = xf_identity();  // aggregate of earlier rounds
-  for (uint64_t r0 = 0; r0 < n; r0 += 64 * kAggPer) {
-    const uint64_t lo = r0 + (uint64_t)lane * kAggPer;
-    Xf x[kAggPer];
-#pragma unroll
-    for (int k = 0; k < kAggPer; ++k) x[k] = lo + k < n ? xf_load_agent(&wgx[lo + k]) : xf_identity();
-    Xf mine = x[0];
-#pragma unroll
-    for (int k = 1; k < kAggPer; ++k) mine = xf_compose(mine, x[k]);
-    const Xf incl = wave_xf_scan(mine, lane, 64);
-    const Xf prev = xf_shfl(incl, lane > 0 ? (int)lane - 1 : 0);
-    Xf run = lane > 0 ? xf_compose(carry, prev) : carry;
-#pragma unroll
-    for (int k = 0; k < kAggPer; ++k) {
-      if (lo + k < n) wgx[lo + k] = run;
-      run = xf_compose(run, x[k]);
-    }
-    carry = xf_compose(carry, xf_readlane(incl, 63));
-  }
-  if (lane == 0) {
-    misc[M_NREC] = carry.n_emit;
-    misc[M_ERR_FRAG] = carry.err ? carry.err_frag : ~0ull;
-    misc[M_ERR_CLASS] = carry.err ? carry.err_class : 0;
-    misc[M_FIRST_BAD] = ~0ull;
-    misc[M_DONE_REC] = 0;
+    misc[M_NE] = total_e;
+    misc[M_DONE_CRC] = 0;         // k_crc's workgroup completion counter
+    misc[M_BAD_CRC] = ~0ull;      // k_crc: first fragment failing its CRC
+    misc[M_FIRST_BAD] = ~0ull;    // k_crc: first record whose RecordFromBytes / Decode fails
   }
 }
 
@@ -700,16 +562,331 @@ struct BodyDesc {
   __device__ __forceinline__ uint32_t lo() const { return (meta >> 19) & 0x7fu; }
 };
 
+// ------------------------------------------------------------------------------------------
+// Record emission. The iterator's per-fragment state machine (wal_iterator.go:69-96: `off` is captured
+// while the accumulated record is empty; Full returns the Full's data with that offset; First/Middle
+// append; Last appends and returns the record; any other type is an error; a CRC mismatch is an error)
+// depends on the CRC verdicts only through the first failing fragment, after which nothing is emitted.
+// So every record is emitted from the header chase alone -- by the k_crc wave that owns its Full/Last
+// fragment, once that wave's CRC passes are done -- and the finalizer counts the records before the first
+// failing fragment. The state entering a wave comes from k_chase's block summaries (kSumHasE): the nearest
+// earlier block with a Full/Last fragment contributes its tail, the blocks after it their whole length.
+
+// byte `pos` of a register window (N dwords, pos < 4N): a select tree on the bits of the dword index
+template <int N>
+__device__ __forceinline__ uint32_t reg_byte(const uint32_t (&h)[N], uint32_t pos) {
+  uint32_t t[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) t[i] = h[i];
+  const uint32_t wi = pos >> 2;
+  int n = N;
+#pragma unroll
+  for (int bit = 0; bit < 6; ++bit) {
+    if (n <= 1) break;
+    const bool hi = (wi >> bit) & 1u;
+#pragma unroll
+    for (int i = 0; i < (N + 1) / 2; ++i) {
+      if (i < (n + 1) / 2) t[i] = (2 * i + 1 < n) ? (hi ? t[2 * i + 1] : t[2 * i]) : t[2 * i];
+    }
+    n = (n + 1) / 2;
+  }
+  return (t[0] >> (8u * (pos & 3u))) & 0xffu;
+}
+
+constexpr int kHeadWords = 20;  // 80 B aligned window: the record's first 64 B (and more) from any alignment
+constexpr int kTailWords = 12;  // 48 B aligned window: the record's last 32 B (hint mode: fid, offset, size)
+
+// logical byte reader of one record: its first bytes and (hint mode) its last bytes in registers, else a
+// walk over its fragments
+struct RegReader {
+  uint32_t h[kHeadWords];
+  uint32_t t[kTailWords];
+  uint32_t hsh, nhead;   // head: window shift, bytes of the record held
+  uint32_t tsh;          // tail: window shift of the byte at tstart
+  uint64_t tstart;       // first record byte held by the tail (>= size when none)
+  const uint8_t* seg;
+  const Frag* frags;
+  uint32_t start_off;
+  uint32_t f_first, f_last;
+  uint32_t cf;
+  uint64_t cbeg, clen, caddr;
+  __device__ __forceinline__ uint32_t operator()(uint64_t pos) {
+    if (pos < nhead) return reg_byte(h, hsh + (uint32_t)pos);
+    if (pos >= tstart) return reg_byte(t, tsh + (uint32_t)(pos - tstart));
+    if (pos < cbeg) {
+      cf = f_first;
+      cbeg = 0;
+      const Frag f = frags[cf];
+      clen = f.len;
+      caddr = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
+    }
+    while (pos >= cbeg + clen && cf < f_last) {
+      cbeg += clen;
+      ++cf;
+      const Frag f = frags[cf];
+      clen = f.len;
+      caddr = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
+    }
+    return seg[caddr + (pos - cbeg)];
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void load_words(const uint8_t* __restrict__ seg, uint64_t seg_len, uint64_t base,
+                                           uint32_t (&w)[N]) {
+  if (base + 4u * N <= seg_len) {
+#pragma unroll
+    for (int k = 0; k < N / 4; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4*>(seg + base + 16 * k);
+      w[4 * k + 0] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < N / 4; ++k) {
+      const uint4 v = load16_safe(seg, seg_len, (int64_t)(base + 16 * k));
+      w[4 * k + 0] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+  }
+}
+
+struct EmitArgs {
+  const uint8_t* seg;
+  uint64_t seg_len;
+  bcw_decode_params p;
+  const Frag* frags;
+  const uint32_t* fbase;
+  const uint32_t* rbase;
+  const uint2* bsum;
+  bcw_record_table tab;
+  uint64_t* misc;
+};
+
+// Emit the records completed by fragments [f0, f1) of blocks starting at b0 (one wave): rows of the record
+// table from rbase[b0] on, RecordFromBytes (record.go:140-239) / HintRecord.Decode (hint.go:50-84) per record,
+// one lane each.
+__device__ void emit_wave(const EmitArgs& A, uint64_t b0, uint64_t f0, uint64_t f1, uint32_t lane) {
+  if (f0 >= f1) return;
+  const Frag* __restrict__ frags = A.frags;
+  const uint32_t start_off = A.p.start_off;
+  // the state entering block b0: walk back over the block summaries, 64 blocks a step, to the nearest block
+  // with a Full/Last fragment (before block 0: an empty state)
+  uint64_t acc = 0, off = 0;
+  uint32_t first = 0;
+  {
+    int64_t nzb = -1;
+    uint32_t nzk = 0, nzs = 0;
+    for (uint64_t top = b0; top > 0;) {
+      const uint64_t q = top - 1 - lane;  // lane 0: the nearest block
+      const uint2 s = top > lane ? A.bsum[q] : make_uint2(0xffff0000u, kSumHasE);
+      const uint64_t he = __ballot((s.y & kSumHasE) != 0u);
+      const uint32_t stop = he ? (uint32_t)__builtin_ctzll(he) : 63u;
+      const bool contrib = lane <= stop;
+      uint32_t ta = contrib ? (s.x & 0xffffu) : 0u;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) ta += (uint32_t)__shfl_xor((int)ta, d, 64);
+      acc += ta;
+      const uint64_t nzm = __ballot(contrib && (s.x >> 16) != 0xffffu);
+      if (nzm) {  // the earliest block (highest lane) holding a non-empty fragment of the pending record
+        const uint32_t L = 63u - __builtin_clzll(nzm);
+        nzb = (int64_t)(top - 1 - L);
+        nzk = (uint32_t)__builtin_amdgcn_readlane((int)(s.x >> 16), L);
+        nzs = (uint32_t)__builtin_amdgcn_readlane((int)(s.y & 0xffffu), L);
+      }
+      if (he) break;
+      top = top > 64 ? top - 64 : 0;
+    }
+    if (nzb >= 0) {
+      off = (uint64_t)start_off + (uint64_t)nzb * kBlock + nzs;
+      first = A.fbase[nzb] + nzk;
+    }
+  }
+  uint64_t rec = A.rbase[b0];
+  const bool hint = A.p.mode == BCW_MODE_HINT;
+  for (uint64_t c0 = f0; c0 < f1; c0 += 64) {
+    const uint64_t g = c0 + lane;
+    const bool valid = g < f1;
+    Frag f{};
+    if (valid) f = frags[g];
+    const uint32_t len = valid ? f.len : 0u;
+    const uint64_t D = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
+    const bool isE = valid && (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST);
+    const uint64_t E = __ballot(isE);
+    const uint64_t NZ = __ballot(valid && len > 0);
+    const uint32_t S = wave_add_scan(len, lane);  // inclusive prefix of lengths
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t pm = E & below;
+    const int prev = pm ? 63 - __builtin_clzll(pm) : -1;
+    const uint32_t S_prev = __shfl(S, prev < 0 ? 0 : prev, 64);
+    const uint64_t between = (uint64_t)(S - len) - (prev < 0 ? 0u : S_prev);  // lengths in (prev, lane)
+    const uint64_t acc_before = (prev < 0 ? acc : 0ull) + between;
+    const uint64_t range = prev < 0 ? below : (below & ~(~0ull >> (63 - prev)));
+    const uint64_t nzr = NZ & range;
+    const int fnz = nzr ? __builtin_ctzll(nzr) : 0;
+    const uint64_t D_fnz = __shfl(D, fnz, 64);
+    // chunk carry-out (state after the last emission of the chunk, or the extended incoming state)
+    const uint64_t V = __ballot(valid);
+    const int last_valid = V ? 63 - __builtin_clzll(V) : -1;
+    const uint32_t S_tot = __shfl(S, last_valid < 0 ? 0 : last_valid, 64);
+    const int lastE = E ? 63 - __builtin_clzll(E) : -1;
+    uint64_t acc2, off2;
+    uint32_t first2;
+    {
+      const uint32_t S_lastE = __shfl(S, lastE < 0 ? 0 : lastE, 64);
+      const uint64_t after = lastE < 0 ? V : (V & ~(~0ull >> (63 - lastE)));
+      const uint64_t nza = NZ & after;
+      const int fa = nza ? __builtin_ctzll(nza) : 0;
+      const uint64_t D_fa = __shfl(D, fa, 64);
+      if (lastE >= 0) {
+        acc2 = (uint64_t)(S_tot - S_lastE);
+        off2 = D_fa;
+        first2 = (uint32_t)(c0 + fa);
+      } else {
+        acc2 = acc + S_tot;
+        if (acc > 0 || !nza) { off2 = off; first2 = first; }
+        else { off2 = D_fa; first2 = (uint32_t)(c0 + fa); }
+      }
+    }
+    // the record each emitting lane completes (evaluated by every lane: the shuffles need all lanes)
+    uint64_t foff;
+    uint32_t ffrag;
+    if (acc_before == 0) { foff = D; ffrag = (uint32_t)g; }
+    else if (prev < 0 && acc > 0) { foff = off; ffrag = first; }
+    else { foff = D_fnz; ffrag = (uint32_t)(c0 + fnz); }
+    const bool full = f.type == BCW_RECORD_FULL;
+    const uint32_t src = full ? (uint32_t)g : ffrag;  // the record's bytes start in fragment src
+    const bool src_here = src >= c0 && src < c0 + 64;
+    const uint32_t sw0 = (uint32_t)__shfl((int)f.blk, src_here ? (int)(src - c0) : (int)lane, 64);
+    const uint32_t sw1 = (uint32_t)__shfl((int)((uint32_t)f.start | ((uint32_t)f.len << 16)),
+                                          src_here ? (int)(src - c0) : (int)lane, 64);
+    if (isE) {
+      const uint64_t size = full ? (uint64_t)len : acc_before + len;
+      const uint64_t r = rec + __builtin_popcountll(E & below);
+      Frag fs = f;
+      if (!full) {
+        if (src_here) { fs.blk = sw0; fs.start = (uint16_t)sw1; fs.len = (uint16_t)(sw1 >> 16); }
+        else fs = frags[src];
+      }
+      RegReader rd;
+      const uint64_t a0 = (uint64_t)start_off + (uint64_t)fs.blk * kBlock + fs.start;
+      uint64_t want = size < 64u ? size : 64u;
+      if (want > fs.len) want = fs.len;
+      const uint64_t hb = a0 & ~15ull;
+      rd.hsh = (uint32_t)(a0 - hb);
+      rd.nhead = (uint32_t)want;
+      load_words(A.seg, A.seg_len, hb, rd.h);
+      rd.tstart = ~0ull;
+      rd.tsh = 0;
+      if (hint) {  // the last bytes: HintRecord.Decode reads fid, offset and size after the key
+        uint64_t nt = size < 32u ? size : 32u;
+        if (nt > len) nt = len;
+        const uint64_t te = D + len - nt;  // this lane's (Full/Last) fragment ends the record
+        const uint64_t tb = te & ~15ull;
+        rd.tsh = (uint32_t)(te - tb);
+        rd.tstart = size - nt;
+        load_words(A.seg, A.seg_len, tb, rd.t);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kTailWords; ++k) rd.t[k] = 0;
+      }
+      rd.seg = A.seg; rd.frags = frags; rd.start_off = start_off;
+      rd.f_first = src; rd.f_last = (uint32_t)g; rd.cf = src; rd.cbeg = 0; rd.clen = fs.len; rd.caddr = a0;
+      uint8_t status, hdr, flags, etag_off;
+      uint64_t key_len, val_len, meta_len, expire, aux0, aux1;
+      parse_record(A.p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
+      const bcw_record_table& tab = A.tab;
+      if (r < tab.capacity) {
+        tab.foff[r] = foff;
+        tab.size[r] = size;
+        tab.expire[r] = expire;
+        if (tab.aux0) tab.aux0[r] = aux0;
+        if (tab.aux1) tab.aux1[r] = aux1;
+        tab.key_len[r] = (uint32_t)key_len;
+        tab.val_len[r] = (uint32_t)val_len;
+        tab.meta_len[r] = (uint32_t)meta_len;
+        tab.first_frag[r] = src;
+        tab.emit_frag[r] = (uint32_t)g;
+        tab.hdr_size[r] = hdr;
+        tab.flags[r] = flags;
+        tab.etag_off[r] = etag_off;
+        tab.status[r] = status;
+      }
+      if (status != BCW_ST_OK) atomicMin((unsigned long long*)&A.misc[M_FIRST_BAD], (unsigned long long)r);
+    }
+    rec += __builtin_popcountll(E);
+    acc = acc2;
+    off = off2;
+    first = first2;
+  }
+}
+
+// The segment result, by one wave once every k_crc wave has verified and emitted: the first failing fragment
+// is the earlier of the first CRC mismatch and the first unknown type (at the same fragment the CRC is
+// checked first, wal_iterator.go:79-95), and the records before it are the Full/Last fragments before it.
+__device__ void finalize(const EmitArgs& A, uint64_t nblocks, uint64_t frag_cap, uint32_t tail_panic, uint64_t gen,
+                         bcw_decode_result* __restrict__ res, uint32_t lane) {
+  uint64_t* misc = A.misc;
+  const uint64_t bad_crc = __hip_atomic_load(&misc[M_BAD_CRC], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t bad_type = __hip_atomic_load(&misc[M_BAD_TYPE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t fb = __hip_atomic_load(&misc[M_FIRST_BAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t nfr = misc[M_NFRAGS];
+  const uint64_t err = bad_crc < bad_type ? bad_crc : bad_type;
+  // records before fragment `lim` (the first failing one, or the fragment capacity of a decode to be retried)
+  uint64_t lim = err < frag_cap ? err : frag_cap;
+  uint64_t nrec = misc[M_NE];
+  if (lim < nfr) {
+    // the block holding fragment lim: the last b with fbase[b] <= lim (64-ary search)
+    uint64_t lo = 0, hi = nblocks;
+    while (hi - lo > 1) {
+      const uint64_t step = (hi - lo + 63) / 64;
+      const uint64_t q = lo + (uint64_t)lane * step;
+      const bool le = q < hi && A.fbase[q] <= lim;
+      const uint64_t m = __ballot(le);
+      const uint32_t L = m ? 63u - __builtin_clzll(m) : 0u;
+      lo = lo + (uint64_t)L * step;
+      hi = lo + step < hi ? lo + step : hi;
+    }
+    uint64_t cnt = 0;
+    for (uint64_t c0 = A.fbase[lo]; c0 < lim; c0 += 64) {
+      const uint64_t g = c0 + lane;
+      const uint32_t ty = g < lim ? A.frags[g].type : 0u;
+      cnt += (uint64_t)__builtin_popcountll(__ballot(ty == BCW_RECORD_FULL || ty == BCW_RECORD_LAST));
+    }
+    nrec = (uint64_t)A.rbase[lo] + cnt;
+  }
+  if (lane != 0) return;
+  bcw_decode_result r{};
+  r.n_records = nrec;
+  r.n_records_total = nrec;
+  r.err_frag = err;
+  r.err_class = err == ~0ull ? BCW_ERR_NONE : (bad_crc <= bad_type ? BCW_ERR_CRC : BCW_ERR_TYPE);
+  r.n_frags = err != ~0ull ? err + 1 : nfr;
+  // a last block of 1..6 bytes makes the reference iterator panic after every earlier record
+  // (wal_iterator.go:62-76 re-slices a header from its stale buffer, then buf[7:7+negative])
+  if (r.err_class == BCW_ERR_NONE && tail_panic) r.err_class = BCW_ERR_PANIC;
+  r.err_file_off = 0;
+  if (err != ~0ull && err < frag_cap) {
+    const Frag f = A.frags[err];
+    r.err_file_off = (uint64_t)A.p.start_off + (uint64_t)f.blk * kBlock + f.start - kHdr;
+  }
+  r.first_bad_record = fb < nrec ? (int32_t)(fb < 0x7fffffffull ? fb : 0x7fffffffull) : -1;
+  r.n_blocks = nblocks;
+  r.retry_frag_capacity = nfr > frag_cap ? nfr : 0;
+  r.generation = gen;
+  *res = r;
+  misc[M_BAD_TYPE] = ~0ull;  // for the next decode's k_chase
+}
+
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
 // 4 no lane-operator / scan combine, 8 no record-state tail, 16 phase stamps, 128 no first-window mask, 256 no last-window fix,
-// 512 per-wave wall-clock stamps (entry, tables loaded, loop done) into lpre as u64[4] per wave, 1024 no
+// 512 per-wave wall-clock stamps (entry, tables loaded, loop done) into the expire column as u64[4] per wave, 1024 no
 // priority balancing
 template <int ABL = 0>
 __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                      uint32_t start_off, uint64_t nblocks,
                                                      const uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
-                                                     uint64_t frag_cap, Tables tabs, Xf* __restrict__ lpre,
-                                                     Xf* __restrict__ wpre, Xf* __restrict__ wgx,
+                                                     uint64_t frag_cap, Tables tabs, EmitArgs ea,
+                                                     uint32_t tail_panic, uint64_t gen,
+                                                     bcw_decode_result* __restrict__ res,
                                                      uint64_t* __restrict__ misc) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kCrcLds / 4];
   const uint64_t t_entry = (ABL & 512) ? wall_clock64() : 0;
@@ -719,7 +896,6 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   uint32_t* s_half = s_carry + 128;
   uint32_t* s_wave_all = s_carry + kLdsOps;
   const uint32_t tid = threadIdx.x;
-  __shared__ Xf s_wagg[kCrcWaves];  // wave aggregates of this workgroup
   __shared__ uint32_t s_wdone;      // waves of this workgroup done
   __shared__ uint32_t s_rem[kCrcWaves];  // windows each wave has left (balance)
   if (tid == 0) s_wdone = 0;
@@ -922,7 +1098,10 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
         w[4 * g + 0] = q.x; w[4 * g + 1] = q.y; w[4 * g + 2] = q.z; w[4 * g + 3] = q.w;
       }
     }
-    if (d.active() && d.last()) frags[f0 + d.fi].ok = (U == 0u) ? 1 : 0;
+    if (d.active() && d.last()) {
+      frags[f0 + d.fi].ok = (U == 0u) ? 1 : 0;
+      if (U != 0u) atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_CRC]), (unsigned long long)(f0 + d.fi));
+    }
     carry = __builtin_amdgcn_readlane(U, 63);
   };
 
@@ -993,315 +1172,29 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
 
   __builtin_amdgcn_s_setprio(0);
   if ((ABL & 512) && lane == 0) {
-    uint64_t* q = reinterpret_cast<uint64_t*>(lpre) + 4 * gw;
+    uint64_t* q = ea.tab.expire + 4 * gw;  // kbench only (the table is overwritten by the emission unless ABL & 8)
     q[0] = t_entry; q[1] = t_tables; q[2] = wall_clock64(); q[3] = nfr;
   }
-  if (ABL & 8) return;
-  // ---- record-state transforms of this wave's blocks (the verdicts were written by its lanes) ----
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const Xf wx_agg = wave_block_xf(frags, f0, f1, b0, b1, start_off, lane, lpre);
-
-  // ---- the last wave of the workgroup scans the 16 wave aggregates ----
-  if (lane == 0) s_wagg[wave] = wx_agg;
+  // ---- the records this wave's Full/Last fragments complete (no CRC verdict needed, see emit_wave) ----
+  if (!(ABL & 8)) emit_wave(ea, b0, f0, f1, lane);
+  // ---- completion: each wave's stores and atomics are done (vmcnt(0)) before it counts itself done in LDS;
+  // the last wave of a workgroup adds the workgroup to the agent-scope counter, and the last workgroup's
+  // last wave writes the segment result from the agent-scope minima (MI355X_MICROARCH.md, inter-workgroup
+  // visibility, row 1) ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   uint32_t order = 0;
   if (lane == 0) order = atomicAdd(&s_wdone, 1u);
   order = __builtin_amdgcn_readlane(order, 0);
   if (order != kCrcWaves - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  {
-    const Xf x = lane < (uint32_t)kCrcWaves ? s_wagg[lane] : xf_identity();
-    const Xf incl = wave_xf_scan(x, lane, kCrcWaves);
-    const Xf prev = xf_shfl(incl, lane > 0 ? (int)lane - 1 : 0);
-    if (lane < (uint32_t)kCrcWaves) wpre[(uint64_t)blockIdx.x * kCrcWaves + lane] = lane > 0 ? prev : xf_identity();
-    if (lane == (uint32_t)kCrcWaves - 1) xf_store_agent(&wgx[blockIdx.x], incl);
-  }
-  // ---- the last workgroup scans the workgroup aggregates ----
-  // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, row 1): the aggregate is stored with `sc1`
-  // (write-through) 8-byte stores by lane kCrcWaves-1, which waits for them (vmcnt(0)) before its
-  // agent-scope add to the one completion counter; the workgroup whose add returns last reads every
-  // aggregate with `sc1` loads (xf_load_agent). Without the wait the add can overtake a store.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   uint64_t gorder = 0;
-  if (lane == (uint32_t)kCrcWaves - 1)
+  if (lane == 0)
     gorder = __hip_atomic_fetch_add(&misc[M_DONE_CRC], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  gorder = (uint64_t)__shfl((long long)gorder, kCrcWaves - 1, 64);
+  gorder = (uint64_t)__shfl((long long)gorder, 0, 64);
   if (gorder != gridDim.x - 1u) return;
-  if (lane == 0) misc[M_T_SCAN0] = wall_clock64();
-  scan_wg_aggregates(wgx, gridDim.x, misc, lane);
-  if (lane == 0) misc[M_T_SCAN1] = wall_clock64();
-}
-
-// ------------------------------------------------------------------------------------------
-// k_records: record emission (one wave per run of blocks, fragments in chunks of 64 lanes) and
-// RecordFromBytes (record.go:140-239) / HintRecord.Decode (hint.go:50-84) per record, one lane each.
-
-constexpr int kRecWaves = 4;
-constexpr uint32_t kStage = 128;      // staged record-prefix bytes per lane
-constexpr uint32_t kStageArea = 144;  // 9 x 16 B aligned loads
-
-// logical byte reader of one record: staged prefix in LDS, then a walk over its fragments
-struct RecReader {
-  const uint8_t* seg;
-  const Frag* frags;
-  uint32_t start_off;
-  const uint8_t* stage;
-  uint32_t nstaged;
-  uint32_t f_first, f_last;
-  uint32_t cf;
-  uint64_t cbeg, clen, caddr;
-  __device__ __forceinline__ uint32_t operator()(uint64_t pos) {
-    if (pos < nstaged) return stage[pos];
-    if (pos < cbeg) {
-      cf = f_first;
-      cbeg = 0;
-      const Frag f = frags[cf];
-      clen = f.len;
-      caddr = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
-    }
-    while (pos >= cbeg + clen && cf < f_last) {
-      cbeg += clen;
-      ++cf;
-      const Frag f = frags[cf];
-      clen = f.len;
-      caddr = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
-    }
-    return seg[caddr + (pos - cbeg)];
-  }
-};
-
-__device__ __forceinline__ void finalize(uint64_t* __restrict__ misc, uint64_t nblocks, uint64_t frag_total,
-                           uint64_t frag_cap, const Frag* __restrict__ frags, uint32_t start_off, uint32_t tail_panic,
-                           uint64_t gen, bcw_decode_result* __restrict__ res) {
-  bcw_decode_result r{};
-  r.n_records = misc[M_NREC];
-  r.n_records_total = misc[M_NREC];
-  r.err_frag = misc[M_ERR_FRAG];
-  r.err_class = (int32_t)misc[M_ERR_CLASS];
-  r.n_frags = r.err_frag != ~0ull ? r.err_frag + 1 : frag_total;
-  // a last block of 1..6 bytes makes the reference iterator panic after every earlier record
-  // (wal_iterator.go:62-76 re-slices a header from its stale buffer, then buf[7:7+negative])
-  if (r.err_class == BCW_ERR_NONE && tail_panic) r.err_class = BCW_ERR_PANIC;
-  r.err_file_off = 0;
-  if (r.err_frag != ~0ull && r.err_frag < frag_cap) {
-    const Frag f = frags[r.err_frag];
-    r.err_file_off = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start - kHdr;
-  }
-  const uint64_t fb = __hip_atomic_fetch_or(&misc[M_FIRST_BAD], 0ull, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-  r.first_bad_record = fb == ~0ull ? -1 : (int32_t)(fb < 0x7fffffffull ? fb : 0x7fffffffull);
-  r.n_blocks = nblocks;
-  r.retry_frag_capacity = frag_total > frag_cap ? frag_total : 0;
-  r.generation = gen;
-  *res = r;
-}
-
-// ABL: ablation bits for tools/kbench only (0 in the product): 1 no parse, 2 no prefix staging loads,
-// 4 no table stores, 8 no finalize
-template <int ABL = 0>
-__global__ __launch_bounds__(256) void k_records(const uint8_t* __restrict__ seg, uint64_t seg_len,
-                                                 bcw_decode_params p, const Frag* __restrict__ frags,
-                                                 const uint32_t* __restrict__ fbase, uint64_t nblocks,
-                                                 uint64_t frag_cap, const Xf* __restrict__ lpre,
-                                                 const Xf* __restrict__ wpre, const Xf* __restrict__ wgx, uint64_t nw,
-                                                 bcw_record_table tab,
-                                                 uint64_t* __restrict__ misc, uint32_t tail_panic, uint64_t gen,
-                                                 bcw_decode_result* __restrict__ res) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[kRecWaves][64][kStageArea];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = threadIdx.x >> 6;
-  // work item = a run of consecutive blocks holding about 64 fragments (one chunk); waves stride
-  // over the items (persistent grid)
-  uint64_t nf = misc[M_NFRAGS];
-  if (nf > frag_cap) nf = frag_cap;
-  uint64_t bpw = nf ? (64 * nblocks) / nf : nblocks;
-  if (bpw < 1) bpw = 1;
-  const uint64_t nitems = (nblocks + bpw - 1) / bpw;
-  // an item's incoming state (the prefix of the k_crc wave holding its first block b, then that wave's blocks
-  // before b) and fragment range, loaded one item ahead: the next item's loads are in flight while this one
-  // emits (an unconditional load at a clamped item, so no branch merges them into a wait)
-  struct ItemIn {
-    Xf w, p, l;
-    uint32_t g0, g1;
-  };
-  const uint64_t stride = (uint64_t)gridDim.x * kRecWaves;
-  auto fetch_item = [&](uint64_t it) {
-    ItemIn r;
-    const uint64_t bi = (it < nitems ? it : nitems - 1) * bpw;
-    const uint64_t bb = bi < nblocks ? bi : nblocks - 1;
-    const uint64_t be = bb + bpw < nblocks ? bb + bpw : nblocks;
-    const uint64_t gwi = ((bb + 1) * nw - 1) / nblocks;
-    r.w = wgx[gwi / kCrcWaves];
-    r.p = wpre[gwi];
-    r.l = lpre[bb];
-    r.g0 = fbase[bb];
-    r.g1 = fbase[be];
-    return r;
-  };
-  // the first fragment chunk of an item, loaded with the item one item ahead (fbase -> frags is a dependent pair,
-  // so it trails the item's own loads by one round trip but is in flight during the current item's emission)
-  auto fetch_chunk = [&](uint32_t g0) -> uint4 {
-    const uint64_t g = (uint64_t)g0 + lane;
-    return reinterpret_cast<const uint4*>(frags)[g < frag_cap ? g : frag_cap - 1];
-  };
-  // the first failing fragment (written by k_crc's final scan): nothing at or after it is emitted
-  const uint64_t err_frag = misc[M_ERR_FRAG];
-  ItemIn nxt_in = fetch_item((uint64_t)blockIdx.x * kRecWaves + wave);
-  uint4 nxt_chunk = fetch_chunk(nxt_in.g0);
-  for (uint64_t item = (uint64_t)blockIdx.x * kRecWaves + wave; item < nitems; item += stride) {
-  const uint64_t b = item * bpw;
-  const ItemIn cur_in = nxt_in;
-  const uint4 cur_chunk = nxt_chunk;
-  nxt_in = fetch_item(item + stride);
-  nxt_chunk = fetch_chunk(nxt_in.g0);
-  do {  // this item's record emission
-  if (b >= nblocks) break;
-  const Xf in = xf_compose(xf_compose(cur_in.w, cur_in.p), cur_in.l);
-  if (in.err) break;
-  uint64_t acc = in.a, off = in.off;
-  uint32_t first = in.first;
-  uint64_t rec = in.n_emit;
-  uint64_t g0 = cur_in.g0, g1 = cur_in.g1;
-  if (g1 > frag_cap) g1 = frag_cap;
-  if (g1 > err_frag) g1 = err_frag;  // nothing at or after the first failing fragment is emitted
-  uint8_t* st = s_stage[wave][lane];
-  for (uint64_t c0 = g0; c0 < g1; c0 += 64) {
-    const uint64_t g = c0 + lane;
-    const bool valid = g < g1;
-    Frag f{};
-    if (c0 == g0) __builtin_memcpy(&f, &cur_chunk, sizeof f);  // prefetched with the item
-    else if (valid) f = frags[g];
-    if (!valid) f = Frag{};
-    const uint32_t len = valid ? f.len : 0u;
-    const uint64_t D = (uint64_t)p.start_off + (uint64_t)f.blk * kBlock + f.start;
-    const bool isE = valid && (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST);
-    const uint64_t E = __ballot(isE);
-    const uint64_t NZ = __ballot(valid && len > 0);
-    const uint32_t S = wave_incl_scan_u32(len, lane);  // inclusive prefix of lengths
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const uint64_t pm = E & below;
-    const int prev = pm ? 63 - __builtin_clzll(pm) : -1;
-    const uint32_t S_prev = __shfl(S, prev < 0 ? 0 : prev, 64);
-    const uint64_t between = (uint64_t)(S - len) - (prev < 0 ? 0u : S_prev);  // lengths in (prev, lane)
-    const uint64_t acc_before = (prev < 0 ? acc : 0ull) + between;
-    const uint64_t range = prev < 0 ? below : (below & ~(~0ull >> (63 - prev)));
-    const uint64_t nzr = NZ & range;
-    const int fnz = nzr ? __builtin_ctzll(nzr) : 0;
-    const uint64_t D_fnz = __shfl(D, fnz, 64);
-    // chunk carry-out (state after the last emission of the chunk, or extended incoming state)
-    const uint64_t V = __ballot(valid);
-    const int last_valid = V ? 63 - __builtin_clzll(V) : -1;
-    const uint32_t S_tot = __shfl(S, last_valid < 0 ? 0 : last_valid, 64);
-    const int lastE = E ? 63 - __builtin_clzll(E) : -1;
-    uint64_t acc2, off2;
-    uint32_t first2;
-    {
-      const uint32_t S_lastE = __shfl(S, lastE < 0 ? 0 : lastE, 64);
-      const uint64_t after = lastE < 0 ? V : (V & ~(~0ull >> (63 - lastE)));
-      const uint64_t nza = NZ & after;
-      const int fa = nza ? __builtin_ctzll(nza) : 0;
-      const uint64_t D_fa = __shfl(D, fa, 64);
-      if (lastE >= 0) {
-        acc2 = (uint64_t)(S_tot - S_lastE);
-        off2 = D_fa;
-        first2 = (uint32_t)(c0 + fa);
-      } else {
-        acc2 = acc + S_tot;
-        if (acc > 0 || !nza) { off2 = off; first2 = first; }
-        else { off2 = D_fa; first2 = (uint32_t)(c0 + fa); }
-      }
-    }
-    // the record each emitting lane completes (evaluated by every lane: the shuffle below needs all lanes)
-    uint64_t foff;
-    uint32_t ffrag;
-    if (acc_before == 0) { foff = D; ffrag = (uint32_t)g; }
-    else if (prev < 0 && acc > 0) { foff = off; ffrag = first; }
-    else { foff = D_fnz; ffrag = (uint32_t)(c0 + fnz); }
-    const bool full = f.type == BCW_RECORD_FULL;
-    const uint32_t src = full ? (uint32_t)g : ffrag;  // the record's bytes start in fragment src
-    // its first fragment: this lane's (Full), another lane's of this chunk (shuffled), else loaded below
-    const bool src_here = src >= c0 && src < c0 + 64;
-    const uint32_t sw0 = (uint32_t)__shfl((int)f.blk, src_here ? (int)(src - c0) : (int)lane, 64);
-    const uint32_t sw1 = (uint32_t)__shfl((int)((uint32_t)f.start | ((uint32_t)f.len << 16)),
-                                          src_here ? (int)(src - c0) : (int)lane, 64);
-    if (isE) {
-      const uint64_t size = full ? (uint64_t)len : acc_before + len;
-      const uint64_t r = rec + __builtin_popcountll(E & below);
-      Frag f0 = f;
-      if (!full) {
-        if (src_here) { f0.blk = sw0; f0.start = (uint16_t)sw1; f0.len = (uint16_t)(sw1 >> 16); }
-        else f0 = frags[src];
-      }
-      // stage the record prefix (when its first fragment holds it) with aligned 16 B loads
-      const uint64_t a0 = (uint64_t)p.start_off + (uint64_t)f0.blk * kBlock + f0.start;
-      uint64_t want = size < kStage ? size : kStage;
-      if (want > f0.len) want = f0.len;
-      const uint64_t base = a0 & ~15ull;
-      const uint32_t sh = (uint32_t)(a0 - base);
-      const uint32_t nld = (uint32_t)((sh + want + 15) >> 4);
-      if (!(ABL & 2)) {
-        // all of the record's prefix loads in flight at once (a rolled load -> LDS store loop would pay one
-        // memory round trip per 16 B); bounds-checked loads only where the prefix touches the segment end
-        uint4 v[kStageArea / 16];
-        if (base + 16ull * nld <= seg_len) {
-#pragma unroll
-          for (uint32_t k = 0; k < kStageArea / 16; ++k)
-            if (k < nld) v[k] = *reinterpret_cast<const uint4*>(seg + base + 16 * k);
-        } else {
-#pragma unroll
-          for (uint32_t k = 0; k < kStageArea / 16; ++k)
-            if (k < nld) v[k] = load16_safe(seg, seg_len, (int64_t)(base + 16 * k));
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kStageArea / 16; ++k)
-          if (k < nld) *reinterpret_cast<uint4*>(st + 16 * k) = v[k];
-      }
-      RecReader rd{seg, frags, p.start_off, st + sh, (uint32_t)want, src, (uint32_t)g, src, 0, f0.len, a0};
-      uint8_t status, hdr, flags, etag_off;
-      uint64_t key_len, val_len, meta_len, expire, aux0, aux1;
-      if (!(ABL & 1)) {
-        parse_record(p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
-      } else {
-        status = hdr = flags = etag_off = 0;
-        key_len = val_len = meta_len = expire = aux0 = aux1 = 0;
-      }
-      if (!(ABL & 4) && r < tab.capacity) {
-        tab.foff[r] = foff;
-        tab.size[r] = size;
-        tab.expire[r] = expire;
-        if (tab.aux0) tab.aux0[r] = aux0;
-        if (tab.aux1) tab.aux1[r] = aux1;
-        tab.key_len[r] = (uint32_t)key_len;
-        tab.val_len[r] = (uint32_t)val_len;
-        tab.meta_len[r] = (uint32_t)meta_len;
-        tab.first_frag[r] = src;
-        tab.emit_frag[r] = (uint32_t)g;
-        tab.hdr_size[r] = hdr;
-        tab.flags[r] = flags;
-        tab.etag_off[r] = etag_off;
-        tab.status[r] = status;
-      }
-      if (status != BCW_ST_OK) atomicMin((unsigned long long*)&misc[M_FIRST_BAD], (unsigned long long)r);
-    }
-    rec += __builtin_popcountll(E);
-    acc = acc2;
-    off = off2;
-    first = first2;
-    wave_sync();
-  }
-  } while (0);
-  }
-  // The last workgroup to finish writes the segment result. The finalizer reads M_FIRST_BAD, which any
-  // wave may have lowered with a no-return atomicMin: every wave waits for its own atomics to complete
-  // (vmcnt(0)) before the workgroup barrier, and only then does one lane count the workgroup done; the
-  // finalizer reads the value with an atomic (performed where the atomicMins were).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t done = __hip_atomic_fetch_add(&misc[M_DONE_REC], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!(ABL & 8) && done == gridDim.x - 1u) finalize(misc, nblocks, misc[M_NFRAGS], frag_cap, frags, p.start_off, tail_panic, gen, res);
-  }
+  if (lane == 0) misc[M_T_FIN] = wall_clock64();
+  finalize(ea, nblocks, frag_cap, tail_panic, gen, res, lane);
 }
 
 __global__ void k_export_frags(const Frag* __restrict__ frags, const uint64_t* __restrict__ misc, uint64_t cap,
@@ -1329,30 +1222,23 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   hipEvent_t ev = nullptr;
   const uint32_t nb_grid = (uint32_t)((nblocks + 63) / 64);
   pr.begin(K_CHASE, stream, ev);
-  k_chase<<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags, s.frag_cap, s.lb,
-                                       s.misc, s.tickets, s.epoch, tabs.initc, s.chase_direct);
+  k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
+                                       s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch, tabs.initc,
+                                       s.chase_direct);
   pr.end(K_CHASE, stream, ev);
   s.tickets += nb_grid;
   if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse
     (void)hipMemsetAsync(s.lb, 0, s.nlb * sizeof(uint64_t), stream);
+    (void)hipMemsetAsync(s.lbe, 0, s.nlb * sizeof(uint64_t), stream);
     s.epoch = 1;
   }
-  pr.begin(K_CRC, stream, ev);
-  const uint64_t nw = (uint64_t)num_cus * kCrcWaves;
-  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
-                                                         s.frag_cap, tabs, s.pre, s.wgagg, s.wgx, s.misc);
-  pr.end(K_CRC, stream, ev);
   const uint64_t tail = (p.seg_len - p.start_off) % kBlock;
   const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;
-  pr.begin(K_RECORDS, stream, ev);
-  // 2 workgroups of 4 waves per CU take the work items (runs of blocks holding ~64 fragments); measured
-  // with tools/kbench: 4 per CU (every resident wave one item) 14 % slower, 8 per CU 50 % slower
-  uint64_t rec_wgs = (nblocks + kRecWaves - 1) / kRecWaves;
-  if (rec_wgs > (uint64_t)num_cus * 2) rec_wgs = (uint64_t)num_cus * 2;
-  k_records<0><<<(uint32_t)rec_wgs, 64 * kRecWaves, 0, stream>>>(
-      d_seg, p.seg_len, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg, s.wgx, nw, t, s.misc, tail_panic,
-      gen, d_result);
-  pr.end(K_RECORDS, stream, ev);
+  const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc};
+  pr.begin(K_CRC, stream, ev);
+  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
+                                                         s.frag_cap, tabs, ea, tail_panic, gen, d_result, s.misc);
+  pr.end(K_CRC, stream, ev);
   return hipGetLastError();
 }
 

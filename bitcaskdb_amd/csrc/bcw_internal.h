@@ -26,19 +26,6 @@ struct Frag {
 };
 static_assert(sizeof(Frag) == 16, "Frag layout");
 
-// Record-state transform of a range of blocks: the composition of the iterator's per-fragment
-// state machine (wal_iterator.go:69-96). See bcw_decode.hip "Record assembly".
-struct Xf {
-  uint64_t n_emit;
-  uint64_t a;      // has_emit: state after the last emission (acc)   else: sum of lengths
-  uint64_t off;    //           ... its offset                         else: first non-empty offset
-  uint32_t first;  //           ... its first fragment                 else: first non-empty fragment
-  uint32_t err_frag;
-  uint8_t has_emit, nz, err, err_class;
-  uint32_t pad;
-};
-static_assert(sizeof(Xf) == 40, "Xf layout");
-
 // shift operators A_{8 * 2^k} for k < kPow2Ops: any shift below 2^16 bytes (a fragment's u16 length)
 constexpr int kPow2Ops = 16;
 
@@ -74,15 +61,14 @@ struct Scratch {
   uint64_t nblocks_cap = 0;
   uint64_t frag_cap = 0;
   uint32_t* fbase = nullptr;   // [nblocks+1] global index of each block's first fragment
-  uint64_t* lb = nullptr;      // [nblocks/256+1] k_chase look-back words (zeroed at allocation)
+  uint32_t* rbase = nullptr;   // [nblocks+1] Full/Last fragments before each block (its first record row)
+  uint2* bsum = nullptr;       // [nblocks] record-state summary of each block (bcw_decode.hip, kSumHasE)
+  uint64_t* lb = nullptr;      // [nblocks/64+2] k_chase look-back words (zeroed at allocation)
+  uint64_t* lbe = nullptr;     // [nblocks/64+2] k_chase look-back words of the Full/Last counts (> kDirect groups)
   uint64_t nlb = 0;
   uint64_t tickets = 0;        // k_chase tickets issued so far (misc[M_TICKET] mirrors it)
   uint64_t epoch = 1;          // look-back epoch of the next launch
   Frag* frags = nullptr;       // [frag_cap]
-  Xf* pre = nullptr;           // [nblocks] record-state prefix of each block within its k_crc wave
-  Xf* wgagg = nullptr;         // [k_crc waves] wave-exclusive prefix within the k_crc workgroup
-  Xf* wgx = nullptr;           // [k_crc workgroups] workgroup aggregates -> exclusive prefixes
-  uint64_t nwave_cap = 0;
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
 };

@@ -265,13 +265,14 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, a, b));
       uint64_t mc[16];
       CK(hipMemcpy(mc, s.misc, sizeof mc, hipMemcpyDeviceToHost));
-      printf("timeline: pipeline %.1f us; k_crc WG0 start -> final scan start %.1f us, final scan %.1f us\n", ms * 1e3,
-             (mc[M_T_SCAN0] - mc[M_T_CRC0]) / 100.0, (mc[M_T_SCAN1] - mc[M_T_SCAN0]) / 100.0);
+      printf("timeline: pipeline %.1f us; k_crc WG0 start -> finalize %.1f us\n", ms * 1e3,
+             (mc[M_T_FIN] - mc[M_T_CRC0]) / 100.0);
     }
   }
   const uint64_t nblocks = (n - 40 + kBlock - 1) / kBlock;
+  const EmitArgs ea{d, n, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc};
   auto run = [&](auto kern, int grid) {
-    return timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, s.pre, s.wgagg, s.wgx, s.misc); },
+    return timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres, s.misc); },
                   reps, st);
   };
   const int cus = ctx->num_cus;
@@ -350,29 +351,29 @@ int main(int argc, char** argv) {
   if (argc > 3) {  // counter-collection mode: only the product k_crc, a few launches
     const int k = atoi(argv[3]);
     const int v = argc > 4 ? atoi(argv[4]) : 0;  // ablation variant
-    float t = 0;
+    float tm = 0;
     for (int i = 0; i < k; ++i) {
       switch (v) {
-        case 1: t = run(k_crc<1>, cus); break;
-        case 2: t = run(k_crc<2>, cus); break;
-        case 4: t = run(k_crc<4>, cus); break;
-        case 8: t = run(k_crc<8>, cus); break;
-        case 128: t = run(k_crc<128>, cus); break;
-        case 256: t = run(k_crc<256>, cus); break;
-        case 384: t = run(k_crc<384>, cus); break;
-        case 7: t = run(k_crc<7>, cus); break;
-        case 520: t = run(k_crc<520>, cus); break;
-        case 1544: t = run(k_crc<1544>, cus); break;
-        case 1024: t = run(k_crc<1024>, cus); break;
-        default: t = run(k_crc<0>, cus);
+        case 1: tm = run(k_crc<1>, cus); break;
+        case 2: tm = run(k_crc<2>, cus); break;
+        case 4: tm = run(k_crc<4>, cus); break;
+        case 8: tm = run(k_crc<8>, cus); break;
+        case 128: tm = run(k_crc<128>, cus); break;
+        case 256: tm = run(k_crc<256>, cus); break;
+        case 384: tm = run(k_crc<384>, cus); break;
+        case 7: tm = run(k_crc<7>, cus); break;
+        case 520: tm = run(k_crc<520>, cus); break;
+        case 1544: tm = run(k_crc<1544>, cus); break;
+        case 1024: tm = run(k_crc<1024>, cus); break;
+        default: tm = run(k_crc<0>, cus);
       }
     }
     CK(hipStreamSynchronize(st));
-    printf("k_crc<%d> x%d done, %.4f ms\n", v, k, t);
+    printf("k_crc<%d> x%d done, %.4f ms\n", v, k, tm);
     if (v == 520 || v == 1544) {  // per-wave stamps of the last launch: start / tables / loop end, by XCD (blockIdx % 8)
       const int nw = cus * kCrcWaves;
       std::vector<uint64_t> q(4 * (size_t)nw);
-      CK(hipMemcpy(q.data(), s.pre, q.size() * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(q.data(), t.expire, q.size() * 8, hipMemcpyDeviceToHost));
       uint64_t t0 = ~0ull, tmax = 0;
       for (int w = 0; w < nw; ++w) { t0 = std::min(t0, q[4 * w]); tmax = std::max(tmax, q[4 * w + 2]); }
       std::vector<double> ends(nw);
@@ -422,13 +423,13 @@ int main(int argc, char** argv) {
   printf("k_crc no-comb   %.4f ms\n", a4);
   printf("k_crc loads+comb only (no chain, no loads) %.4f ms\n", a3);
   printf("k_crc skeleton (1|2|4) %.4f ms\n", a7);
-  printf("k_crc no tail   %.4f ms\n", a8);
+  printf("k_crc no emission %.4f ms\n", a8);
   const float as = timeit([&] {
-    hipMemsetAsync(&s.misc[5], 0, 8, st);  // M_DONE_CRC: the last workgroup runs the aggregate scan
-    k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, s.pre, s.wgagg,
-                                          s.wgx, s.misc);
+    hipMemsetAsync(&s.misc[M_DONE_CRC], 0, 8, st);  // the last workgroup finalizes
+    k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
+                                          s.misc);
   }, reps, st);
-  printf("k_crc + scan    %.4f ms\n", as);
+  printf("k_crc + finalize %.4f ms\n", as);
   {
     CK(hipMemset(&s.misc[7], 0, 24));
     run(k_crc<16 | 8>, cus);
@@ -439,38 +440,31 @@ int main(int argc, char** argv) {
            m[2] / w);
   }
   {
+    CK(bcw_decode_segment_async(ctx, d, &p, &t, dres));
+    CK(hipStreamSynchronize(st));
     uint64_t m[16];
     CK(hipMemcpy(m, s.misc, sizeof m, hipMemcpyDeviceToHost));
     int hz = 0;
     CK(hipDeviceGetAttribute(&hz, hipDeviceAttributeWallClockRate, 0));  // kHz
-    printf("  stamps: first WG start -> scan start %.1f us, scan %.1f us (wall clock %d kHz)\n",
-           (m[11] - m[10]) * 1e3 / hz, (m[12] - m[11]) * 1e3 / hz, hz);
-  }
-  {  // k_records ablations (after a full pipeline run: its inputs are in place)
-    CK(bcw_decode_segment_async(ctx, d, &p, &t, dres));
-    CK(hipStreamSynchronize(st));
-    const uint64_t nw = (uint64_t)cus * kCrcWaves;
-    auto rrun = [&](auto kern, uint64_t wgs) {
+    printf("  stamps: first WG start -> finalize %.1f us (wall clock %d kHz)\n", (m[M_T_FIN] - m[M_T_CRC0]) * 1e3 / hz, hz);
+    auto crun = [&](auto kern) {
       return timeit([&] {
-        hipMemsetAsync(&s.misc[M_DONE_REC], 0, 8, st);  // so the last workgroup finalizes every launch
-        kern<<<(uint32_t)wgs, 64 * kRecWaves, 0, st>>>(d, n, p, s.frags, s.fbase, nblocks, s.frag_cap, s.pre, s.wgagg,
-                                                       s.wgx, nw, t, s.misc, 0u, 0ull, dres);
+        kern<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
+                                                              s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch,
+                                                              ctx->tabs.initc, s.chase_direct);
+        s.tickets += (nblocks + 63) / 64;
+        ++s.epoch;
       }, reps, st);
     };
-    const uint64_t g4 = (uint64_t)cus * 4, g2 = (uint64_t)cus * 2, g8 = (uint64_t)cus * 8;
-    printf("k_records: full %.4f  grid 2/CU %.4f  grid 8/CU %.4f | no parse %.4f  no staging %.4f  no stores %.4f  "
-           "no finalize %.4f  skeleton(1|2|4|8) %.4f ms\n",
-           rrun(k_records<0>, g4), rrun(k_records<0>, g2), rrun(k_records<0>, g8), rrun(k_records<1>, g4),
-           rrun(k_records<2>, g4), rrun(k_records<4>, g4), rrun(k_records<8>, g4), rrun(k_records<15>, g4));
-    const float ck = timeit([&] {
-      k_chase<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, s.lb,
-                                                               s.misc, s.tickets, s.epoch, ctx->tabs.initc, s.chase_direct);
-      s.tickets += (nblocks + 63) / 64;
-      ++s.epoch;
-    }, reps, st);
-    printf("k_chase alone %.4f ms\n", ck);
-    const float ms0 = timeit([&] { hipMemsetAsync(&s.misc[M_DONE_REC], 0, 8, st); }, reps, st);
-    printf("(k_records rows include an 8-byte memset: %.4f ms alone)\n", ms0);
+    printf("k_chase alone %.4f  no sum %.4f  no writes %.4f  chase only %.4f ms\n", crun(k_chase<0>), crun(k_chase<1>),
+           crun(k_chase<2>), crun(k_chase<3>));
+    CK(hipMemset(&s.misc[7], 0, 24));
+    crun(k_chase<16>);
+    uint64_t m3[3];
+    CK(hipMemcpy(m3, &s.misc[7], 24, hipMemcpyDeviceToHost));
+    const double wl = (double)((nblocks + 63) / 64) * (reps + 1);
+    printf("  k_chase phase cycles per workgroup (s_memtime): chase %.0f  sum %.0f  writes %.0f\n", m3[0] / wl,
+           m3[1] / wl, m3[2] / wl);
   }
   // verify still OK after variants (re-run the real pipeline)
   CK(bcw_decode_segment_async(ctx, d, &p, &t, dres));
