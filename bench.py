@@ -118,6 +118,20 @@ def cpu_pread_config_a(O, L, seconds):
     return int(n.value) * passes / 2 ** 30 / dt, passes, dt, int(n.value)
 
 
+def _fs_of(path: str) -> str:
+    """filesystem type and device of the mount holding `path` (/proc/mounts: the longest matching mount point)"""
+    best, out = "", "unknown"
+    try:
+        with open("/proc/mounts") as fh:
+            for ln in fh:
+                dev, mnt, fs = ln.split()[:3]
+                if path.startswith(mnt) and len(mnt) > len(best):
+                    best, out = mnt, f"{fs} ({dev} on {mnt})"
+    except OSError:
+        pass
+    return out
+
+
 def end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec, reps=3):
     """file -> pinned slices -> HBM -> decode, and file -> decode -> re-encode (all kept) -> dst WAL + hint
     files, through bcw_stage (f3); the files sit in the page cache (written just before)"""
@@ -147,6 +161,37 @@ def end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec, 
                 step()
                 torch.cuda.synchronize()
             res["decode_file_GiBs"] = round(seg_len / 2 ** 30 / ((time.perf_counter() - t) / reps), 2)
+            # from the storage device: the file's pages written back and dropped from the page cache before every
+            # read (posix_fadvise DONTNEED), and through an O_DIRECT descriptor (no page cache at all)
+            os.fsync(fd)
+            t_cold = 0.0
+            for _ in range(reps):
+                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                st.read(fd, 0, seg_len, d_seg.data_ptr(), stream.cuda_stream, threads=8)
+                step()
+                torch.cuda.synchronize()
+                t_cold += time.perf_counter() - t
+            res["decode_file_cold_GiBs"] = round(seg_len / 2 ** 30 / (t_cold / reps), 2)
+            try:
+                dfd = os.open(src, os.O_RDONLY | os.O_DIRECT)
+            except OSError as e:
+                res["decode_file_odirect_GiBs"] = f"O_DIRECT open refused: {e.strerror}"
+            else:
+                try:
+                    torch.cuda.synchronize()
+                    t = time.perf_counter()
+                    for _ in range(reps):
+                        st.read(dfd, 0, seg_len, d_seg.data_ptr(), stream.cuda_stream, threads=8)
+                        step()
+                        torch.cuda.synchronize()
+                    res["decode_file_odirect_GiBs"] = round(seg_len / 2 ** 30 / ((time.perf_counter() - t) / reps), 2)
+                except OSError as e:
+                    res["decode_file_odirect_GiBs"] = f"O_DIRECT read failed: {e}"
+                finally:
+                    os.close(dfd)
+            res["tmp_fs"] = _fs_of(tmp)
             t = time.perf_counter()
             for i in range(reps):
                 st.read(fd, 0, seg_len, d_seg.data_ptr(), stream.cuda_stream, threads=8)
@@ -169,8 +214,10 @@ def end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec, 
         finally:
             os.close(fd)
     st.close()
-    res["note"] = ("source and output files in the page cache; 16 pinned 8 MiB slices, 8 pread / pwrite threads; compaction = "
-                   "read + decode + re-encode + hint rebuild + dst WAL and hint written back")
+    res["note"] = ("decode_file / compaction: source and output files in the page cache; decode_file_cold: the source "
+                   "written back and dropped from the page cache (posix_fadvise DONTNEED) before every read; "
+                   "decode_file_odirect: read through an O_DIRECT descriptor; 16 pinned 8 MiB slices, 8 pread / pwrite "
+                   "threads; compaction = read + decode + re-encode + hint rebuild + dst WAL and hint written back")
     return res
 
 

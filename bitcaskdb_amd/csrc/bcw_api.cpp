@@ -332,13 +332,14 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.lbe);
   (void)hipFree(s.frags);
   (void)hipFree(s.misc);
+  (void)hipFree(s.equeue);
   s = Scratch{};
 }
 
 static void free_enc_scratch(EncScratch& e) {
   void* ptrs[] = {e.sz,    e.mflag, e.dsrc, e.da,      e.hda,       e.hsz,  e.dpos,
                   e.hpos,  e.tiles, e.ev,   e.evb,     e.recdesc,   e.emisc, e.evt,
-                  e.hnl,   e.evw};
+                  e.hnl,   e.evw,   e.wl};
   for (void* q : ptrs) (void)hipFree(q);
   hipStream_t aux = e.aux;
   hipEvent_t evs[3] = {e.ev_scan, e.ev_hscan, e.ev_desc};
@@ -405,7 +406,7 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.rbase, (nb + 1) * 4) == hipSuccess &&
             hipMalloc(&s.bsum, (nb + 1) * sizeof(uint2)) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
             hipMalloc(&s.lbe, nwg * 8) == hipSuccess && hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
-            hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess;
+            hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess && hipMalloc(&s.equeue, 8 * 128) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;
   s.frag_cap = fc;
@@ -660,7 +661,7 @@ static int ensure_enc_scratch(bcw_ctx* c, uint64_t rows) {
             hipMalloc(&e.ev, (r + 2) * enc_sizeof_ev()) == hipSuccess && hipMalloc(&e.evb, nwin * 4) == hipSuccess &&
             hipMalloc(&e.evt, nwin * 32768 * 8) == hipSuccess && hipMalloc(&e.hnl, r * 2) == hipSuccess &&
             hipMalloc(&e.evw, nwin * 12) == hipSuccess &&
-            hipMalloc(&e.recdesc, r * enc_sizeof_recdesc()) == hipSuccess &&
+            hipMalloc(&e.recdesc, r * enc_sizeof_recdesc()) == hipSuccess && hipMalloc(&e.wl, r * 4) == hipSuccess &&
             hipMalloc(&e.emisc, 64 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_enc_scratch(e); return BCW_E_NOMEM; }
   if (!e.aux && (hipStreamCreateWithFlags(&e.aux, hipStreamNonBlocking) != hipSuccess ||

@@ -191,6 +191,7 @@ __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, u
 // 0xffff: none) << 16; y = that fragment's block-relative start | has-Full/Last << 16. The tail is the part
 // after the block's last Full/Last fragment (the whole block when it has none).
 constexpr uint32_t kSumHasE = 1u << 16;
+constexpr int kEqStride = 32;  // k_crc's per-XCD emission queue heads: 128 B apart
 
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no predecessor sum, 2 no table writes,
 // 16 phase cycles (chase, sum, writes; s_memtime) summed into misc[7..9]
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                               Frag* __restrict__ frags, uint64_t frag_cap, uint64_t* __restrict__ lb,
                                               uint64_t* __restrict__ lbe, uint64_t* __restrict__ misc,
                                               uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc,
-                                              uint32_t direct_max) {
+                                              uint32_t direct_max, uint32_t* __restrict__ equeue) {
   // {crc, start | len << 16} and type of each lane's headers: 9 KiB, so a k_chase workgroup fits beside a k_crc
   // workgroup (which leaves 11 KiB of the CU's LDS) when another segment's decode is in flight
   __shared__ uint32_t s_hold[kChaseHold][2][64];
@@ -363,6 +364,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     misc[M_BAD_CRC] = ~0ull;      // k_crc: first fragment failing its CRC
     misc[M_FIRST_BAD] = ~0ull;    // k_crc: first record whose RecordFromBytes / Decode fails
   }
+  if (wg == 0 && lane < 8u) equeue[lane * kEqStride] = 0;  // k_crc's emission queues
 }
 
 // ------------------------------------------------------------------------------------------
@@ -567,9 +569,9 @@ struct BodyDesc {
 // while the accumulated record is empty; Full returns the Full's data with that offset; First/Middle
 // append; Last appends and returns the record; any other type is an error; a CRC mismatch is an error)
 // depends on the CRC verdicts only through the first failing fragment, after which nothing is emitted.
-// So every record is emitted from the header chase alone -- by the k_crc wave that owns its Full/Last
-// fragment, once that wave's CRC passes are done -- and the finalizer counts the records before the first
-// failing fragment. The state entering a wave comes from k_chase's block summaries (kSumHasE): the nearest
+// So every record is emitted from the header chase alone -- by k_crc waves whose CRC passes are done, from
+// per-XCD queues of ~64-fragment work items (emit_item) -- and the finalizer counts the records before the
+// first failing fragment. The state entering a wave comes from k_chase's block summaries (kSumHasE): the nearest
 // earlier block with a Full/Last fragment contributes its tail, the blocks after it their whole length.
 
 // byte `pos` of a register window (N dwords, pos < 4N): a select tree on the bits of the dword index
@@ -593,51 +595,51 @@ __device__ __forceinline__ uint32_t reg_byte(const uint32_t (&h)[N], uint32_t po
   return (t[0] >> (8u * (pos & 3u))) & 0xffu;
 }
 
-constexpr int kHeadWords = 20;  // 80 B aligned window: the record's first 64 B (and more) from any alignment
-constexpr int kTailWords = 12;  // 48 B aligned window: the record's last 32 B (hint mode: fid, offset, size)
+// record bytes held in registers, loaded with unaligned 16 B loads (global_load_dwordx4 at any byte address)
+constexpr int kHeadWords = 16;  // the record's first 64 B
+constexpr int kTailWords = 8;   // its last 32 B (hint mode: fid, offset and size follow the key)
+
+// byte `pos` of a record whose bytes start in fragment f_first (and end in f_last), by a walk over its fragments:
+// the reader's rare slow path, out of line so that its code exists once
+__device__ __attribute__((noinline)) uint32_t walk_byte(const uint8_t* __restrict__ seg, const Frag* __restrict__ frags,
+                                                        uint32_t start_off, uint32_t f_first, uint32_t f_last,
+                                                        uint64_t pos) {
+  uint64_t beg = 0;
+  for (uint32_t cf = f_first;; ++cf) {
+    const Frag f = frags[cf];
+    if (pos < beg + f.len || cf >= f_last)
+      return seg[(uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start + (pos - beg)];
+    beg += f.len;
+  }
+}
 
 // logical byte reader of one record: its first bytes and (hint mode) its last bytes in registers, else a
 // walk over its fragments
 struct RegReader {
   uint32_t h[kHeadWords];
   uint32_t t[kTailWords];
-  uint32_t hsh, nhead;   // head: window shift, bytes of the record held
-  uint32_t tsh;          // tail: window shift of the byte at tstart
+  uint32_t nhead;        // head: record bytes held
   uint64_t tstart;       // first record byte held by the tail (>= size when none)
   const uint8_t* seg;
   const Frag* frags;
   uint32_t start_off;
   uint32_t f_first, f_last;
-  uint32_t cf;
-  uint64_t cbeg, clen, caddr;
   __device__ __forceinline__ uint32_t operator()(uint64_t pos) {
-    if (pos < nhead) return reg_byte(h, hsh + (uint32_t)pos);
-    if (pos >= tstart) return reg_byte(t, tsh + (uint32_t)(pos - tstart));
-    if (pos < cbeg) {
-      cf = f_first;
-      cbeg = 0;
-      const Frag f = frags[cf];
-      clen = f.len;
-      caddr = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
-    }
-    while (pos >= cbeg + clen && cf < f_last) {
-      cbeg += clen;
-      ++cf;
-      const Frag f = frags[cf];
-      clen = f.len;
-      caddr = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
-    }
-    return seg[caddr + (pos - cbeg)];
+    if (pos < nhead) return reg_byte(h, (uint32_t)pos);
+    if (pos >= tstart) return reg_byte(t, (uint32_t)(pos - tstart));
+    return walk_byte(seg, frags, start_off, f_first, f_last, pos);
   }
 };
 
+// 4N bytes at seg + base (any alignment; bounds-checked bytes where they pass the segment end)
 template <int N>
 __device__ __forceinline__ void load_words(const uint8_t* __restrict__ seg, uint64_t seg_len, uint64_t base,
                                            uint32_t (&w)[N]) {
   if (base + 4u * N <= seg_len) {
 #pragma unroll
     for (int k = 0; k < N / 4; ++k) {
-      const uint4 v = *reinterpret_cast<const uint4*>(seg + base + 16 * k);
+      uint4 v;
+      __builtin_memcpy(&v, seg + base + 16 * k, 16);
       w[4 * k + 0] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
     }
   } else {
@@ -659,54 +661,85 @@ struct EmitArgs {
   const uint2* bsum;
   bcw_record_table tab;
   uint64_t* misc;
+  uint32_t* equeue;  // [8 x kEqStride] per-XCD emission work-queue heads (reset by k_chase)
+  uint32_t kb_flags; // tools/kbench only (0 in the product): 1 = skip the emission at run time
+  uint64_t* kb_stamps;  // tools/kbench only (null in the product): per wave {CRC done, emission done, items}
 };
 
-// Emit the records completed by fragments [f0, f1) of blocks starting at b0 (one wave): rows of the record
-// table from rbase[b0] on, RecordFromBytes (record.go:140-239) / HintRecord.Decode (hint.go:50-84) per record,
+// The iterator state entering block b0 (wave-uniform): the pending record's length, its first non-empty
+// fragment as (block, block-local index, block-relative start), and the record row of block b0.
+struct EmitState {
+  uint64_t acc;
+  int64_t nzb;  // -1: no non-empty fragment pending
+  uint32_t nzk, nzs;
+  uint64_t rec;
+};
+// the first walk-back step's summaries (lane l: block b0 - 1 - l), loaded ahead by the caller
+__device__ __forceinline__ uint2 emit_prefetch(const EmitArgs& A, uint64_t b0, uint32_t lane) {
+  return b0 > lane ? A.bsum[b0 - 1 - lane] : make_uint2(0xffff0000u, kSumHasE);
+}
+// walk back over the block summaries, 64 blocks a step, to the nearest block with a Full/Last fragment (before
+// block 0: an empty state); s = emit_prefetch(A, b0, lane)
+__device__ __forceinline__ EmitState emit_state(const EmitArgs& A, uint64_t b0, uint32_t lane, uint2 s, uint32_t rec) {
+  EmitState st{0, -1, 0, 0, rec};
+  uint64_t acc = 0;
+  for (uint64_t top = b0; top > 0;) {
+    if (top != b0) {
+      const uint64_t q = top - 1 - lane;
+      s = top > lane ? A.bsum[q] : make_uint2(0xffff0000u, kSumHasE);
+    }
+    const uint64_t he = __ballot((s.y & kSumHasE) != 0u);
+    const uint32_t stop = he ? (uint32_t)__builtin_ctzll(he) : 63u;
+    const bool contrib = lane <= stop;
+    uint32_t ta = contrib ? (s.x & 0xffffu) : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) ta += (uint32_t)__shfl_xor((int)ta, d, 64);
+    acc += (uint32_t)__builtin_amdgcn_readfirstlane(ta);
+    const uint64_t nzm = __ballot(contrib && (s.x >> 16) != 0xffffu);
+    if (nzm) {  // the earliest block (highest lane) holding a non-empty fragment of the pending record
+      const uint32_t L = 63u - __builtin_clzll(nzm);
+      st.nzb = (int64_t)(top - 1 - L);
+      st.nzk = (uint32_t)__builtin_amdgcn_readlane((int)(s.x >> 16), L);
+      st.nzs = (uint32_t)__builtin_amdgcn_readlane((int)(s.y & 0xffffu), L);
+    }
+    if (he) break;
+    top = top > 64 ? top - 64 : 0;
+  }
+  st.acc = acc;
+  return st;
+}
+
+// Emit the records completed by fragments [f0, f1) (one wave), entering with state es: rows of the record
+// table from es.rec on, RecordFromBytes (record.go:140-239) / HintRecord.Decode (hint.go:50-84) per record,
 // one lane each.
-__device__ void emit_wave(const EmitArgs& A, uint64_t b0, uint64_t f0, uint64_t f1, uint32_t lane) {
-  if (f0 >= f1) return;
+// hook(): called once, right after the first chunk's fragment descriptors are requested (the caller issues the
+// next work item's loads there, so they fly beside this item's).
+template <int ABL = 0, typename Hook>  // kbench ablations: 4096 no parse, 8192 no parse and no record-prefix loads
+__device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& es, uint64_t f0, uint64_t f1,
+                                            uint32_t lane, Hook&& hook) {
+  if (f0 >= f1) {
+    hook();
+    return;
+  }
   const Frag* __restrict__ frags = A.frags;
   const uint32_t start_off = A.p.start_off;
-  // the state entering block b0: walk back over the block summaries, 64 blocks a step, to the nearest block
-  // with a Full/Last fragment (before block 0: an empty state)
-  uint64_t acc = 0, off = 0;
+  uint64_t acc = es.acc, off = 0;
   uint32_t first = 0;
-  {
-    int64_t nzb = -1;
-    uint32_t nzk = 0, nzs = 0;
-    for (uint64_t top = b0; top > 0;) {
-      const uint64_t q = top - 1 - lane;  // lane 0: the nearest block
-      const uint2 s = top > lane ? A.bsum[q] : make_uint2(0xffff0000u, kSumHasE);
-      const uint64_t he = __ballot((s.y & kSumHasE) != 0u);
-      const uint32_t stop = he ? (uint32_t)__builtin_ctzll(he) : 63u;
-      const bool contrib = lane <= stop;
-      uint32_t ta = contrib ? (s.x & 0xffffu) : 0u;
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) ta += (uint32_t)__shfl_xor((int)ta, d, 64);
-      acc += ta;
-      const uint64_t nzm = __ballot(contrib && (s.x >> 16) != 0xffffu);
-      if (nzm) {  // the earliest block (highest lane) holding a non-empty fragment of the pending record
-        const uint32_t L = 63u - __builtin_clzll(nzm);
-        nzb = (int64_t)(top - 1 - L);
-        nzk = (uint32_t)__builtin_amdgcn_readlane((int)(s.x >> 16), L);
-        nzs = (uint32_t)__builtin_amdgcn_readlane((int)(s.y & 0xffffu), L);
-      }
-      if (he) break;
-      top = top > 64 ? top - 64 : 0;
-    }
-    if (nzb >= 0) {
-      off = (uint64_t)start_off + (uint64_t)nzb * kBlock + nzs;
-      first = A.fbase[nzb] + nzk;
-    }
+  if (es.nzb >= 0) {
+    off = (uint64_t)start_off + (uint64_t)es.nzb * kBlock + es.nzs;
+    first = A.fbase[es.nzb] + es.nzk;
   }
-  uint64_t rec = A.rbase[b0];
+  uint64_t rec = es.rec;
   const bool hint = A.p.mode == BCW_MODE_HINT;
   for (uint64_t c0 = f0; c0 < f1; c0 += 64) {
     const uint64_t g = c0 + lane;
     const bool valid = g < f1;
-    Frag f{};
-    if (valid) f = frags[g];
+    // unconditional (clamped) load: a branch around it would make the compiler wait for it at the merge
+    const uint4 fr = reinterpret_cast<const uint4*>(frags)[valid ? g : f1 - 1];
+    if (c0 == f0) hook();
+    Frag f;
+    __builtin_memcpy(&f, &fr, sizeof f);
+    if (!valid) f = Frag{};
     const uint32_t len = valid ? f.len : 0u;
     const uint64_t D = (uint64_t)start_off + (uint64_t)f.blk * kBlock + f.start;
     const bool isE = valid && (f.type == BCW_RECORD_FULL || f.type == BCW_RECORD_LAST);
@@ -770,29 +803,34 @@ __device__ void emit_wave(const EmitArgs& A, uint64_t b0, uint64_t f0, uint64_t 
       const uint64_t a0 = (uint64_t)start_off + (uint64_t)fs.blk * kBlock + fs.start;
       uint64_t want = size < 64u ? size : 64u;
       if (want > fs.len) want = fs.len;
-      const uint64_t hb = a0 & ~15ull;
-      rd.hsh = (uint32_t)(a0 - hb);
       rd.nhead = (uint32_t)want;
-      load_words(A.seg, A.seg_len, hb, rd.h);
+      if (ABL & 8192) {
+#pragma unroll
+        for (int k = 0; k < kHeadWords; ++k) rd.h[k] = 0;
+      } else {
+        load_words(A.seg, A.seg_len, a0, rd.h);
+      }
       rd.tstart = ~0ull;
-      rd.tsh = 0;
       if (hint) {  // the last bytes: HintRecord.Decode reads fid, offset and size after the key
         uint64_t nt = size < 32u ? size : 32u;
         if (nt > len) nt = len;
-        const uint64_t te = D + len - nt;  // this lane's (Full/Last) fragment ends the record
-        const uint64_t tb = te & ~15ull;
-        rd.tsh = (uint32_t)(te - tb);
         rd.tstart = size - nt;
-        load_words(A.seg, A.seg_len, tb, rd.t);
+        load_words(A.seg, A.seg_len, D + len - nt, rd.t);  // this lane's (Full/Last) fragment ends the record
       } else {
 #pragma unroll
         for (int k = 0; k < kTailWords; ++k) rd.t[k] = 0;
       }
       rd.seg = A.seg; rd.frags = frags; rd.start_off = start_off;
-      rd.f_first = src; rd.f_last = (uint32_t)g; rd.cf = src; rd.cbeg = 0; rd.clen = fs.len; rd.caddr = a0;
+      rd.f_first = src; rd.f_last = (uint32_t)g;
       uint8_t status, hdr, flags, etag_off;
       uint64_t key_len, val_len, meta_len, expire, aux0, aux1;
-      parse_record(A.p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
+      if (ABL & (4096 | 8192)) {
+        status = (uint8_t)(rd.h[0] == 0x12345u);
+        hdr = flags = etag_off = 0;
+        key_len = val_len = meta_len = expire = aux0 = aux1 = rd.h[1];
+      } else {
+        parse_record(A.p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
+      }
       const bcw_record_table& tab = A.tab;
       if (r < tab.capacity) {
         tab.foff[r] = foff;
@@ -817,6 +855,26 @@ __device__ void emit_wave(const EmitArgs& A, uint64_t b0, uint64_t f0, uint64_t 
     off = off2;
     first = first2;
   }
+}
+
+// Emission work item `it`: the records completed by the fragments of blocks [it * bpw, (it + 1) * bpw) (about 64
+// fragments), by whichever k_crc wave takes it from its XCD's queue once its own CRC passes are done -- the waves
+// that finish early emit for the whole segment, so the last wave to finish its CRC seldom finds work left.
+struct ItemMeta {
+  uint64_t bb;
+  uint2 s;  // emit_prefetch of block bb
+  uint32_t f0, f1, rec;
+};
+__device__ __forceinline__ ItemMeta item_meta(const EmitArgs& A, uint64_t it, uint64_t bpw, uint64_t nblocks,
+                                              uint32_t lane) {
+  ItemMeta m;
+  m.bb = it * bpw < nblocks ? it * bpw : nblocks - 1;  // a clamped (unconditional) load for an exhausted queue
+  const uint64_t be = m.bb + bpw < nblocks ? m.bb + bpw : nblocks;
+  m.s = emit_prefetch(A, m.bb, lane);
+  m.f0 = A.fbase[m.bb];
+  m.f1 = A.fbase[be];
+  m.rec = A.rbase[m.bb];
+  return m;
 }
 
 // The segment result, by one wave once every k_crc wave has verified and emitted: the first failing fragment
@@ -879,7 +937,7 @@ __device__ void finalize(const EmitArgs& A, uint64_t nblocks, uint64_t frag_cap,
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
 // 4 no lane-operator / scan combine, 8 no record-state tail, 16 phase stamps, 128 no first-window mask, 256 no last-window fix,
 // 512 per-wave wall-clock stamps (entry, tables loaded, loop done) into the expire column as u64[4] per wave, 1024 no
-// priority balancing
+// priority balancing, 32768 no CRC passes (the emission alone)
 template <int ABL = 0>
 __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                      uint32_t start_off, uint64_t nblocks,
@@ -897,17 +955,26 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   uint32_t* s_wave_all = s_carry + kLdsOps;
   const uint32_t tid = threadIdx.x;
   __shared__ uint32_t s_wdone;      // waves of this workgroup done
+  __shared__ uint32_t s_eq;         // the workgroup's emission items taken
   __shared__ uint32_t s_rem[kCrcWaves];  // windows each wave has left (balance)
-  if (tid == 0) s_wdone = 0;
+  if (tid == 0) { s_wdone = 0; s_eq = 0; }
   const uint32_t lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
-  const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
-  const uint64_t b0 = nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
+  // ABL & 65536: the workgroup's last wave is a dedicated record emitter (no CRC passes) from the kernel's start
+  constexpr bool kEm = (ABL & 65536) != 0;
+  constexpr uint32_t kNCrc = kEm ? kCrcWaves - 1 : kCrcWaves;  // CRC waves per workgroup
+  const bool emitter = kEm && wave == kCrcWaves - 1;
+  const uint64_t nw = (uint64_t)gridDim.x * kNCrc;
+  const uint64_t gw = (uint64_t)blockIdx.x * kNCrc + (emitter ? kNCrc - 1 : wave);
+  const uint64_t b0 = emitter ? nblocks * (gw + 1) / nw : nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
   // the wave's fragment range and its first descriptors are loaded while the table image crosses into LDS
   // (that chain of dependent loads no longer follows the image copy)
   const uint64_t f0 = fbase[b0];
   uint64_t f1 = fbase[b1];
+  // the emission work items (blocks per item for ~64 fragments each; see emit_item)
+  const uint64_t nf_all = misc[M_NFRAGS] < frag_cap ? misc[M_NFRAGS] : frag_cap;
+  uint64_t bpw = nf_all ? (64 * nblocks) / nf_all : nblocks;
+  if (bpw < 1) bpw = 1;
   uint4 pf = make_uint4(0, 0, 0, 0);  // the next group's 64 fragment descriptors (raw; see load_win)
   {  // table image -> LDS: all 16 B loads in flight before the first store
     constexpr uint32_t kVec = kLdsImage / 4;
@@ -1100,7 +1167,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     }
     if (d.active() && d.last()) {
       frags[f0 + d.fi].ok = (U == 0u) ? 1 : 0;
-      if (U != 0u) atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_CRC]), (unsigned long long)(f0 + d.fi));
+      if (U != 0u && !(ABL & 7)) atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_CRC]), (unsigned long long)(f0 + d.fi));
     }
     carry = __builtin_amdgcn_readlane(U, 63);
   };
@@ -1162,7 +1229,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       dn = describe(p + 64u);
     }
   };
-  if (nfr > 0u) pipeline();
+  if (nfr > 0u && !(ABL & 32768)) pipeline();
   stamp(t_comp);
   if ((ABL & 16) && lane == 0) {
     atomicAdd(reinterpret_cast<unsigned long long*>(&misc[7]), (unsigned long long)t_desc);
@@ -1175,8 +1242,47 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     uint64_t* q = ea.tab.expire + 4 * gw;  // kbench only (the table is overwritten by the emission unless ABL & 8)
     q[0] = t_entry; q[1] = t_tables; q[2] = wall_clock64(); q[3] = nfr;
   }
-  // ---- the records this wave's Full/Last fragments complete (no CRC verdict needed, see emit_wave) ----
-  if (!(ABL & 8)) emit_wave(ea, b0, f0, f1, lane);
+  // ---- record emission: the workgroup's work items (those starting in its blocks), taken from an LDS counter by
+  // its waves as they finish their CRC passes, so the early finishers emit for the late ones (ItemMeta). The next
+  // item is taken and its block data requested while this item's fragment descriptors are in flight, so an item
+  // costs two dependent round trips (descriptors, record prefixes) ----
+  if (!(ABL & 8) && !(ea.kb_flags & 1u)) {
+    const uint64_t B0 = nblocks * ((uint64_t)blockIdx.x * kNCrc) / nw;
+    const uint64_t B1 = nblocks * ((uint64_t)(blockIdx.x + 1) * kNCrc) / nw;
+    const uint64_t i0 = (B0 + bpw - 1) / bpw, nitems = (!kEm || emitter) ? (B1 + bpw - 1) / bpw : 0;
+    uint32_t taken = 0;  // the dedicated emitter takes every item in order
+    auto deq = [&]() -> uint64_t {
+      uint32_t j = 0;
+      if (kEm) {
+        j = taken++;
+      } else {
+        if (lane == 0) j = atomicAdd(&s_eq, 1u);
+        j = __builtin_amdgcn_readfirstlane(j);
+      }
+      return i0 + j;
+    };
+    const uint64_t t_crc = ea.kb_stamps ? wall_clock64() : 0;
+    uint64_t n_items = 0;
+    uint64_t it = deq();
+    ItemMeta m = item_meta(ea, it, bpw, nblocks, lane);
+    while (it < nitems) {
+      ++n_items;
+      const EmitState es = emit_state(ea, m.bb, lane, m.s, m.rec);
+      const uint64_t f1 = m.f1 < frag_cap ? m.f1 : frag_cap;
+      uint64_t nx = 0;
+      ItemMeta mn;
+      emit_chunks<ABL & (4096 | 8192)>(ea, es, m.f0, f1, lane, [&]() {
+        nx = deq();
+        mn = item_meta(ea, nx, bpw, nblocks, lane);
+      });
+      it = nx;
+      m = mn;
+    }
+    if (ea.kb_stamps && lane == 0) {
+      uint64_t* q = ea.kb_stamps + 4 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
+      q[0] = t_crc; q[1] = wall_clock64(); q[2] = n_items; q[3] = nfr;
+    }
+  }
   // ---- completion: each wave's stores and atomics are done (vmcnt(0)) before it counts itself done in LDS;
   // the last wave of a workgroup adds the workgroup to the agent-scope counter, and the last workgroup's
   // last wave writes the segment result from the agent-scope minima (MI355X_MICROARCH.md, inter-workgroup
@@ -1224,7 +1330,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   pr.begin(K_CHASE, stream, ev);
   k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
                                        s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch, tabs.initc,
-                                       s.chase_direct);
+                                       s.chase_direct, s.equeue);
   pr.end(K_CHASE, stream, ev);
   s.tickets += nb_grid;
   if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse
@@ -1234,7 +1340,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   }
   const uint64_t tail = (p.seg_len - p.start_off) % kBlock;
   const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;
-  const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc};
+  const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
   pr.begin(K_CRC, stream, ev);
   k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
                                                          s.frag_cap, tabs, ea, tail_panic, gen, d_result, s.misc);

@@ -56,6 +56,8 @@ enum {
   X_SRCERR = 2,   // source error class (BCW_ENC_ERR_SRC when iteration stopped on a bad row / fragment)
   X_NDENSE = 3,   // records written
   X_FAIL = 4,     // BCW_ENC_ERR_TABLE / BCW_ENC_ERR_STALE: the source inputs are unusable, nothing encoded
+  X_WL16 = 5,     // dst records k_wcopy leaves to k_write<16> (work list from the front of wl)
+  X_WLG = 6,      // ... and to k_write_general (from the back of wl)
   X_LAY = 8,      // per layout (wal: 8, hint: 16): +0 A_N, +1 nev, +2 k_end, +3 end, +4 b0, +5 U, +6 ok
 };
 constexpr int kLayStride = 8;
@@ -921,6 +923,9 @@ struct WArgs {
   const uint32_t* wops;   // enc_ops (layout in bcw_internal.h)
   const uint32_t* initc;  // A_{8L}(0xFFFFFFFF)
   uint32_t abl;           // measurement-only ablations of k_wcopy (BCW_ENC_ABL bits 4/8/16); 0 in the product
+  uint32_t* wl;           // [rows] k_wcopy's leftover dst records: k_write<16>'s from the front, k_write_general's
+  uint64_t rows;          //   from the back (counts in emisc[X_WL16], emisc[X_WLG])
+  uint64_t* wcnt;         // emisc + X_WL16
 };
 
 __device__ __forceinline__ uint64_t blk_end(uint64_t P) { return P + kL - (P - 40) % kL; }
@@ -1057,7 +1062,9 @@ __device__ __forceinline__ uint4 unit_general(const EncDev& e, const WRec& R, co
 
 template <int kG>
 __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
-  const uint64_t N = A.emisc[X_NDENSE];
+  // the dst records k_wcopy listed (usually none: then every workgroup leaves before building its tables)
+  const uint64_t nitems = A.wcnt[0];
+  if ((uint64_t)blockIdx.x * (kWT / kG) >= nitems) return;
   const EncDev& e = A.e;
   __shared__ uint32_t t8[8 * 256];
   __shared__ uint32_t sop[40 * kWopStride];  // A_{8*16*n}, A_{8*256*n} (n < 16), A_{8*4096*n} (n < 8)
@@ -1089,26 +1096,25 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
   const bool ok0 = lay_ok(A.emisc, A.w[0]), ok1 = A.nlay > 1 && lay_ok(A.emisc, A.w[1]);
   const uint32_t* hop = sop + (kG < 16 ? kG : 16 + kG / 16) * kWopStride;  // A_{8*16*kG}: one round of the group
 
-  // items: the records of layout 0, then those of layout 1 (short hint records last), one per group
-  // of kG lanes. An item's descriptor is loaded one item ahead: the RecDescW spread over the group's
-  // lanes 0-7 (header, then the literal bytes), da[j], da[j+1] and fpos[j] in every lane.
+  // items: the listed dst records, one per group of kG lanes. An item's descriptor is loaded one item ahead:
+  // the RecDescW spread over the group's lanes 0-7 (header, then the literal bytes), da[j], da[j+1] and fpos[j]
+  // in every lane.
   static_assert(kG == 16, "group size: the DPP row rotation shares source blocks within rows of 16 lanes");
-  const uint64_t nitems = N * A.nlay;
   struct Pre {
     uint4 q;
-    uint64_t a0, a1, fp;
+    uint64_t a0, a1, fp, j;
   };
   auto fetch = [&](uint64_t it2, Pre& p) {
     p.q = make_uint4(0, 0, 0, 0);
-    p.a0 = p.a1 = p.fp = 0;
+    p.a0 = p.a1 = p.fp = p.j = 0;
     if (it2 >= nitems) return;
-    const bool l2 = it2 >= N;
-    const uint64_t j2 = it2 - (l2 ? N : 0);
-    const WLay& W2 = l2 ? A.w[1] : A.w[0];
+    const uint64_t j2 = A.wl[it2];
+    const WLay& W2 = A.w[0];
     if (gl < 8) p.q = reinterpret_cast<const uint4*>(static_cast<const RecDescW*>(W2.rd) + j2)[gl];
     p.a0 = W2.da[j2];
     p.a1 = W2.da[j2 + 1];
     p.fp = W2.fpos[j2];
+    p.j = j2;
   };
   // the group's lane k holds word x
   auto gw = [&](uint32_t x, uint32_t k) { return (uint32_t)__shfl((int)x, (int)(gb + k), 64); };
@@ -1118,8 +1124,8 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
     const Pre pc = pn;
     const uint4 qc = pc.q;
     fetch(it + ng, pn);  // in flight while this item is written
-    const uint32_t li = it >= N ? 1u : 0u;
-    const uint64_t j = it - (li ? N : 0);
+    const uint32_t li = 0;
+    const uint64_t j = pc.j;
     const WLay& Ly = li ? A.w[1] : A.w[0];
     if (!(li ? ok1 : ok0)) continue;  // nothing to write / does not fit (the result says so)
     const uint32_t h1w = gw(qc.w, 1);
@@ -1314,27 +1320,11 @@ __global__ __launch_bounds__(kWT) void k_write(WArgs A) {
 
 // The general records of k_write (literal bytes beyond kWLit): one thread per record, bytewise.
 template <int PM>
-__global__ __launch_bounds__(256) void k_write_general(WArgs WA, uint32_t li, const uint32_t* __restrict__ dsrc,
-                                                        const uint64_t* __restrict__ dst_da,
-                                                        const uint64_t* __restrict__ dpos,
-                                                        const uint8_t* __restrict__ mflag) {
-  const WLay A = li ? WA.w[1] : WA.w[0];
-  __shared__ uint32_t t0[256];
-  for (uint32_t i = threadIdx.x; i < 256; i += 256) {
-    uint32_t c = i;
-    for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
-    t0[i] = c;
-  }
-  __syncthreads();
-  if (!lay_ok(WA.emisc, A)) return;
-  const uint64_t j = blockIdx.x * 256ull + threadIdx.x;
-  if (j >= WA.emisc[X_NDENSE]) return;
-  const RecDescW* D = static_cast<const RecDescW*>(A.rd) + j;
-  if (!D->general) return;
+__device__ void write_general_rec(const WArgs& WA, const WLay& A, uint64_t j, const uint32_t* __restrict__ dsrc,
+                                  const uint64_t* __restrict__ dst_da, const uint64_t* __restrict__ dpos,
+                                  const uint8_t* __restrict__ mflag, const uint32_t* t0, Prog& p, uint8_t* plit) {
   const EncDev& e = WA.e;
   const uint64_t row = dsrc[j];
-  Prog p;
-  uint8_t plit[48];
   const LitLocal lit{plit};
   prog_of<PM>(e, j, row, dst_da, dpos, mflag, p, lit);
   const SrcRec sr = src_rec(e.t, e.frags, row);
@@ -1376,6 +1366,32 @@ __global__ __launch_bounds__(256) void k_write_general(WArgs WA, uint32_t li, co
     hp = be;
   }
 }
+
+// The records come from k_wcopy's work list (the back of wl, emisc[X_WLG] of them; usually none, and then every
+// workgroup leaves at once); persistent grid. The payload program and its literals live in LDS (no scratch).
+template <int PM>
+__global__ __launch_bounds__(256) void k_write_general(WArgs WA, uint32_t li, const uint32_t* __restrict__ dsrc,
+                                                        const uint64_t* __restrict__ dst_da,
+                                                        const uint64_t* __restrict__ dpos,
+                                                        const uint8_t* __restrict__ mflag) {
+  const uint64_t nitems = WA.wcnt[1];
+  if ((uint64_t)blockIdx.x * 256 >= nitems) return;
+  const WLay A = li ? WA.w[1] : WA.w[0];
+  __shared__ uint32_t t0[256];
+  __shared__ Prog s_prog[256];
+  __shared__ uint8_t s_plit[256][48];
+  for (uint32_t i = threadIdx.x; i < 256; i += 256) {
+    uint32_t c = i;
+    for (int b = 0; b < 8; ++b) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    t0[i] = c;
+  }
+  __syncthreads();
+  if (!lay_ok(WA.emisc, A)) return;
+  for (uint64_t it = blockIdx.x * 256ull + threadIdx.x; it < nitems; it += (uint64_t)gridDim.x * 256)
+    write_general_rec<PM>(WA, A, WA.wl[WA.rows - 1 - it], dsrc, dst_da, dpos, mflag, t0, s_prog[threadIdx.x],
+                          s_plit[threadIdx.x]);
+}
+
 
 // ------------------------------------------------------------------------------------------
 // k_wcopy: the dst WAL records whose CRC follows from rcrc (RecDescW `regular` bits 0 and 1) and that
@@ -1481,7 +1497,13 @@ __global__ __launch_bounds__(kCT) void k_wcopy(WArgs A) {
     const uint64_t P = uni64(nP), aj = uni64(na0), len = uni64(na1) - aj - kHdr;
     fetch(j + nw);
     const uint32_t h1w = uni((uint32_t)__shfl((int)dw, 7, 64));
-    if (!wcopy_item(h1w, P, len)) continue;
+    if (!wcopy_item(h1w, P, len)) {  // k_write<16>'s or, with long literals, k_write_general's
+      if (lane == 0) {
+        if ((h1w >> 24) != 0) A.wl[A.rows - 1 - atomicAdd((unsigned long long*)&A.wcnt[1], 1ull)] = (uint32_t)j;
+        else A.wl[atomicAdd((unsigned long long*)&A.wcnt[0], 1ull)] = (uint32_t)j;
+      }
+      continue;
+    }
     __builtin_amdgcn_wave_barrier();
     if (lane < 32) sd[lane] = dw;  // the previous record's reads are done (LDS keeps a wave's order)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1891,6 +1913,9 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     W.w[0] = WLay{s.da, s.dpos, wd, L.out.wal, L.p.wal_pos, L.out.wal_cap, 0};
     W.w[1] = WLay{s.hda, s.hpos, nullptr, L.out.hint, L.p.hint_pos, L.out.hint_cap, 1};
     W.nlay = 1;
+    W.wl = s.wl;
+    W.rows = rows;
+    W.wcnt = s.emisc + X_WL16;
     const int abl = abl_env & 3;
     pr.begin(K_ENC_WRITE, st, ev0);
     // measurement-only ablation (BCW_ENC_ABL: 1 = dst WAL only, 2 = hint WAL only); 0 in the product
@@ -1898,7 +1923,8 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
       k_wcopy<<<(uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, (uint64_t)L.num_cus * 8)), kCT, 0,
                 st>>>(W);
       k_write<16><<<wgrid(16), kWT, 0, st>>>(W);
-      k_write_general<PM_DST><<<rgrid, 256, 0, st>>>(W, 0, s.dsrc, nullptr, nullptr, s.mflag);
+      k_write_general<PM_DST><<<std::min<uint32_t>(rgrid, (uint32_t)L.num_cus * 4), 256, 0, st>>>(W, 0, s.dsrc, nullptr,
+                                                                                            nullptr, s.mflag);
     }
     if (abl != 1) k_hwrite<PM_HINT_DST><<<rgrid, 256, 0, st>>>(W, 1, s.dsrc, s.da, s.dpos);
     pr.end(K_ENC_WRITE, st, ev0);

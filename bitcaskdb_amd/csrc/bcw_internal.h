@@ -70,6 +70,7 @@ struct Scratch {
   uint64_t epoch = 1;          // look-back epoch of the next launch
   Frag* frags = nullptr;       // [frag_cap]
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
+  uint32_t* equeue = nullptr;  // [8 x 32] k_crc emission work-queue heads, one 128 B line per XCD
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
 };
 
@@ -130,6 +131,7 @@ struct EncScratch {
   uint16_t* hnl = nullptr;    // [rows] next event inside the window (k_ev_win)
   uint32_t* evw = nullptr;    // [rows/win+2][3] window entries (k_ev_walk)
   void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc_w -> k_write), dst WAL
+  uint32_t* wl = nullptr;     // [rows] dst records k_wcopy leaves to k_write<16> / k_write_general
   uint64_t* emisc = nullptr;  // [64] counters
   // the payload descriptors are built on an auxiliary stream while the serial layout scans run
   hipStream_t aux = nullptr;

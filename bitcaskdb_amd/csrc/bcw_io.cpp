@@ -5,6 +5,7 @@
 // pinned staging slices: reader threads pread slices into pinned buffers while earlier slices are
 // already crossing PCIe (hipMemcpyAsync on the caller's stream), and device output comes back in
 // slices whose pwrite overlaps the next slice's copy.
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
@@ -77,6 +78,13 @@ int bcw_stage_read(bcw_stage* s, int fd, uint64_t file_off, uint64_t len, uint8_
   DeviceGuard dg(s->ctx->device);
   if (!dg.ok) return BCW_E_HIP;
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : s->ctx->cur;
+  // a descriptor opened with O_DIRECT (reads from the device, past the page cache, like the reference's io_uring
+  // block reader on an O_DIRECT file, block_reader/iouring.go): offsets 4 KiB-aligned, every request a whole
+  // number of 4 KiB units (the pinned slices are page-aligned; a short read at end of file is the tail)
+  const int fl = fcntl(fd, F_GETFL);
+  const bool direct = fl >= 0 && (fl & O_DIRECT) != 0;
+  constexpr uint64_t kDio = 4096;
+  if (direct && (file_off % kDio != 0 || s->slice % kDio != 0)) return BCW_E_INVAL;
   const uint64_t nsl = (len + s->slice - 1) / s->slice;
   const uint32_t ns = (uint32_t)s->slots.size();
   const uint32_t nt = std::max<uint32_t>(1, std::min<uint32_t>({threads ? threads : 4, ns, (uint32_t)nsl}));
@@ -91,10 +99,12 @@ int bcw_stage_read(bcw_stage* s, int fd, uint64_t file_off, uint64_t len, uint8_
       const uint64_t off = k * s->slice, n = std::min(s->slice, len - off);
       uint64_t got = 0;
       while (got < n) {  // PreadFull (utils.go:32-48)
-        const ssize_t r = pread(fd, q.host + got, n - got, (off_t)(file_off + off + got));
+        const uint64_t want = direct ? (n - got + kDio - 1) / kDio * kDio : n - got;  // <= slice - got
+        const ssize_t r = pread(fd, q.host + got, want, (off_t)(file_off + off + got));
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) { err = BCW_E_IO; return; }
         got += (uint64_t)r;
+        if (direct && got < n && (got % kDio) != 0) { err = BCW_E_IO; return; }  // a short read before the end
       }
       if (hipMemcpyAsync(d_dst + off, q.host, n, hipMemcpyHostToDevice, st) != hipSuccess ||
           hipEventRecord(q.done, st) != hipSuccess) {

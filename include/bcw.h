@@ -455,7 +455,9 @@ int bcw_read_records(bcw_ctx* ctx, const uint8_t* h_seg, const bcw_read_params* 
 typedef struct bcw_stage bcw_stage;
 int bcw_stage_create(bcw_ctx* ctx, uint64_t slice_bytes, uint32_t nslices, bcw_stage** out);
 int bcw_stage_destroy(bcw_stage* st);
-/* len bytes of fd at file_off -> d_dst (device). Returns BCW_E_IO on a read error or a short file. */
+/* len bytes of fd at file_off -> d_dst (device). Returns BCW_E_IO on a read error or a short file. A descriptor
+ * opened with O_DIRECT is read past the page cache (the reference's io_uring block reader, block_reader/
+ * iouring.go:47-76): file_off and slice_bytes must then be multiples of 4096 (else BCW_E_INVAL). */
 int bcw_stage_read(bcw_stage* st, int fd, uint64_t file_off, uint64_t len, uint8_t* d_dst, void* hip_stream,
                    uint32_t threads);
 /* len bytes of d_src (device) -> fd at file_off: each slice is copied back after the work queued on

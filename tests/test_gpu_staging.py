@@ -43,6 +43,31 @@ def test_stage_roundtrip(ctx, tmp_path, size, slice_, threads):
     st.close()
 
 
+@pytest.mark.parametrize("size", [4096, (9 << 20) + 4096 * 3 + 123])
+def test_stage_read_odirect(ctx, tmp_path, size):
+    """an O_DIRECT descriptor (reads past the page cache): whole-4-KiB requests, the short tail at end of file;
+    unaligned offsets are refused. Skipped where the filesystem refuses O_DIRECT (tmpfs)."""
+    rng = np.random.default_rng(size)
+    data = rng.integers(0, 256, size, dtype=np.uint8)
+    src = tmp_path / "src.bin"
+    src.write_bytes(data.tobytes())
+    try:
+        fd = os.open(str(src), os.O_RDONLY | os.O_DIRECT)
+    except OSError as e:
+        pytest.skip(f"O_DIRECT refused here: {e.strerror}")
+    st = Stage(ctx, 1 << 20, 4)
+    buf = D.DevBuf(size + 64)
+    try:
+        st.read(fd, 0, size, buf.ptr, threads=3)
+        ctx.sync()
+        assert bytes(buf.download(size)) == data.tobytes()
+        with pytest.raises(OSError):
+            st.read(fd, 100, 4096, buf.ptr)  # not 4 KiB-aligned
+    finally:
+        os.close(fd)
+        st.close()
+
+
 def test_file_to_file_compaction(ctx, tmp_path):
     """a data WAL on disk -> staged into HBM -> decode -> re-encode (all kept) and hint rebuild on the device
     -> staged back to the dst WAL / hint files: the files equal the oracle's."""

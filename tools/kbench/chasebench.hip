@@ -1,0 +1,58 @@
+// Header-chase latency probe (not product code): one lane per 32 KiB block of a 1 GiB buffer, a chain of
+// dependent 12-byte loads, with the chain's start at the block start (+40, like a WAL segment) or at a random
+// offset, and with the stride between hops taken from the loaded data (like the chase) -- to see whether
+// block-aligned starts collide on HBM channels and what one dependent round trip costs.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#define CK(x) do { auto e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s:%d err %d\n", __FILE__, __LINE__, (int)e_); exit(1);} } while (0)
+
+template <int HOPS>
+__global__ __launch_bounds__(64) void k_hops(const uint8_t* __restrict__ buf, uint64_t n, uint32_t start_mode,
+                                             uint32_t* __restrict__ out) {
+  const uint64_t b = blockIdx.x * 64ull + threadIdx.x;
+  uint64_t off = b * 32768 + (start_mode == 0 ? 40 : ((b * 2654435761ull) & 32000));
+  uint32_t acc = 0;
+#pragma unroll 1
+  for (int h = 0; h < HOPS; ++h) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(buf + (off & ~3ull));
+    const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+    acc ^= w0 ^ w2;
+    off += 7 + (w1 & 0xfffu);  // data-dependent hop (the buffer holds small values)
+    if (off + 12 > (b + 1) * 32768) off = b * 32768 + 40;
+  }
+  out[b] = acc;
+}
+
+int main() {
+  const uint64_t n = 1ull << 30;
+  uint8_t* d;
+  CK(hipMalloc(&d, n));
+  std::vector<uint32_t> h(n / 4);
+  for (size_t i = 0; i < h.size(); ++i) h[i] = (uint32_t)((i * 2654435761u) >> 7) & 0xfffu;
+  CK(hipMemcpy(d, h.data(), n, hipMemcpyHostToDevice));
+  uint32_t* out;
+  CK(hipMalloc(&out, (n / 32768) * 4));
+  hipEvent_t a, e;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&e));
+  const uint32_t grid = (uint32_t)(n / 32768 / 64);
+  auto t = [&](auto k, uint32_t mode) {
+    float best = 1e9;
+    for (int r = 0; r < 10; ++r) {
+      CK(hipEventRecord(a));
+      k<<<grid, 64>>>(d, n, mode, out);
+      CK(hipEventRecord(e));
+      CK(hipEventSynchronize(e));
+      float ms; CK(hipEventElapsedTime(&ms, a, e));
+      if (ms < best) best = ms;
+    }
+    return best * 1e3;
+  };
+  printf("hops 1: block-start %.1f us  random %.1f us\n", t(k_hops<1>, 0), t(k_hops<1>, 1));
+  printf("hops 2: block-start %.1f us  random %.1f us\n", t(k_hops<2>, 0), t(k_hops<2>, 1));
+  printf("hops 4: block-start %.1f us  random %.1f us\n", t(k_hops<4>, 0), t(k_hops<4>, 1));
+  printf("hops 8: block-start %.1f us  random %.1f us\n", t(k_hops<8>, 0), t(k_hops<8>, 1));
+  printf("hops 16: block-start %.1f us  random %.1f us\n", t(k_hops<16>, 0), t(k_hops<16>, 1));
+  return 0;
+}

@@ -270,20 +270,54 @@ int main(int argc, char** argv) {
     }
   }
   const uint64_t nblocks = (n - 40 + kBlock - 1) / kBlock;
-  const EmitArgs ea{d, n, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc};
-  auto run = [&](auto kern, int grid) {
-    return timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres, s.misc); },
+  const EmitArgs ea{d, n, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
+  EmitArgs ea_off = ea;
+  ea_off.kb_flags = 1u;  // the product kernel with its emission skipped at run time
+  EmitArgs ea_st = ea;   // ... with per-wave stamps of its CRC end, emission end and items
+  CK(hipMalloc(&ea_st.kb_stamps, 4 * 8 * (size_t)ctx->num_cus * kCrcWaves));
+  auto stamp_report = [&]() {
+    const int nw = ctx->num_cus * kCrcWaves;
+    std::vector<uint64_t> q(4 * (size_t)nw);
+    CK(hipMemcpy(q.data(), ea_st.kb_stamps, q.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull;
+    for (int w = 0; w < nw; ++w) t0 = std::min(t0, q[4 * w]);
+    std::vector<double> ce(nw), ee(nw);
+    std::vector<uint64_t> it(nw);
+    uint64_t tot = 0;
+    for (int w = 0; w < nw; ++w) { ce[w] = (q[4 * w] - t0) / 100.0; ee[w] = (q[4 * w + 1] - t0) / 100.0; it[w] = q[4 * w + 2]; tot += it[w]; }
+    std::vector<double> sc = ce, se = ee; std::sort(sc.begin(), sc.end()); std::sort(se.begin(), se.end());
+    std::vector<uint64_t> si = it; std::sort(si.begin(), si.end());
+    printf("emission stamps (us after the first wave's CRC end): CRC end p10 %.1f p50 %.1f p90 %.1f max %.1f | "
+           "emission end p50 %.1f p90 %.1f max %.1f | items total %lu, per wave p50 %lu p90 %lu max %lu\n",
+           sc[nw / 10], sc[nw / 2], sc[nw * 9 / 10], sc[nw - 1], se[nw / 2], se[nw * 9 / 10], se[nw - 1], tot,
+           si[nw / 2], si[nw * 9 / 10], si[nw - 1]);
+    int last = 0; for (int w = 0; w < nw; ++w) if (ee[w] > ee[last]) last = w;
+    printf("  last wave to finish: w%d CRC end %.1f emission end %.1f items %lu\n", last, ce[last], ee[last], it[last]);
+  };
+  auto run = [&](auto kern, int grid, const EmitArgs& a) {
+    return timeit([&] { hipMemsetAsync(s.equeue, 0, 1024, st);  // the emission queues (k_chase resets them)
+                        kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc); },
                   reps, st);
   };
   const int cus = ctx->num_cus;
   auto runv = [&](int v) -> float {
     switch (v) {
-      case 1: return run(k_crc<1>, cus);
-      case 2: return run(k_crc<2>, cus);
-      case 8: return run(k_crc<8>, cus);
-      case 128: return run(k_crc<128>, cus);
-      case 1024: return run(k_crc<1024>, cus);
-      default: return run(k_crc<0>, cus);
+      case 1: return run(k_crc<1>, cus, ea);
+      case 99: return run(k_crc<0>, cus, ea_off);
+      case 32768: return run(k_crc<32768>, cus, ea);
+      case 40960: return run(k_crc<32768 | 8192>, cus, ea);
+      case 32776: return run(k_crc<32768 | 8>, cus, ea);
+      case 65536: return run(k_crc<65536>, cus, ea);
+      case 65537: { const float r = run(k_crc<65536>, cus, ea_st); stamp_report(); return r; }
+      case 36864: return run(k_crc<32768 | 4096>, cus, ea);
+      case 98: { const float r = run(k_crc<0>, cus, ea_st); stamp_report(); return r; }
+      case 2: return run(k_crc<2>, cus, ea);
+      case 8: return run(k_crc<8>, cus, ea);
+      case 128: return run(k_crc<128>, cus, ea);
+      case 1024: return run(k_crc<1024>, cus, ea);
+      case 4096: return run(k_crc<4096>, cus, ea);
+      case 8192: return run(k_crc<8192>, cus, ea);
+      default: return run(k_crc<0>, cus, ea);
     }
   };
   if (argc > 4 && std::string(argv[3]) == "cmp") {  // k_crc variants interleaved in one process (same buffers)
@@ -354,18 +388,18 @@ int main(int argc, char** argv) {
     float tm = 0;
     for (int i = 0; i < k; ++i) {
       switch (v) {
-        case 1: tm = run(k_crc<1>, cus); break;
-        case 2: tm = run(k_crc<2>, cus); break;
-        case 4: tm = run(k_crc<4>, cus); break;
-        case 8: tm = run(k_crc<8>, cus); break;
-        case 128: tm = run(k_crc<128>, cus); break;
-        case 256: tm = run(k_crc<256>, cus); break;
-        case 384: tm = run(k_crc<384>, cus); break;
-        case 7: tm = run(k_crc<7>, cus); break;
-        case 520: tm = run(k_crc<520>, cus); break;
-        case 1544: tm = run(k_crc<1544>, cus); break;
-        case 1024: tm = run(k_crc<1024>, cus); break;
-        default: tm = run(k_crc<0>, cus);
+        case 1: tm = run(k_crc<1>, cus, ea); break;
+        case 2: tm = run(k_crc<2>, cus, ea); break;
+        case 4: tm = run(k_crc<4>, cus, ea); break;
+        case 8: tm = run(k_crc<8>, cus, ea); break;
+        case 128: tm = run(k_crc<128>, cus, ea); break;
+        case 256: tm = run(k_crc<256>, cus, ea); break;
+        case 384: tm = run(k_crc<384>, cus, ea); break;
+        case 7: tm = run(k_crc<7>, cus, ea); break;
+        case 520: tm = run(k_crc<520>, cus, ea); break;
+        case 1544: tm = run(k_crc<1544>, cus, ea); break;
+        case 1024: tm = run(k_crc<1024>, cus, ea); break;
+        default: tm = run(k_crc<0>, cus, ea);
       }
     }
     CK(hipStreamSynchronize(st));
@@ -415,8 +449,8 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
-  float a0 = run(k_crc<0>, cus), a1 = run(k_crc<1>, cus), a2 = run(k_crc<2>, cus), a4 = run(k_crc<4>, cus),
-        a3 = run(k_crc<3>, cus), a7 = run(k_crc<7>, cus), a8 = run(k_crc<8>, cus);
+  float a0 = run(k_crc<0>, cus, ea), a1 = run(k_crc<1>, cus, ea), a2 = run(k_crc<2>, cus, ea), a4 = run(k_crc<4>, cus, ea),
+        a3 = run(k_crc<3>, cus, ea), a7 = run(k_crc<7>, cus, ea), a8 = run(k_crc<8>, cus, ea);
   printf("k_crc full      %.4f ms  %.1f GB/s\n", a0, n / (a0 * 1e-3) / 1e9);
   printf("k_crc no-chain  %.4f ms\n", a1);
   printf("k_crc no-loads  %.4f ms\n", a2);
@@ -426,13 +460,14 @@ int main(int argc, char** argv) {
   printf("k_crc no emission %.4f ms\n", a8);
   const float as = timeit([&] {
     hipMemsetAsync(&s.misc[M_DONE_CRC], 0, 8, st);  // the last workgroup finalizes
+    hipMemsetAsync(s.equeue, 0, 1024, st);
     k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
                                           s.misc);
   }, reps, st);
   printf("k_crc + finalize %.4f ms\n", as);
   {
     CK(hipMemset(&s.misc[7], 0, 24));
-    run(k_crc<16 | 8>, cus);
+    run(k_crc<16 | 8>, cus, ea);
     uint64_t m[3];
     CK(hipMemcpy(m, &s.misc[7], 24, hipMemcpyDeviceToHost));
     const double w = (double)cus * kCrcWaves * (reps + 1);  // waves x launches
@@ -451,7 +486,7 @@ int main(int argc, char** argv) {
       return timeit([&] {
         kern<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
                                                               s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch,
-                                                              ctx->tabs.initc, s.chase_direct);
+                                                              ctx->tabs.initc, s.chase_direct, s.equeue);
         s.tickets += (nblocks + 63) / 64;
         ++s.epoch;
       }, reps, st);
