@@ -50,6 +50,8 @@ def parse():
                          "(own stream, segment, record table); the headline value is one segment at a time")
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events bracket every N-th k_crc launch of the timed region")
+    ap.add_argument("--decode-path", type=int, default=1, choices=[0, 1],
+                    help="0: one launch per segment (k_scan, the default); 1: k_chase + k_crc (BCW_OPT_DECODE_PATH)")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_v6_k_crc_pmc.json"),
                     help="PMC traffic summary (rocprofv3 --pmc of this command) to report as roofline.traffic")
@@ -291,6 +293,7 @@ def main():
         d_res = torch.zeros(C.sizeof(L.DecodeResult), dtype=torch.uint8, device=dev)
         params = L.DecodeParams(seg_len, BASE_TIME, 40, 20, 20, L.MODE_RECORD)
         sctx = Context(torch.cuda.current_device())
+        sctx.set_option(L.OPT_DECODE_PATH, args.decode_path)
         sstream = torch.cuda.Stream()  # dedicated stream: the codec's kernels and the timing events share it
         sctx.set_stream(sstream.cuda_stream)
         slots.append(dict(host=host, seg_len=seg_len, n_rec=n_rec, d_seg=d_seg, cols=cols, table=table, d_res=d_res,
@@ -339,7 +342,9 @@ def main():
     # kernel ids by name (the pipeline's kernel list is the library's)
     nk = int(L.lib.bcw_ctx_kernel_times(ctx.handle, None, None, 0))
     names = [L.lib.bcw_kernel_name(k).decode() for k in range(nk)]
-    roof_k = names.index("k_crc")
+    # the dominant kernel: the whole one-launch decode (k_scan), or k_crc of the two-launch path
+    roof_name = "k_crc" if args.decode_path == 1 else "k_scan"
+    roof_k = names.index(roof_name)
 
     def kernel_times(ctxs):
         """per-kernel average over the given contexts (reading resets their accumulators)"""
@@ -355,7 +360,7 @@ def main():
 
     all_ctx = [sl["ctx"] for sl in slots]
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks ----
-    # HIP events bracket only the roofline kernel (k_crc) on each codec stream
+    # HIP events bracket only the roofline kernel (k_scan / k_crc) on each codec stream
     # (every --event-every-th launch: an event pair idles that stream for a few microseconds)
     for cx in all_ctx:
         L.lib.bcw_ctx_set_profiling(cx.handle, 1 << roof_k)
@@ -369,7 +374,7 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize()
     ev_ms = ev0.elapsed_time(ev1)
-    crc_ms, crc_samples = kernel_times(all_ctx)["k_crc"]
+    crc_ms, crc_samples = kernel_times(all_ctx)[roof_name]
     bytes_total = seg_len * args.steps
     # pipelined: the same K steps rotating over the in-flight segments (an extra key, never `value`: with two
     # streams a k_crc event pair also spans the other segment's kernels)
@@ -419,19 +424,20 @@ def main():
             dist.destroy_process_group()
         return
 
-    # ---- roofline of the dominant kernel (k_crc): algorithmic bytes per launch / avg duration ----
+    # ---- roofline of the dominant kernel (k_scan: the whole decode; k_crc on the two-launch path): algorithmic
+    # bytes per launch / avg duration ----
     alg_bytes = seg_len + 17 * n_frags  # segment read once + fragment descriptors (16 B read, 1 B verdict)
     achieved = alg_bytes / (crc_ms * 1e-3) / 1e9
     traffic = None
     if args.pmc and os.path.exists(args.pmc):
         try:
             pm = json.load(open(args.pmc))
-            if pm.get("seg_bytes") == seg_len:
+            if pm.get("seg_bytes") == seg_len and pm.get("kernel") == roof_name:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_crc",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": roof_name,
                 "kernel_ms": round(crc_ms, 4), "kernel_launches_timed": crc_samples, "alg_bytes": alg_bytes,
                 "pipeline_GBs": round(bytes_total / args.steps / (ms_per_step * 1e-3) / 1e9, 1),
                 "kernel_ms_all": {k: round(v, 4) for k, v in kern.items()}}

@@ -333,6 +333,8 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.frags);
   (void)hipFree(s.misc);
   (void)hipFree(s.equeue);
+  (void)hipFree(s.lbw);
+  (void)hipFree(s.pwin);
   s = Scratch{};
 }
 
@@ -402,11 +404,13 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   const uint64_t nb = std::max(nblocks, s.nblocks_cap);
   const uint64_t fc = std::max(frag_cap, s.frag_cap);
   free_scratch(s);
-  const uint64_t nwg = nb / 64 + 2;  // k_chase look-back words: one per 64-block workgroup
+  // look-back words: one per 64-block k_chase workgroup, or one per k_scan workgroup (one per CU)
+  const uint64_t nwg = std::max<uint64_t>(nb / 64 + 2, (uint64_t)c->num_cus + 2);
   bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.rbase, (nb + 1) * 4) == hipSuccess &&
             hipMalloc(&s.bsum, (nb + 1) * sizeof(uint2)) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
             hipMalloc(&s.lbe, nwg * 8) == hipSuccess && hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
-            hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess && hipMalloc(&s.equeue, 8 * 128) == hipSuccess;
+            hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess && hipMalloc(&s.equeue, 8 * 128) == hipSuccess &&
+            hipMalloc(&s.lbw, nwg * 8) == hipSuccess && hipMalloc(&s.pwin, (nb * 256 + 4) * 4) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;
   s.frag_cap = fc;
@@ -414,13 +418,18 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   s.tickets = 0;
   s.epoch = 1;
   s.chase_direct = c->chase_direct;
+  s.scan = c->scan;
   // on the codec's stream: a null-stream hipMemset is not ordered before kernels on a non-blocking
   // stream, and a look-back word zeroed after k_chase published it would never be seen again
   // misc[15] (the first unknown-type fragment, an atomicMin in k_chase) starts at UINT64_MAX; every decode's
   // finalizer resets it for the next one
+  // k_scan has no k_chase in front to reset misc[0] (first bad record) and misc[14] (first CRC failure): they start
+  // at UINT64_MAX too
   if (hipMemsetAsync(s.lb, 0, nwg * 8, c->cur) != hipSuccess || hipMemsetAsync(s.lbe, 0, nwg * 8, c->cur) != hipSuccess ||
-      hipMemsetAsync(s.misc, 0, 15 * sizeof(uint64_t), c->cur) != hipSuccess ||
-      hipMemsetAsync(s.misc + 15, 0xff, sizeof(uint64_t), c->cur) != hipSuccess) {
+      hipMemsetAsync(s.lbw, 0, nwg * 8, c->cur) != hipSuccess ||
+      hipMemsetAsync(s.misc, 0, 16 * sizeof(uint64_t), c->cur) != hipSuccess ||
+      hipMemsetAsync(s.misc + 14, 0xff, 2 * sizeof(uint64_t), c->cur) != hipSuccess ||
+      hipMemsetAsync(s.misc, 0xff, sizeof(uint64_t), c->cur) != hipSuccess) {
     free_scratch(s);
     return BCW_E_HIP;
   }
@@ -483,7 +492,7 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
                                                                                                   : BCW_E_HIP;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_records", "k_enc_prep", "k_enc_scan", "k_events",
+static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_scan", "k_enc_prep", "k_enc_scan", "k_events",
                                           "k_write", "k_hint_layout", "k_events_hint"};
 
 int bcw_ctx_reserve_fragments(bcw_ctx* c, uint64_t n) {
@@ -499,6 +508,11 @@ int bcw_ctx_set_option(bcw_ctx* c, int option, uint64_t value) {
       if (value > BCW_CHASE_DIRECT_MAX) return BCW_E_INVAL;
       c->s.chase_direct = (uint32_t)value;
       c->chase_direct = (uint32_t)value;
+      return BCW_OK;
+    case BCW_OPT_DECODE_PATH:
+      if (value > 1) return BCW_E_INVAL;
+      c->s.scan = value == 0 ? 1u : 0u;
+      c->scan = c->s.scan;
       return BCW_OK;
     default:
       return BCW_E_INVAL;

@@ -678,15 +678,46 @@ struct EmitState {
 __device__ __forceinline__ uint2 emit_prefetch(const EmitArgs& A, uint64_t b0, uint32_t lane) {
   return b0 > lane ? A.bsum[b0 - 1 - lane] : make_uint2(0xffff0000u, kSumHasE);
 }
+// k_scan: the block summaries, fragment table and block bases of an earlier workgroup's blocks (blocks < B0) were
+// written inside the same launch by another CU. A wave reads them only after every predecessor has published its
+// "written" word (behind an agent release) and the wave has run an agent acquire (MI355X_MICROARCH.md,
+// inter-workgroup visibility: one relaxed poll, one agent acquire, s_waitcnt vmcnt(0)) -- lazily, the first time a
+// walk-back has to cross B0. k_crc (whose tables come from k_chase, an earlier launch) passes B0 = 0, acq = true.
+struct PredSync {
+  uint64_t B0 = 0;
+  const uint64_t* lbw = nullptr;  // per-workgroup "written" words (epoch << 40 | 1)
+  uint64_t wg = 0, epoch = 0;
+  bool acq = true;
+  __device__ __forceinline__ void acquire(uint32_t lane) {
+    for (uint64_t q0 = 0; q0 < wg; q0 += 64) {
+      const uint64_t q = q0 + lane;
+      if (q < wg)
+        while ((__hip_atomic_load(&lbw[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 40) != epoch)
+          __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    acq = true;
+  }
+};
 // walk back over the block summaries, 64 blocks a step, to the nearest block with a Full/Last fragment (before
 // block 0: an empty state); s = emit_prefetch(A, b0, lane)
-__device__ __forceinline__ EmitState emit_state(const EmitArgs& A, uint64_t b0, uint32_t lane, uint2 s, uint32_t rec) {
+__device__ __forceinline__ EmitState emit_state(const EmitArgs& A, uint64_t b0, uint32_t lane, uint2 s, uint32_t rec,
+                                                PredSync& ps) {
   EmitState st{0, -1, 0, 0, rec};
   uint64_t acc = 0;
   for (uint64_t top = b0; top > 0;) {
     if (top != b0) {
       const uint64_t q = top - 1 - lane;
       s = top > lane ? A.bsum[q] : make_uint2(0xffff0000u, kSumHasE);
+    }
+    if (!ps.acq) {  // lanes past B0 read another workgroup's summaries: acquire them unless a nearer block ends a record
+      const uint64_t q = top - 1 - lane;
+      const bool pred = top > lane && q < ps.B0;
+      if (__ballot(pred) != 0ull && __ballot(top > lane && !pred && (s.y & kSumHasE) != 0u) == 0ull) {
+        ps.acquire(lane);
+        if (pred) s = A.bsum[q];
+      }
     }
     const uint64_t he = __ballot((s.y & kSumHasE) != 0u);
     const uint32_t stop = he ? (uint32_t)__builtin_ctzll(he) : 63u;
@@ -880,17 +911,23 @@ __device__ __forceinline__ ItemMeta item_meta(const EmitArgs& A, uint64_t it, ui
 // The segment result, by one wave once every k_crc wave has verified and emitted: the first failing fragment
 // is the earlier of the first CRC mismatch and the first unknown type (at the same fragment the CRC is
 // checked first, wal_iterator.go:79-95), and the records before it are the Full/Last fragments before it.
-__device__ void finalize(const EmitArgs& A, uint64_t nblocks, uint64_t frag_cap, uint32_t tail_panic, uint64_t gen,
+__device__ __forceinline__ void finalize(const EmitArgs& A, uint64_t nblocks, uint64_t frag_cap, uint32_t tail_panic, uint64_t gen,
                          bcw_decode_result* __restrict__ res, uint32_t lane) {
   uint64_t* misc = A.misc;
   const uint64_t bad_crc = __hip_atomic_load(&misc[M_BAD_CRC], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t bad_type = __hip_atomic_load(&misc[M_BAD_TYPE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t fb = __hip_atomic_load(&misc[M_FIRST_BAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t nfr = misc[M_NFRAGS];
+  const uint64_t nfr = __hip_atomic_load(&misc[M_NFRAGS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t err = bad_crc < bad_type ? bad_crc : bad_type;
   // records before fragment `lim` (the first failing one, or the fragment capacity of a decode to be retried)
   uint64_t lim = err < frag_cap ? err : frag_cap;
-  uint64_t nrec = misc[M_NE];
+  uint64_t nrec = __hip_atomic_load(&misc[M_NE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // k_scan wrote the block bases and the fragment table inside this launch, on other CUs: every workgroup has
+  // completed (its written word preceded its completion), so one agent acquire makes them readable here
+  if (lim < nfr || err != ~0ull) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   if (lim < nfr) {
     // the block holding fragment lim: the last b with fbase[b] <= lim (64-ary search)
     uint64_t lo = 0, hi = nblocks;
@@ -931,7 +968,11 @@ __device__ void finalize(const EmitArgs& A, uint64_t nblocks, uint64_t frag_cap,
   r.retry_frag_capacity = nfr > frag_cap ? nfr : 0;
   r.generation = gen;
   *res = r;
-  misc[M_BAD_TYPE] = ~0ull;  // for the next decode's k_chase
+  // for the next decode (k_chase resets the first three again; k_scan relies on these)
+  misc[M_DONE_CRC] = 0;
+  misc[M_BAD_CRC] = ~0ull;
+  misc[M_FIRST_BAD] = ~0ull;
+  misc[M_BAD_TYPE] = ~0ull;
 }
 
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
@@ -1265,9 +1306,10 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     uint64_t n_items = 0;
     uint64_t it = deq();
     ItemMeta m = item_meta(ea, it, bpw, nblocks, lane);
+    PredSync ps;  // k_chase's tables: nothing to acquire
     while (it < nitems) {
       ++n_items;
-      const EmitState es = emit_state(ea, m.bb, lane, m.s, m.rec);
+      const EmitState es = emit_state(ea, m.bb, lane, m.s, m.rec, ps);
       const uint64_t f1 = m.f1 < frag_cap ? m.f1 : frag_cap;
       uint64_t nx = 0;
       ItemMeta mn;
@@ -1303,6 +1345,481 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   finalize(ea, nblocks, frag_cap, tail_panic, gen, res, lane);
 }
 
+// ------------------------------------------------------------------------------------------
+// k_scan: the whole decode of a segment in ONE launch, so the header chase no longer runs as a
+// launch of its own in front of the CRC stream. One 1024-thread workgroup per CU; workgroups take tickets and own
+// consecutive block ranges [B0, B1) in ticket order (so a workgroup only ever waits on running ones).
+//
+// The CRC work is made independent of the fragment geometry. Windows are the absolute 128 B windows of the segment
+// (m: bytes [128m, 128m + 128)); workgroup w owns the windows m0 <= m < m1 whose first byte lies in its blocks. A
+// unit is 64 consecutive windows of the workgroup from m0 + 64u; lane l computes v = R(window) (raw CRC-32C, init
+// 0), maps it to the unit's end with F_l = A_{1024(63-l)} and the wave stores the prefix XOR
+//     P[m] = XOR_{i <= l} F_i(v_{m0 + 64u + i})           (the unit-end frame; pwin, 4 B per window).
+// A fragment with data [GS, GE) and check word J passes iff R(data || J) = 0 (J = the raw CRC its stored CRC
+// implies, see k_crc); with a = GS >> 7, j0 = GE >> 7 and j1 = (GE + 3) >> 7 that is
+//     T = XOR_{m = a..j1} A_{1024(F - m)}(z_m) = 0       (any frame F >= j1: the shift is invertible)
+// where z_m = R(window m with the bytes outside [GS, GE) zeroed and J written at [GE, GE + 4)). Every window
+// strictly between a and j0 lies inside the data (z_m = v_m) and inside the workgroup's own windows, so per unit
+// its sum is P[hi] ^ P[lo - 1]; the edge windows a, j0, j1 are recomputed masked (at most three per fragment).
+// Horner over the units a..j1 spans (A_{8*8192} between units) gives T in the frame of j1's unit end.
+//
+// Phases of a workgroup:
+//   chase   waves 0..nch-1 (nch = ceil((B1 - B0) / 64)) chase one block per lane (chase_block, the first headers
+//           held in LDS), the last of them publishes the workgroup's fragment / Full-Last counts and sums its
+//           predecessors' (direct: at most one word per CU), then every chaser writes its blocks' fragment table
+//           entries, fbase, rbase and summaries, and the last one publishes "written" behind an agent release.
+//   windows the other waves start at once (the chasers once done): units from an LDS counter, software-pipelined
+//           like k_crc (the next unit's loads issued right after the chain).
+//   verify  after a workgroup barrier: items of 64 of the workgroup's fragments, one lane per fragment.
+//   emit    k_crc's emission items over the workgroup's blocks; a walk-back that crosses B0 acquires the
+//           predecessors' writes first (PredSync).
+constexpr int kScanHoldWords = kCrcWaves * kWaveLds;  // the chasers' held headers (48 KiB, k_crc's ring space)
+
+// window bytes of a fragment for its zero test: data outside [gs, ge) zeroed, J at [ge, ge + 4) (window-relative,
+// any values). Per word: a kept-byte mask and the J bytes that land in it.
+__device__ __forceinline__ void mask_frag_window(uint32_t (&w)[32], int gs, int ge, uint32_t J) {
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int q = 4 * i;
+    const int lo = min(max(gs - q, 0), 4), hi = min(max(ge - q, 0), 4);  // kept bytes [lo, hi) of the word
+    const uint32_t keep = (uint32_t)((1ull << (8 * hi)) - 1ull) & ~(uint32_t)((1ull << (8 * lo)) - 1ull);
+    const int s = ge - q;  // position of J's first byte in the word
+    const uint32_t jw = (s > -4 && s < 4) ? (uint32_t)(((uint64_t)J << (8 * (s + 4))) >> 32) : 0u;
+    w[i] = (w[i] & keep) | jw;
+  }
+}
+
+// z_m of a fragment (absolute data [GS, GE), check word J): R of its masked / J-patched window m
+__device__ __forceinline__ uint32_t edge_window(const uint8_t* __restrict__ seg, uint64_t seg_len, int64_t m,
+                                                int64_t GS, int64_t GE, uint32_t J, const uint32_t* __restrict__ tab,
+                                                const uint32_t* __restrict__ half, const SliceLane& sl) {
+  const int64_t o = m * (int64_t)kWin;
+  uint32_t w[32];
+  if (o < GE && o + (int64_t)kWin > GS) {  // the window holds data bytes
+    load_window(seg, seg_len, o, (uint64_t)o + kWin <= seg_len, w);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) w[i] = 0u;
+  }
+  mask_frag_window(w, (int)(GS - o), (int)(GE - o), J);
+  return crc_window(tab, half, sl, 0u, w);
+}
+
+// ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain in the window units, 2 no verify,
+// 4 no window units, 8 no emission, 32 static unit ranges per wave, 512 per-wave wall-clock stamps into ea.kb_stamps
+// (8 x u64 per wave: entry, tables in LDS, chase written (chasers), units done, chase seen, verify done, all done)
+template <int ABL = 0>
+__global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict__ seg, uint64_t seg_len,
+                                                      uint32_t start_off, uint64_t nblocks, uint32_t* __restrict__ fbase,
+                                                      uint32_t* __restrict__ rbase, uint2* __restrict__ bsum,
+                                                      Frag* __restrict__ frags, uint64_t frag_cap,
+                                                      uint32_t* __restrict__ pwin,
+                                                      uint64_t* __restrict__ lb, uint64_t* __restrict__ lbe,
+                                                      uint64_t* __restrict__ lbw, uint64_t ticket_base, uint64_t epoch,
+                                                      Tables tabs, EmitArgs ea, uint32_t tail_panic, uint64_t gen,
+                                                      bcw_decode_result* __restrict__ res) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsImage + kScanHoldWords];
+  __shared__ uint64_t s_base[4];       // workgroup's first fragment, first record row, fragments, Full/Last fragments
+  __shared__ uint32_t s_ctot[kScanWaves], s_etot[kScanWaves];  // per chaser wave: fragments, Full/Last fragments
+  __shared__ uint32_t s_chn, s_chw, s_ready, s_unit, s_vq, s_eq, s_wdone;
+  __shared__ uint64_t s_wg;
+  __shared__ uint32_t s_udone[(kScanMaxBlocks * (kBlock / 8192) + 2 + 31) / 32];  // window units done (bit per unit)
+  __shared__ uint64_t s_em[4];  // emission items: B0, B1, blocks per item, the workgroup's fragment end
+  uint32_t* s_slice = lds;
+  uint32_t* s_fwd = lds + kLdsSlice;
+  uint32_t* s_carry = s_fwd + kLdsFwd;  // A_{8*8192}: one unit
+  uint32_t* s_half = s_carry + 128;
+  uint32_t* s_hold = lds + kLdsImage;
+  uint64_t* misc = ea.misc;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto stamp = [&](int k) {
+    if ((ABL & 512) && lane == 0) ea.kb_stamps[((uint64_t)blockIdx.x * kScanWaves + wave) * 8 + k] = wall_clock64();
+  };
+  stamp(0);
+  if (tid == 0) {
+    s_wg = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_TICKET]), 1ull) - ticket_base;
+    s_chn = s_chw = s_ready = s_unit = s_vq = s_eq = s_wdone = 0;
+  }
+  for (uint32_t i = tid; i < sizeof(s_udone) / 4; i += kScanThreads) s_udone[i] = 0u;
+  {  // table image -> LDS: all 16 B loads in flight before the first store
+    constexpr uint32_t kVec = kLdsImage / 4;
+    constexpr int kFull = (int)(kVec / kScanThreads);
+    const uint4* src = reinterpret_cast<const uint4*>(tabs.lds_image);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    uint4 v[kFull];
+#pragma unroll
+    for (int k2 = 0; k2 < kFull; ++k2) v[k2] = src[tid + k2 * kScanThreads];
+    const uint32_t tail = tid + kFull * kScanThreads;
+    uint4 vt = make_uint4(0, 0, 0, 0);
+    if (tail < kVec) vt = src[tail];
+    if (tail < kVec) dst[tail] = vt;
+#pragma unroll
+    for (int k2 = 0; k2 < kFull; ++k2) dst[tid + k2 * kScanThreads] = v[k2];
+  }
+  __syncthreads();
+  stamp(1);
+  stamp(2);
+  const uint64_t G = gridDim.x;
+  const uint64_t wg = s_wg;
+  const uint64_t B0 = nblocks * wg / G, B1 = nblocks * (wg + 1) / G;
+  const uint32_t nch = (uint32_t)((B1 - B0 + 63) / 64) > 0u ? (uint32_t)((B1 - B0 + 63) / 64) : 1u;
+  const uint64_t tag = epoch << 40;
+  // the workgroup's windows [m0, m1): those whose first byte lies in its blocks and in the segment (a window past the
+  // segment's end is never interior to a fragment). Only the last unit can then be partial or touch the segment's
+  // end -- at most one slow ("deferred") unit per workgroup, which the unit loop relies on.
+  const uint64_t mseg = (seg_len + kWin - 1) / kWin;
+  const uint64_t m0 = ((uint64_t)start_off + B0 * kBlock + kWin - 1) / kWin;
+  uint64_t m1 = ((uint64_t)start_off + B1 * kBlock + kWin - 1) / kWin;
+  if (m1 > mseg) m1 = mseg;
+  if (m1 < m0) m1 = m0;
+  const uint32_t nunits = (uint32_t)((m1 - m0 + 63) / 64);
+  const uint64_t mb = start_off / kWin;  // pwin[m - mb] holds window m's prefix
+  const SliceLane sl = slice_lane(lane);
+
+  // ---- chase (waves 0..nch-1): k_chase's per-block walk, one block per lane ----
+  if (wave < nch) {
+    const uint32_t NL = nch * 64u, L = wave * 64u + lane;
+    const uint32_t H = (uint32_t)kScanHoldWords / (3u * NL);  // held headers per lane
+    const uint64_t b = B0 + L;
+    uint32_t bufsize = 0;
+    uint64_t boff = 0;
+    if (b < B1) {
+      boff = (uint64_t)start_off + b * kBlock;
+      bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
+    }
+    uint32_t ne = 0, tacc = 0, tnz = 0xffffu, tst = 0, badk = 0xffffffffu;
+    const uint32_t n = chase_block(seg, seg_len, boff, bufsize,
+                                   [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
+                                     if (k < H) {
+                                       uint32_t* e = s_hold + (k * NL + L) * 3u;
+                                       e[0] = crc;
+                                       e[1] = start | (len << 16);
+                                       e[2] = type;
+                                     }
+                                     if (type == BCW_RECORD_FULL || type == BCW_RECORD_LAST) {
+                                       ++ne;
+                                       tacc = 0;
+                                       tnz = 0xffffu;
+                                     } else {
+                                       if (len > 0 && tnz == 0xffffu) { tnz = k; tst = start; }
+                                       tacc += len;
+                                       if ((type < BCW_RECORD_FULL || type > BCW_RECORD_LAST) && badk == 0xffffffffu)
+                                         badk = k;
+                                     }
+                                   });
+    const uint32_t incl = wave_add_scan(n, lane);
+    const uint32_t incl_e = wave_add_scan(ne, lane);
+    if (lane == 63) { s_ctot[wave] = incl; s_etot[wave] = incl_e; }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    uint32_t ord = 0;
+    if (lane == 0) ord = atomicAdd(&s_chn, 1u);
+    ord = __builtin_amdgcn_readfirstlane(ord);
+    if (ord == nch - 1u) {  // the last chaser wave: publish the workgroup's counts, sum the predecessors'
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      uint64_t wt = 0, wte = 0;
+      for (uint32_t c = 0; c < nch; ++c) { wt += s_ctot[c]; wte += s_etot[c]; }
+      if (lane == 0) {
+        __hip_atomic_store(&lb[wg], tag | (kLbAgg << 38) | (wt & kLbMask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&lbe[wg], tag | (kLbAgg << 38) | (wte & kLbMask), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint64_t c = 0, ce = 0;
+      for (uint64_t q0 = 0; q0 < wg; q0 += 64) {
+        const uint64_t q = q0 + lane;
+        if (q < wg) {
+          uint64_t v, ve;
+          while (((v = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
+            __builtin_amdgcn_s_sleep(1);
+          while (((ve = __hip_atomic_load(&lbe[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
+            __builtin_amdgcn_s_sleep(1);
+          c += v & kLbMask;
+          ce += ve & kLbMask;
+        }
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        c += (uint64_t)__shfl_xor((long long)c, d, 64);
+        ce += (uint64_t)__shfl_xor((long long)ce, d, 64);
+      }
+      if (lane == 0) {
+        s_base[0] = c; s_base[1] = ce; s_base[2] = wt; s_base[3] = wte;
+        const uint64_t bpw = wt ? (64 * (B1 - B0)) / wt : (B1 - B0);
+        s_em[0] = B0; s_em[1] = B1; s_em[2] = bpw < 1 ? 1 : bpw;
+        s_em[3] = c + wt < 0xffffffffull ? c + wt : 0xffffffffull;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    while (__hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+      __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    uint64_t wpre = 0, wpre_e = 0;
+    for (uint32_t c = 0; c < wave; ++c) { wpre += s_ctot[c]; wpre_e += s_etot[c]; }
+    const uint64_t g0 = s_base[0] + wpre + incl - n;
+    const uint64_t r0 = s_base[1] + wpre_e + incl_e - ne;
+    if (b < B1) {
+      fbase[b] = (uint32_t)(g0 < 0xffffffffull ? g0 : 0xffffffffull);
+      rbase[b] = (uint32_t)(r0 < 0xffffffffull ? r0 : 0xffffffffull);
+      bsum[b] = make_uint2(tacc | (tnz << 16), tst | (ne ? kSumHasE : 0u));
+      if (badk != 0xffffffffu)  // the first unknown-type fragment of the segment (reset by the previous finalize)
+        atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_TYPE]), (unsigned long long)(g0 + badk));
+      const uint32_t nh = n < H ? n : H;
+      for (uint32_t k = 0; k < nh; ++k) {
+        const uint32_t* e = s_hold + (k * NL + L) * 3u;
+        put_frag(frags, g0 + k, frag_cap, (uint32_t)b, e[1] & 0xffffu, e[1] >> 16, e[0], e[2], tabs.initc);
+      }
+      if (n > H)  // the tail of a block with more headers than held
+        chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
+          if (k >= H) put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, tabs.initc);
+        });
+    }
+    if (wg == G - 1u && wave == 0u && lane == 0u) {  // the segment totals
+      const uint64_t total = s_base[0] + s_base[2], total_e = s_base[1] + s_base[3];
+      fbase[nblocks] = (uint32_t)(total < 0xffffffffull ? total : 0xffffffffull);
+      rbase[nblocks] = (uint32_t)(total_e < 0xffffffffull ? total_e : 0xffffffffull);
+      __hip_atomic_store(&misc[M_NFRAGS], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&misc[M_NE], total_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // every chaser wave's stores are done before it counts itself; the last one releases them all (agent) and
+    // publishes the workgroup's written word
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    uint32_t ordw = 0;
+    if (lane == 0) ordw = atomicAdd(&s_chw, 1u);
+    ordw = __builtin_amdgcn_readfirstlane(ordw);
+    if (ordw == nch - 1u && lane == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&lbw[wg], tag | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    stamp(2);
+  }
+
+  // the chasers' writes are visible to this workgroup's waves (they wait for it before verify and emission)
+  auto wait_chase = [&]() {
+    while (__hip_atomic_load(&s_chw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < nch) __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  auto mark_done = [&](uint32_t u) {  // unit u's prefixes are stored (the caller waited for its store)
+    if (u < nunits && lane == 0) atomicOr(&s_udone[u >> 5], 1u << (u & 31u));
+  };
+  const bool chaser = wave < nch;
+  // A chaser wave, its fragment table written, emits records (a latency-bound chain: it needs no CRC result) while
+  // the other waves stream the window units; then every wave: units, verify items, the emission items left.
+  for (int ph = chaser ? 0 : 1; ph < 2; ++ph) {
+    if (ph == 1) {
+      // ---- windows: units of 64 windows from the LDS counter ----
+      const uint8_t* safe_win = seg_len >= kWin ? seg : reinterpret_cast<const uint8_t*>(tabs.lds_image);
+      // ABL & 32: static contiguous unit ranges per wave instead of the LDS counter (kbench)
+      const uint32_t su0 = nunits * wave / kScanWaves, su1 = nunits * (wave + 1) / kScanWaves;
+      uint32_t snext = su0;
+      auto take = [&]() -> uint32_t {
+        if (ABL & 32) { const uint32_t r = snext < su1 ? snext : nunits; ++snext; return r; }
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(&s_unit, 1u);
+        return __builtin_amdgcn_readfirstlane(u);
+      };
+      auto win_of = [&](uint32_t u) -> uint64_t { return m0 + 64ull * u + lane; };
+      auto fast = [&](uint32_t u) {  // every lane's window is in the segment (and the workgroup's)
+        return u < nunits && m0 + 64ull * u + 64 <= m1 && (m0 + 64ull * u + 64) * kWin <= seg_len;
+      };
+      // two window buffers: a unit's loads are issued one unit ahead, so they fly through the previous unit's chain
+      // (a single buffer reloaded after the chain left them nothing to overlap but the store: the loop waited ~ a
+      // full load latency per unit). Every lane loads (an invalid unit reads safe_win) so the loads are one
+      // straight-line group, and no load sits in a branch of the loop (the compiler then waits for every load in
+      // flight, both buffers'): the unit that is not "fast" -- the workgroup's partial last unit, or one at the
+      // segment's end -- is set aside and done after the loop with bounds-checked loads.
+      auto issue = [&](uint32_t u, uint32_t (&w)[32]) {
+        const uint4* q = reinterpret_cast<const uint4*>(fast(u) ? seg + win_of(u) * kWin : safe_win);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          const uint4 v = q[g];
+          w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+        }
+      };
+      auto finish = [&](uint32_t u, uint32_t (&w)[32], bool valid) {
+        const uint64_t m = win_of(u);
+        uint32_t v = (ABL & 1) ? (w[0] ^ w[31]) : crc_window(s_slice, s_half, sl, 0u, w);
+        if (!valid) v = 0u;
+        v = apply_fwd(s_fwd, lane, v);
+        const uint32_t P = wave_scan_z(v, [](uint32_t x, uint32_t y) { return x ^ y; });
+        if (valid) pwin[m - mb] = P;
+      };
+      uint32_t deferred = nunits;  // this wave's slow unit, if it took one
+      auto process = [&](uint32_t u, uint32_t (&w)[32]) {
+        if (u < nunits) {
+          if (fast(u)) finish(u, w, true);
+          else deferred = u;
+        }
+      };
+      uint32_t wa[32], wb[32];
+      uint32_t ua = (ABL & 4) ? nunits : take();
+      issue(ua, wa);
+      uint32_t ub = (ABL & 4) ? nunits : take();
+      issue(ub, wb);
+      // no exit between the halves (an exit there made the compiler wait for both buffers' loads): ub > ua, so a
+      // half whose unit is past the end only skips its compute. Before each half, every op but the other buffer's
+      // 8 loads has completed -- the previous half's store among them -- so that unit is marked done there.
+      uint32_t prev = nunits;
+      while (ua < nunits) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (prev != deferred) mark_done(prev);
+        process(ua, wa);
+        const uint32_t pa = ua;
+        ua = take();
+        issue(ua, wa);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (pa != deferred) mark_done(pa);
+        process(ub, wb);
+        prev = ub;
+        ub = take();
+        issue(ub, wb);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (prev != deferred) mark_done(prev);
+      if (deferred < nunits) {
+        const uint64_t m = win_of(deferred);
+        load_window(seg, seg_len, (int64_t)(m * kWin), false, wa);
+        finish(deferred, wa, m < m1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        mark_done(deferred);
+      }
+      stamp(3);
+
+      // ---- verify: one lane per fragment of the workgroup, items of 64 fragments once their units are done ----
+      wait_chase();
+      stamp(4);
+      const uint64_t F0 = s_base[0], NF = s_base[2];
+      const uint64_t Fa = F0 < frag_cap ? F0 : frag_cap;
+      const uint64_t Fb = F0 + NF < frag_cap ? F0 + NF : frag_cap;
+      const int64_t M0 = (int64_t)m0;
+      for (; !(ABL & 2);) {
+        uint32_t it = 0;
+        if (lane == 0) it = atomicAdd(&s_vq, 1u);
+        it = __builtin_amdgcn_readfirstlane(it);
+        const uint64_t g = Fa + 64ull * it + lane;
+        if (Fa + 64ull * it >= Fb) break;
+        Frag f{};
+        if (g < Fb) {
+          const uint4 raw = reinterpret_cast<const uint4*>(frags)[g];
+          __builtin_memcpy(&f, &raw, sizeof f);
+        }
+        const int64_t GS = (int64_t)start_off + (int64_t)f.blk * kBlock + f.start, GE = GS + f.len;
+        const int64_t a = GS >> 7, j0 = GE >> 7, j1 = (GE + 3) >> 7;
+        {  // wait for the units holding the interior windows (a, j0) of the item's fragments
+          const bool has = g < Fb && j0 - 1 > a;
+          const uint32_t ulo = has ? (uint32_t)((a + 1 - M0) >> 6) : 0xffffffffu;
+          const uint32_t uhi = has ? (uint32_t)((j0 - 1 - M0) >> 6) : 0u;
+          uint32_t mn = ulo, mx = uhi;
+#pragma unroll
+          for (int d = 32; d >= 1; d >>= 1) {
+            mn = min(mn, (uint32_t)__shfl_xor((int)mn, d, 64));
+            mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+          }
+          mn = __builtin_amdgcn_readfirstlane(mn);
+          mx = __builtin_amdgcn_readfirstlane(mx);
+          if (mn <= mx) {
+            for (uint32_t wd = mn >> 5; wd <= (mx >> 5); ++wd) {
+              const uint32_t blo = wd == (mn >> 5) ? (mn & 31u) : 0u, bhi = wd == (mx >> 5) ? (mx & 31u) : 31u;
+              const uint32_t need = (uint32_t)((2ull << bhi) - 1ull) & ~((1u << blo) - 1u);
+              while ((__hip_atomic_load(&s_udone[wd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & need) != need)
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          }
+        }
+        if (g < Fb) {
+          // the edge windows one at a time (one window of registers)
+          uint32_t z[3] = {0u, 0u, 0u};
+#pragma unroll 1
+          for (int e = 0; e < 3; ++e) {
+            const int64_t m = e == 0 ? a : (e == 1 ? j0 : j1);
+            if (e == 1 && j0 == a) continue;
+            if (e == 2 && (j1 == j0 || j1 == a)) continue;
+            const uint32_t v = edge_window(seg, seg_len, m, GS, GE, f.chk, s_slice, s_half, sl);
+            z[0] = e == 0 ? v : z[0];
+            z[1] = e == 1 ? v : z[1];
+            z[2] = e == 2 ? v : z[2];
+          }
+          const uint32_t za = z[0], zj0 = z[1], zj1 = z[2];
+          const int64_t pa = (a - M0) >> 6, pf = (j1 - M0) >> 6;
+          uint32_t T = 0;
+          for (int64_t p = pa; p <= pf; ++p) {
+            if (p > pa) T = apply_op(s_carry, T);
+            const int64_t wlo = M0 + 64 * p, whi = wlo + 63;
+            const int64_t lo = a + 1 > wlo ? a + 1 : wlo, hi = j0 - 1 < whi ? j0 - 1 : whi;
+            if (lo <= hi) T ^= pwin[hi - (int64_t)mb] ^ (lo > wlo ? pwin[lo - 1 - (int64_t)mb] : 0u);
+            if (((a - M0) >> 6) == p) T ^= apply_fwd(s_fwd, (uint32_t)((a - M0) & 63), za);
+            if (j0 != a && ((j0 - M0) >> 6) == p) T ^= apply_fwd(s_fwd, (uint32_t)((j0 - M0) & 63), zj0);
+            if (j1 != j0 && j1 != a && ((j1 - M0) >> 6) == p) T ^= apply_fwd(s_fwd, (uint32_t)((j1 - M0) & 63), zj1);
+          }
+          frags[g].ok = T == 0u ? 1 : 0;
+          if (T != 0u) atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_CRC]), (unsigned long long)g);
+        }
+      }
+      stamp(5);
+    }
+
+    // ---- record emission: items of ~64 fragments over the workgroup's blocks (k_crc's emit_chunks) ----
+    if (!(ABL & 8)) {
+      wait_chase();
+      const uint64_t nitems = (s_em[1] - s_em[0] + s_em[2] - 1) / s_em[2];
+      PredSync ps;
+      ps.B0 = B0; ps.lbw = lbw; ps.wg = wg; ps.epoch = epoch; ps.acq = (wg == 0);
+      // the item geometry lives in LDS and is re-read per item: the emission runs at the register limit
+      auto meta = [&](uint64_t it) -> ItemMeta {
+        const uint64_t b0 = s_em[0], b1 = s_em[1], bpw = s_em[2];
+        ItemMeta mm;
+        mm.bb = b0 + it * bpw;
+        if (mm.bb >= b1) mm.bb = b1 - 1;  // an exhausted queue: a clamped (unconditional) load
+        const uint64_t be = mm.bb + bpw < b1 ? mm.bb + bpw : b1;
+        mm.s = emit_prefetch(ea, mm.bb, lane);
+        mm.f0 = ea.fbase[mm.bb];
+        mm.f1 = be < b1 ? ea.fbase[be] : (uint32_t)s_em[3];
+        mm.rec = ea.rbase[mm.bb];
+        return mm;
+      };
+      auto deq = [&]() -> uint64_t {
+        uint32_t j = 0;
+        if (lane == 0) j = atomicAdd(&s_eq, 1u);
+        return __builtin_amdgcn_readfirstlane(j);
+      };
+      uint64_t it = deq();
+      ItemMeta m = meta(it);
+      while (it < nitems) {
+        const EmitState es = emit_state(ea, m.bb, lane, m.s, m.rec, ps);
+        const uint64_t f1 = m.f1 < frag_cap ? m.f1 : frag_cap;
+        uint64_t nx = 0;
+        ItemMeta mn;
+        emit_chunks<0>(ea, es, m.f0, f1, lane, [&]() {
+          nx = deq();
+          mn = meta(nx);
+        });
+        it = nx;
+        m = mn;
+      }
+    }
+  }
+
+  stamp(6);
+  // ---- completion (k_crc's protocol) ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  uint32_t order = 0;
+  if (lane == 0) order = atomicAdd(&s_wdone, 1u);
+  order = __builtin_amdgcn_readlane(order, 0);
+  if (order != kScanWaves - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  uint64_t gorder = 0;
+  if (lane == 0)
+    gorder = __hip_atomic_fetch_add(&misc[M_DONE_CRC], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  gorder = (uint64_t)__shfl((long long)gorder, 0, 64);
+  if (gorder != gridDim.x - 1u) return;
+  finalize(ea, nblocks, frag_cap, tail_panic, gen, res, lane);
+}
+
 __global__ void k_export_frags(const Frag* __restrict__ frags, const uint64_t* __restrict__ misc, uint64_t cap,
                                uint32_t start_off, bcw_frag_table out, const uint32_t* __restrict__ initc) {
   const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -1326,6 +1843,28 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   Prof dummy;
   Prof& pr = prof ? *prof : dummy;
   hipEvent_t ev = nullptr;
+  const uint64_t tail = (p.seg_len - p.start_off) % kBlock;
+  const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;
+  auto next_epoch = [&]() {
+    if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse
+      (void)hipMemsetAsync(s.lb, 0, s.nlb * sizeof(uint64_t), stream);
+      (void)hipMemsetAsync(s.lbe, 0, s.nlb * sizeof(uint64_t), stream);
+      (void)hipMemsetAsync(s.lbw, 0, s.nlb * sizeof(uint64_t), stream);
+      s.epoch = 1;
+    }
+  };
+  if (s.scan && nblocks <= (uint64_t)kScanMaxBlocks * (uint64_t)num_cus) {  // one launch (k_scan)
+    const uint32_t grid = (uint32_t)(nblocks < (uint64_t)num_cus ? nblocks : (uint64_t)num_cus);
+    const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
+    pr.begin(K_SCAN, stream, ev);
+    k_scan<0><<<grid, kScanThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum,
+                                                s.frags, s.frag_cap, s.pwin, s.lb, s.lbe, s.lbw, s.tickets, s.epoch,
+                                                tabs, ea, tail_panic, gen, d_result);
+    pr.end(K_SCAN, stream, ev);
+    s.tickets += grid;
+    next_epoch();
+    return hipGetLastError();
+  }
   const uint32_t nb_grid = (uint32_t)((nblocks + 63) / 64);
   pr.begin(K_CHASE, stream, ev);
   k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
@@ -1333,13 +1872,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
                                        s.chase_direct, s.equeue);
   pr.end(K_CHASE, stream, ev);
   s.tickets += nb_grid;
-  if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse
-    (void)hipMemsetAsync(s.lb, 0, s.nlb * sizeof(uint64_t), stream);
-    (void)hipMemsetAsync(s.lbe, 0, s.nlb * sizeof(uint64_t), stream);
-    s.epoch = 1;
-  }
-  const uint64_t tail = (p.seg_len - p.start_off) % kBlock;
-  const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;
+  next_epoch();
   const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
   pr.begin(K_CRC, stream, ev);
   k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,

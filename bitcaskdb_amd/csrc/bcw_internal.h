@@ -56,6 +56,12 @@ constexpr int kLdsImage = kLdsSlice + kLdsFwd + kLdsOps;
 #endif
 constexpr int kCrcWaves = BCW_CRC_WAVES;  // waves per k_crc workgroup (one workgroup per CU)
 constexpr int kCrcThreads = kCrcWaves * 64;
+#ifndef BCW_SCAN_WAVES
+#define BCW_SCAN_WAVES 12
+#endif
+constexpr int kScanWaves = BCW_SCAN_WAVES;  // waves per k_scan workgroup (one workgroup per CU; 170 VGPRs at 12)
+constexpr int kScanThreads = kScanWaves * 64;
+constexpr uint32_t kScanMaxBlocks = 64u * kScanWaves;  // k_scan: blocks per workgroup at most (one chaser lane each)
 
 struct Scratch {
   uint64_t nblocks_cap = 0;
@@ -72,11 +78,14 @@ struct Scratch {
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
   uint32_t* equeue = nullptr;  // [8 x 32] k_crc emission work-queue heads, one 128 B line per XCD
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
+  uint64_t* lbw = nullptr;     // [nlb] k_scan: per-workgroup "written" words (zeroed at allocation)
+  uint32_t* pwin = nullptr;    // [nblocks * 256 + 4] k_scan: per-window prefixes (window m at m - start_off / 128)
+  uint32_t scan = 0;           // BCW_OPT_DECODE_PATH: 1 = one launch (k_scan) when the segment fits, 0 = k_chase + k_crc
 };
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
 // stream around every kernel of the pipeline.
-enum KernelId { K_CHASE = 0, K_CRC, K_RECORDS, K_ENC_PREP, K_ENC_SCAN, K_ENC_EVENTS, K_ENC_WRITE, K_ENC_HINT_LAYOUT,
+enum KernelId { K_CHASE = 0, K_CRC, K_SCAN, K_ENC_PREP, K_ENC_SCAN, K_ENC_EVENTS, K_ENC_WRITE, K_ENC_HINT_LAYOUT,
                 K_ENC_EVENTS_HINT, K_NUM };
 struct Prof {
   uint32_t mask = 0;   // bit k: time kernel id k
@@ -218,6 +227,7 @@ struct bcw_ctx {
   bcw_index_result* d_ires = nullptr;  // sync index calls
   uint32_t last_start_off = 0;
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // BCW_OPT_CHASE_DIRECT
+  uint32_t scan = 0;                             // BCW_OPT_DECODE_PATH
   uint64_t last_nfrag_cap = 0;
   bcw::Prof prof;
 };

@@ -189,8 +189,13 @@ const char* bcw_kernel_name(int kernel_id);
  *   BCW_OPT_CHASE_DIRECT  k_chase workgroups (64 blocks = 2 MiB each) up to which every workgroup sums all of its
  *                         predecessors' fragment counts directly; larger segments use the decoupled look-back.
  *                         0..BCW_CHASE_DIRECT_MAX (default BCW_CHASE_DIRECT_MAX); 0 forces the look-back at
- *                         every size (the tests drive that branch on small segments with it). */
+ *                         every size (the tests drive that branch on small segments with it; with
+ *                         BCW_OPT_DECODE_PATH 1, since only k_chase has it).
+ *   BCW_OPT_DECODE_PATH   0 (default): a segment of at most 1024 blocks per CU (8 GiB on 256 CUs) decodes in one
+ *                         launch (k_scan), larger ones in two (k_chase + k_crc); 1: always the two launches.
+ *                         Both give identical tables and results. */
 #define BCW_OPT_CHASE_DIRECT 1
+#define BCW_OPT_DECODE_PATH 2
 #define BCW_CHASE_DIRECT_MAX 1024
 int bcw_ctx_set_option(bcw_ctx* ctx, int option, uint64_t value);
 /* Size the context's fragment scratch for at least n fragments on the next decode (after a decode

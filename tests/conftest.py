@@ -24,7 +24,39 @@ def gpu_available() -> bool:
 def ctx():
     if not gpu_available():
         pytest.fail("GPU test selected but no HIP device is visible")
-    from bitcaskdb_amd import Context
+    from bitcaskdb_amd import Context, _lib
     c = Context(0)
+    if os.environ.get("BCW_TEST_DECODE_PATH"):  # bring-up: pin the default context's decode path
+        c.set_option(_lib.OPT_DECODE_PATH, int(os.environ["BCW_TEST_DECODE_PATH"]))
     yield c
     c.close()
+
+
+@pytest.fixture(scope="session")
+def ctx_two():
+    """a context pinned to the two-launch decode (k_chase + k_crc; BCW_OPT_DECODE_PATH 1)"""
+    if not gpu_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    from bitcaskdb_amd import Context, _lib
+    c = Context(0)
+    c.set_option(_lib.OPT_DECODE_PATH, 1)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="session")
+def ctx_scan():
+    """a context pinned to the one-launch decode (k_scan; BCW_OPT_DECODE_PATH 0)"""
+    if not gpu_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    from bitcaskdb_amd import Context, _lib
+    c = Context(0)
+    c.set_option(_lib.OPT_DECODE_PATH, 0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(params=["scan", "two"])
+def ctx_path(request, ctx_scan, ctx_two):
+    """both decode paths: the one-launch k_scan and k_chase + k_crc"""
+    return ctx_scan if request.param == "scan" else ctx_two

@@ -1,6 +1,7 @@
 """GPU decode parity: libbcw.so on the MI355X against the CPU oracle, bit-exact.
 
-Every comparison goes through the C-ABI (bcw_decode_segment / bcw_decode_fragments) on cuda:0."""
+Every comparison goes through the C-ABI (bcw_decode_segment / bcw_decode_fragments) on cuda:0; the ctx_path tests
+run both decode paths (the one-launch k_scan and k_chase + k_crc)."""
 from __future__ import annotations
 
 import random
@@ -59,9 +60,9 @@ def assert_parity(ctx, data, p, name=""):
 
 
 @pytest.mark.parametrize("name", list(cases.ALL))
-def test_cases(ctx, name):
+def test_cases(ctx_path, name):
     data, p = cases.ALL[name]()
-    assert_parity(ctx, data, p, name)
+    assert_parity(ctx_path, data, p, name)
 
 
 def test_synth_config_a_fragment(ctx):
@@ -71,37 +72,37 @@ def test_synth_config_a_fragment(ctx):
     assert got.result.err_class == 0 and (got.table["status"] == 0).all()
 
 
-def test_synth_zipf(ctx):
+def test_synth_zipf(ctx_path):
     data = O.synth(24 << 20, 0, 42, value_mode=1)
-    assert_parity(ctx, data, cases.params(), "zipf24m")
+    assert_parity(ctx_path, data, cases.params(), "zipf24m")
 
 
 @pytest.mark.parametrize("seed", range(12))
-def test_corruption_fuzz(ctx, seed):
+def test_corruption_fuzz(ctx_path, seed):
     """random bit flips: same first failing fragment, error class and delivered records."""
     rng = random.Random(seed)
     base, p = cases.case_zipf(120, seed) if seed % 2 else cases.case_config_shape(120, 2000)
     data = cases.corrupt(base, rng, nflips=1 + seed % 3)
-    assert_parity(ctx, data, p, f"fuzz{seed}")
+    assert_parity(ctx_path, data, p, f"fuzz{seed}")
 
 
 @pytest.mark.parametrize("cut", [0, 1, 6, 7, 39, 40, 41, 47, 48, 100, 32807, 32808, 32809])
-def test_truncations(ctx, cut):
+def test_truncations(ctx_path, cut):
     data, p = cases.case_config_shape(20, 3000)
-    assert_parity(ctx, data[:cut] if cut < len(data) else data, p, f"cut{cut}")
+    assert_parity(ctx_path, data[:cut] if cut < len(data) else data, p, f"cut{cut}")
 
 
-def test_empty_and_small(ctx):
+def test_empty_and_small(ctx_path):
     for data in (b"", bytes(40), bytes(46), bytes(47)):
-        assert_parity(ctx, data, cases.params(), f"small{len(data)}")
+        assert_parity(ctx_path, data, cases.params(), f"small{len(data)}")
 
 
 @pytest.mark.parametrize("vlen,mib,mode", [(10, 24, 0), (0, 24, 0), (300, 16, 0)])
-def test_dense_fragments_at_scale(ctx, vlen, mib, mode):
+def test_dense_fragments_at_scale(ctx_path, vlen, mib, mode):
     """~230 fragments per block (hint-WAL density) over many workgroups: exercises the fragment-table
     retry (first capacity guess too small) and the multi-window ring of k_crc at full occupancy."""
     seg = O.synth(mib << 20, 0, 11 + vlen, 20, 100, vlen, 0)
-    assert_parity(ctx, seg, cases.params(), f"dense vlen={vlen}")
+    assert_parity(ctx_path, seg, cases.params(), f"dense vlen={vlen}")
 
 
 def test_hint_wal_at_scale(ctx):

@@ -130,9 +130,11 @@ def test_config_e_compaction_200k(ctx):
 
 @pytest.fixture
 def lookback_ctx():
-    """a context whose k_chase takes the decoupled look-back at every size (BCW_OPT_CHASE_DIRECT 0)"""
+    """a context on the two-launch path whose k_chase takes the decoupled look-back at every size
+    (BCW_OPT_DECODE_PATH 1, BCW_OPT_CHASE_DIRECT 0)"""
     from bitcaskdb_amd import Context
     c = Context(0)
+    c.set_option(L.OPT_DECODE_PATH, 1)
     c.set_option(L.OPT_CHASE_DIRECT, 0)
     yield c
     c.close()
@@ -198,3 +200,20 @@ def test_config_e_compaction_2m_rebase(ctx):
     assert bad.size == 0, f"dst WAL differs from byte {bad[:1]}"
     assert hb == ref_hint, "hint WAL differs"
     np.testing.assert_array_equal(goffs[:n], offs[:n])
+
+
+def test_config_b_two_launch(ctx_two, config_b):
+    """config B on the two-launch path (k_chase + k_crc, BCW_OPT_DECODE_PATH 1): every column equals the
+    oracle's, as on the default one-launch k_scan."""
+    got, _ = full_parity(ctx_two, config_b, cases.params(), "B two-launch")
+    assert got.result.err_class == 0 and got.n_records > 250000
+
+
+@pytest.mark.parametrize("where", [0.0001, 0.5])
+def test_config_c_corruption(ctx, where):
+    """config C with a flipped byte near the start (workgroup 0) and in the middle: k_scan's edge windows and
+    per-window prefixes decide the same first failing fragment as the oracle."""
+    data = bytearray(O.synth(1 << 30, 0, 42, value_mode=1))
+    data[int(len(data) * where)] ^= 0x24
+    got, ref = full_parity(ctx, bytes(data), cases.params(), f"C flip@{where}")
+    assert got.result.err_class in (L.ERR_CRC, L.ERR_TYPE)

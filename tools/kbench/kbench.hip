@@ -320,6 +320,68 @@ int main(int argc, char** argv) {
       default: return run(k_crc<0>, cus, ea);
     }
   };
+  if (argc > 4 && std::string(argv[3]) == "scan") {  // k_scan variants (one-launch decode), interleaved
+    EmitArgs ea_s = ea;
+    CK(hipMalloc(&ea_s.kb_stamps, 8 * 8 * (size_t)ctx->num_cus * kScanWaves));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nblocks, (uint64_t)cus);
+    auto run_scan = [&](auto kern, const EmitArgs& a) {
+      return timeit([&] {
+        kern<<<grid, kScanThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags, s.frag_cap, s.pwin,
+                                            s.lb, s.lbe, s.lbw, s.tickets, s.epoch, ctx->tabs, a, 0u, 0ull, dres);
+        s.tickets += grid;
+        if ((++s.epoch & 0xffffffull) == 0) {
+          hipMemsetAsync(s.lb, 0, s.nlb * 8, st); hipMemsetAsync(s.lbe, 0, s.nlb * 8, st);
+          hipMemsetAsync(s.lbw, 0, s.nlb * 8, st); s.epoch = 1;
+        }
+      }, reps, st);
+    };
+    auto scan_report = [&]() {  // phase ends per wave (us after the first wave's entry)
+      const int nw = (int)grid * kScanWaves;
+      std::vector<uint64_t> q(8 * (size_t)nw);
+      CK(hipMemcpy(q.data(), ea_s.kb_stamps, q.size() * 8, hipMemcpyDeviceToHost));
+      uint64_t t0 = ~0ull;
+      for (int w = 0; w < nw; ++w) t0 = std::min(t0, q[8 * w]);
+      const char* nm[7] = {"entry", "tables", "chased", "units", "barrier", "verify", "emit"};
+      for (int k = 0; k < 7; ++k) {
+        std::vector<double> v(nw);
+        for (int w = 0; w < nw; ++w) v[w] = (q[8 * w + k] - t0) / 100.0;
+        std::sort(v.begin(), v.end());
+        printf("  %-8s p0 %6.1f p10 %6.1f p50 %6.1f p90 %6.1f max %6.1f us\n", nm[k], v[0], v[nw / 10], v[nw / 2],
+               v[nw * 9 / 10], v[nw - 1]);
+      }
+      std::vector<double> ch;  // chasers only (wave 0 of each workgroup)
+      for (int w = 0; w < nw; w += kScanWaves) ch.push_back((q[8 * w + 2] - t0) / 100.0);
+      std::sort(ch.begin(), ch.end());
+      printf("  chaser wave 0 written: p10 %.1f p50 %.1f p90 %.1f max %.1f us\n", ch[ch.size() / 10],
+             ch[ch.size() / 2], ch[ch.size() * 9 / 10], ch.back());
+    };
+    auto runs = [&](int v) -> float {
+      switch (v) {
+        case 1: return run_scan(k_scan<1>, ea);
+        case 2: return run_scan(k_scan<2>, ea);
+        case 4: return run_scan(k_scan<4>, ea);
+        case 8: return run_scan(k_scan<8>, ea);
+        case 10: return run_scan(k_scan<10>, ea);
+        case 14: return run_scan(k_scan<14>, ea);
+        case 42: return run_scan(k_scan<42>, ea);
+        case 74: return run_scan(k_scan<74>, ea);
+        case 106: return run_scan(k_scan<106>, ea);
+        case 11: return run_scan(k_scan<11>, ea);
+        case 43: return run_scan(k_scan<43>, ea);
+        case 512: { const float r = run_scan(k_scan<512>, ea_s); scan_report(); return r; }
+        default: return run_scan(k_scan<0>, ea);
+      }
+    };
+    const int nv = argc - 4;
+    std::vector<std::vector<float>> ts(nv);
+    for (int r = 0; r < 5; ++r)
+      for (int i = 0; i < nv; ++i) ts[i].push_back(runs(atoi(argv[4 + i])));
+    for (int i = 0; i < nv; ++i) {
+      std::sort(ts[i].begin(), ts[i].end());
+      printf("k_scan<%s>: min %.4f  median %.4f  max %.4f ms\n", argv[4 + i], ts[i][0], ts[i][2], ts[i][4]);
+    }
+    return 0;
+  }
   if (argc > 4 && std::string(argv[3]) == "cmp") {  // k_crc variants interleaved in one process (same buffers)
     const int nv = argc - 4;
     std::vector<std::vector<float>> ts(nv);
