@@ -410,7 +410,8 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
             hipMalloc(&s.bsum, (nb + 1) * sizeof(uint2)) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
             hipMalloc(&s.lbe, nwg * 8) == hipSuccess && hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
             hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess && hipMalloc(&s.equeue, 8 * 128) == hipSuccess &&
-            hipMalloc(&s.lbw, nwg * 8) == hipSuccess && hipMalloc(&s.pwin, (nb * 256 + 4) * 4) == hipSuccess;
+            hipMalloc(&s.lbw, nwg * 8) == hipSuccess &&
+            hipMalloc(&s.pwin, (uint64_t)c->num_cus * scan_unit_stride(nb, (uint64_t)c->num_cus) * 256) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;
   s.frag_cap = fc;

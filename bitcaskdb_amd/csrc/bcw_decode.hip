@@ -24,6 +24,7 @@ enum { M_FIRST_BAD = 0,  // first record whose parse fails (atomicMin in k_crc's
        M_NE = 1,         // Full/Last fragments of the whole segment (k_chase)
        M_NFRAGS = 4, M_DONE_CRC = 5,
        M_T_CRC0 = 10, M_T_FIN = 11,  // wall_clock64 stamps (diagnostics)
+       M_ABORT = 12,     // k_scan: the wait site that timed out (0: none); reported as BCW_ERR_INTERNAL
        M_TICKET = 13,    // k_chase workgroup tickets (monotonic across launches)
        M_BAD_CRC = 14,   // first fragment failing its CRC (atomicMin in k_crc; reset by k_chase)
        M_BAD_TYPE = 15 };  // first fragment of an unknown type (atomicMin in k_chase; reset by k_crc's finalize)
@@ -678,6 +679,24 @@ struct EmitState {
 __device__ __forceinline__ uint2 emit_prefetch(const EmitArgs& A, uint64_t b0, uint32_t lane) {
   return b0 > lane ? A.bsum[b0 - 1 - lane] : make_uint2(0xffff0000u, kSumHasE);
 }
+// A bounded wait (k_scan): every spin of the one-launch decode gives up after 200 ms (a correct wait lasts microseconds)
+// or once another wave has given up, records its site in misc[M_ABORT] and lets the kernel run to its end; the decode
+// then reports BCW_ERR_INTERNAL instead of hanging the device.
+struct Spin {
+  uint64_t t0 = 0;
+  __device__ __forceinline__ bool go(uint64_t* misc, uint32_t site) {  // true: keep waiting
+    const uint64_t t = wall_clock64();
+    if (t0 == 0) t0 = t;
+    if (t - t0 < 20000000ull &&
+        __hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull) {
+      __builtin_amdgcn_s_sleep(1);
+      return true;
+    }
+    atomicMax(reinterpret_cast<unsigned long long*>(&misc[M_ABORT]), (unsigned long long)site);
+    return false;
+  }
+};
+
 // k_scan: the block summaries, fragment table and block bases of an earlier workgroup's blocks (blocks < B0) were
 // written inside the same launch by another CU. A wave reads them only after every predecessor has published its
 // "written" word (behind an agent release) and the wave has run an agent acquire (MI355X_MICROARCH.md,
@@ -687,13 +706,15 @@ struct PredSync {
   uint64_t B0 = 0;
   const uint64_t* lbw = nullptr;  // per-workgroup "written" words (epoch << 40 | 1)
   uint64_t wg = 0, epoch = 0;
+  uint64_t* misc = nullptr;  // k_scan: bounded waits (Spin)
   bool acq = true;
   __device__ __forceinline__ void acquire(uint32_t lane) {
     for (uint64_t q0 = 0; q0 < wg; q0 += 64) {
       const uint64_t q = q0 + lane;
+      Spin sp;
       if (q < wg)
         while ((__hip_atomic_load(&lbw[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 40) != epoch)
-          __builtin_amdgcn_s_sleep(1);
+          if (!sp.go(misc, 8)) break;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -958,6 +979,10 @@ __device__ __forceinline__ void finalize(const EmitArgs& A, uint64_t nblocks, ui
   // a last block of 1..6 bytes makes the reference iterator panic after every earlier record
   // (wal_iterator.go:62-76 re-slices a header from its stale buffer, then buf[7:7+negative])
   if (r.err_class == BCW_ERR_NONE && tail_panic) r.err_class = BCW_ERR_PANIC;
+  if (__hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) {
+    r.err_class = BCW_ERR_INTERNAL;
+    r.err_frag = __hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the wait site
+  }
   r.err_file_off = 0;
   if (err != ~0ull && err < frag_cap) {
     const Frag f = A.frags[err];
@@ -973,6 +998,7 @@ __device__ __forceinline__ void finalize(const EmitArgs& A, uint64_t nblocks, ui
   misc[M_BAD_CRC] = ~0ull;
   misc[M_FIRST_BAD] = ~0ull;
   misc[M_BAD_TYPE] = ~0ull;
+  misc[M_ABORT] = 0;
 }
 
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no CRC chain, 2 no window loads,
@@ -1375,6 +1401,45 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
 //           predecessors' writes first (PredSync).
 constexpr int kScanHoldWords = kCrcWaves * kWaveLds;  // the chasers' held headers (48 KiB, k_crc's ring space)
 
+// Quad-coalesced unit loads: load g (g = 4 p2 + 2 w1 + w0) gives the 4 lanes of quad a the 16 B pieces 4 p2 .. 4 p2 + 3
+// of window 4a + (g & 3) -- 64 contiguous bytes per quad, 1 KiB per instruction in 16 runs, instead of one 16 B piece
+// of 64 different lines (the texture addresser's tag lookups per instruction drop 4x). Two lane-bit <-> register-bit
+// exchanges (DPP quad_perm) then leave piece p of window W in w[4p..4p+3] of lane W (kbench: loads + chain of a
+// 1 GiB segment at 12 waves 186 us, lane-per-window 210 us). k_scan's units are contiguous 8 KiB, so they can.
+__device__ __forceinline__ void load_unit_quad(const uint8_t* __restrict__ base, uint32_t lane, uint32_t (&w)[32]) {
+  const uint32_t qb = 16u * (lane & 3u) + 512u * (lane >> 2);  // quad a's 512 B, this lane's 16 B column
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + qb + 128u * (g & 3) + 64u * (g >> 2));
+    w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+  }
+}
+template <int K>
+__device__ __forceinline__ void swap_lane_reg_bit(uint32_t (&w)[32], uint32_t lane) {
+  constexpr int CTRL = K == 0 ? 0xB1 : 0x4E;  // quad_perm partner lane ^ 1 / lane ^ 2
+  const bool hi = (lane >> K) & 1u;
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    if (x & (1 << K)) continue;
+    const int y = x | (1 << K);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t rx = w[4 * x + d], ry = w[4 * y + d];
+      const uint32_t px = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rx, CTRL, 0xf, 0xf, true);
+      const uint32_t py = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ry, CTRL, 0xf, 0xf, true);
+      w[4 * x + d] = hi ? py : rx;
+      w[4 * y + d] = hi ? ry : px;
+    }
+  }
+}
+// after load_unit_quad: register group g = 4 p2 + 2 w1 + w0 of lane 4a + l holds piece 4 p2 + l of window 4a + 2 w1 + w0;
+// exchanging lane bit 0 with register bit 0 and lane bit 1 with register bit 1 leaves piece 4 p2 + 2 w1' + w0' of
+// window 4a + l in group g of lane 4a + l, i.e. the lane's own window in order
+__device__ __forceinline__ void unit_quad_transpose(uint32_t (&w)[32], uint32_t lane) {
+  swap_lane_reg_bit<0>(w, lane);
+  swap_lane_reg_bit<1>(w, lane);
+}
+
 // window bytes of a fragment for its zero test: data outside [gs, ge) zeroed, J at [ge, ge + 4) (window-relative,
 // any values). Per word: a kept-byte mask and the J bytes that land in it.
 __device__ __forceinline__ void mask_frag_window(uint32_t (&w)[32], int gs, int ge, uint32_t J) {
@@ -1413,7 +1478,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
                                                       uint32_t start_off, uint64_t nblocks, uint32_t* __restrict__ fbase,
                                                       uint32_t* __restrict__ rbase, uint2* __restrict__ bsum,
                                                       Frag* __restrict__ frags, uint64_t frag_cap,
-                                                      uint32_t* __restrict__ pwin,
+                                                      uint32_t* __restrict__ pwin, uint32_t ustride,
                                                       uint64_t* __restrict__ lb, uint64_t* __restrict__ lbe,
                                                       uint64_t* __restrict__ lbw, uint64_t ticket_base, uint64_t epoch,
                                                       Tables tabs, EmitArgs ea, uint32_t tail_panic, uint64_t gen,
@@ -1425,6 +1490,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
   __shared__ uint64_t s_wg;
   __shared__ uint32_t s_udone[(kScanMaxBlocks * (kBlock / 8192) + 2 + 31) / 32];  // window units done (bit per unit)
   __shared__ uint64_t s_em[4];  // emission items: B0, B1, blocks per item, the workgroup's fragment end
+  constexpr uint32_t kVItems = 256;  // verify items whose unit range the chasers record (later ones: from descriptors)
+  __shared__ uint32_t s_vlo[kVItems], s_vhi[kVItems];  // first / last window unit a verify item's interiors need
+  // prefix rows on their way to HBM: the streaming waves put a unit's 64 prefixes here and the writer wave stores them
+  // (vmcnt retires in order per wave, so a streaming wave's own store would hold up the waits for its later loads
+  // until the store is acknowledged -- slow under a read-saturated load: 35-50 us of a config-B decode, kbench)
+  constexpr uint32_t kRing = 32;
+  __shared__ uint32_t s_ring[kRing * 64];
+  __shared__ uint32_t s_rstate[kRing];  // 0: free, else the unit + 1 whose row the slot holds
+  constexpr uint32_t kWDepth = 48;  // the writer's stores in flight (vmcnt(47) below)
+  __shared__ uint32_t s_rhead, s_wunit[kWDepth];
   uint32_t* s_slice = lds;
   uint32_t* s_fwd = lds + kLdsSlice;
   uint32_t* s_carry = s_fwd + kLdsFwd;  // A_{8*8192}: one unit
@@ -1442,6 +1517,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
     s_chn = s_chw = s_ready = s_unit = s_vq = s_eq = s_wdone = 0;
   }
   for (uint32_t i = tid; i < sizeof(s_udone) / 4; i += kScanThreads) s_udone[i] = 0u;
+  for (uint32_t i = tid; i < kVItems; i += kScanThreads) { s_vlo[i] = 0xffffffffu; s_vhi[i] = 0u; }
+  for (uint32_t i = tid; i < kRing; i += kScanThreads) s_rstate[i] = 0u;
+  if (tid == 0) s_rhead = 0u;
   {  // table image -> LDS: all 16 B loads in flight before the first store
     constexpr uint32_t kVec = kLdsImage / 4;
     constexpr int kFull = (int)(kVec / kScanThreads);
@@ -1474,7 +1552,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
   if (m1 > mseg) m1 = mseg;
   if (m1 < m0) m1 = m0;
   const uint32_t nunits = (uint32_t)((m1 - m0 + 63) / 64);
-  const uint64_t mb = start_off / kWin;  // pwin[m - mb] holds window m's prefix
+  // the workgroup's prefix rows: unit u's 64 prefixes are one aligned 256 B row at pw + 64 u (rows indexed from the
+  // workgroup's first window, not by absolute window: a row straddling 128 B lines made every store a partial-line
+  // write, ~35 us of a config-B decode)
+  uint32_t* const pw = pwin + (uint64_t)wg * ustride * 64u;
   const SliceLane sl = slice_lane(lane);
 
   // ---- chase (waves 0..nch-1): k_chase's per-block walk, one block per lane ----
@@ -1489,7 +1570,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
       bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
     }
     uint32_t ne = 0, tacc = 0, tnz = 0xffffu, tst = 0, badk = 0xffffffffu;
-    const uint32_t n = chase_block(seg, seg_len, boff, bufsize,
+    const uint32_t n = chase_block(seg, seg_len, boff, (ABL & 4096) ? 0u : bufsize,
                                    [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
                                      if (k < H) {
                                        uint32_t* e = s_hold + (k * NL + L) * 3u;
@@ -1529,10 +1610,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
         const uint64_t q = q0 + lane;
         if (q < wg) {
           uint64_t v, ve;
+          Spin sp;
           while (((v = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
-            __builtin_amdgcn_s_sleep(1);
+            if (!sp.go(misc, 1)) break;
           while (((ve = __hip_atomic_load(&lbe[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
-            __builtin_amdgcn_s_sleep(1);
+            if (!sp.go(misc, 2)) break;
           c += v & kLbMask;
           ce += ve & kLbMask;
         }
@@ -1551,8 +1633,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
         __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
-    while (__hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-      __builtin_amdgcn_s_sleep(2);
+    {
+      Spin sp;
+      while (__hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        if (!sp.go(misc, 3)) break;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     uint64_t wpre = 0, wpre_e = 0;
     for (uint32_t c = 0; c < wave; ++c) { wpre += s_ctot[c]; wpre_e += s_etot[c]; }
@@ -1564,14 +1649,30 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
       bsum[b] = make_uint2(tacc | (tnz << 16), tst | (ne ? kSumHasE : 0u));
       if (badk != 0xffffffffu)  // the first unknown-type fragment of the segment (reset by the previous finalize)
         atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_TYPE]), (unsigned long long)(g0 + badk));
+      // the window units a verify item's interior windows lie in (min over its fragments, max over them), for the
+      // verify items taken between units (each item: 64 consecutive fragments of the workgroup)
+      const uint64_t Fw = s_base[0];
+      auto vrange = [&](uint64_t g, uint32_t start, uint32_t len) {
+        const int64_t GS = (int64_t)boff + start, GE = GS + len;
+        const int64_t a = GS >> 7, j0 = GE >> 7;
+        if (j0 - 1 <= a) return;
+        const uint64_t it = (g - Fw) / 64;
+        if (it >= kVItems) return;
+        atomicMin(&s_vlo[it], (uint32_t)((a + 1 - (int64_t)m0) >> 6));
+        atomicMax(&s_vhi[it], (uint32_t)((j0 - 1 - (int64_t)m0) >> 6));
+      };
       const uint32_t nh = n < H ? n : H;
       for (uint32_t k = 0; k < nh; ++k) {
         const uint32_t* e = s_hold + (k * NL + L) * 3u;
         put_frag(frags, g0 + k, frag_cap, (uint32_t)b, e[1] & 0xffffu, e[1] >> 16, e[0], e[2], tabs.initc);
+        vrange(g0 + k, e[1] & 0xffffu, e[1] >> 16);
       }
       if (n > H)  // the tail of a block with more headers than held
         chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
-          if (k >= H) put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, tabs.initc);
+          if (k >= H) {
+            put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, tabs.initc);
+            vrange(g0 + k, start, len);
+          }
         });
     }
     if (wg == G - 1u && wave == 0u && lane == 0u) {  // the segment totals
@@ -1599,17 +1700,69 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
 
   // the chasers' writes are visible to this workgroup's waves (they wait for it before verify and emission)
   auto wait_chase = [&]() {
-    while (__hip_atomic_load(&s_chw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < nch) __builtin_amdgcn_s_sleep(2);
+    Spin sp;
+    while (__hip_atomic_load(&s_chw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < nch)
+      if (!sp.go(misc, 4)) break;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
-  auto mark_done = [&](uint32_t u) {  // unit u's prefixes are stored (the caller waited for its store)
-    if (u < nunits && lane == 0) atomicOr(&s_udone[u >> 5], 1u << (u & 31u));
-  };
   const bool chaser = wave < nch;
-  // A chaser wave, its fragment table written, emits records (a latency-bound chain: it needs no CRC result) while
-  // the other waves stream the window units; then every wave: units, verify items, the emission items left.
-  for (int ph = chaser ? 0 : 1; ph < 2; ++ph) {
-    if (ph == 1) {
+  const int64_t M0 = (int64_t)m0;
+  auto frag_range = [&](uint64_t& fa, uint64_t& fb) {  // the workgroup's fragments (after wait_chase)
+    const uint64_t F0 = s_base[0], NF = s_base[2];
+    fa = F0 < frag_cap ? F0 : frag_cap;
+    fb = F0 + NF < frag_cap ? F0 + NF : frag_cap;
+  };
+  auto units_done = [&](uint32_t mn, uint32_t mx) -> bool {  // every unit in [mn, mx] stored (wave-uniform)
+    if (mn > mx) return true;
+    for (uint32_t wd = mn >> 5; wd <= (mx >> 5); ++wd) {
+      const uint32_t blo = wd == (mn >> 5) ? (mn & 31u) : 0u, bhi = wd == (mx >> 5) ? (mx & 31u) : 31u;
+      const uint32_t need = (uint32_t)((2ull << bhi) - 1ull) & ~((1u << blo) - 1u);
+      if ((__hip_atomic_load(&s_udone[wd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & need) != need)
+        return false;
+    }
+    return true;
+  };
+  // Steps of a wave. A chaser, its fragment table written: record emission (a latency-bound chain that needs no CRC
+  // result), then verify items as the window units they need get stored -- it trails the unit frontier, so little
+  // verify work is left when the streaming ends. Every other wave: window units, then the verify and emission
+  // items left.
+  enum { ST_UNITS = 0, ST_VERIFY = 1, ST_EMIT = 2, ST_WRITE = 3 };
+  const bool writer = wave == kScanWaves - 1;  // never a chaser (kScanMaxBlocks)
+  const int nsteps = chaser ? 2 : 3;
+  for (int st = 0; st < nsteps; ++st) {
+    const int kind = chaser ? (st == 0 ? ST_EMIT : ST_VERIFY)
+                            : (st == 0 ? (writer ? ST_WRITE : ST_UNITS) : (st == 1 ? ST_VERIFY : ST_EMIT));
+    if (kind == ST_WRITE) {
+      // ---- the writer: every unit's prefix row, ring slot by slot in ticket order, to HBM; a unit is marked done
+      // once its store has retired (8 rows later, or at the end) ----
+      for (uint32_t t = 0; t < nunits; ++t) {
+        const uint32_t slot = t % kRing;
+        uint32_t v;
+        Spin sp;
+        while ((v = __hip_atomic_load(&s_rstate[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0u)
+          if (!sp.go(misc, 6)) { v = 1u; break; }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t u = v - 1u;
+        const uint32_t P = s_ring[slot * 64 + lane];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the row is read before the slot is freed
+        if (lane == 0) __hip_atomic_store(&s_rstate[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // kWDepth stores in flight (write acks take microseconds under this read load: at 8 in flight the writer fell
+        // behind and the ring stalled the streaming waves). The store of row t - kWDepth (slot t % kWDepth, read
+        // before row t takes it over) has retired at vmcnt(kWDepth - 1); its unit is then marked done.
+        if (t >= kWDepth) {
+          asm volatile("s_waitcnt vmcnt(47)" ::: "memory");
+          const uint32_t ud = s_wunit[t % kWDepth];
+          if (lane == 0) atomicOr(&s_udone[ud >> 5], 1u << (ud & 31u));
+        }
+        if (!(ABL & 2048) && m0 + 64ull * u + lane < m1) pw[64ull * u + lane] = P;
+        if (lane == 0) s_wunit[t % kWDepth] = u;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (uint32_t t = nunits > kWDepth ? nunits - kWDepth : 0; t < nunits; ++t) {
+        const uint32_t ud = s_wunit[t % kWDepth];
+        if (lane == 0) atomicOr(&s_udone[ud >> 5], 1u << (ud & 31u));
+      }
+    } else if (kind == ST_UNITS) {
       // ---- windows: units of 64 windows from the LDS counter ----
       const uint8_t* safe_win = seg_len >= kWin ? seg : reinterpret_cast<const uint8_t*>(tabs.lds_image);
       // ABL & 32: static contiguous unit ranges per wave instead of the LDS counter (kbench)
@@ -1625,13 +1778,21 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
       auto fast = [&](uint32_t u) {  // every lane's window is in the segment (and the workgroup's)
         return u < nunits && m0 + 64ull * u + 64 <= m1 && (m0 + 64ull * u + 64) * kWin <= seg_len;
       };
-      // two window buffers: a unit's loads are issued one unit ahead, so they fly through the previous unit's chain
-      // (a single buffer reloaded after the chain left them nothing to overlap but the store: the loop waited ~ a
-      // full load latency per unit). Every lane loads (an invalid unit reads safe_win) so the loads are one
-      // straight-line group, and no load sits in a branch of the loop (the compiler then waits for every load in
-      // flight, both buffers'): the unit that is not "fast" -- the workgroup's partial last unit, or one at the
-      // segment's end -- is set aside and done after the loop with bounds-checked loads.
+      // Two window buffers: a unit's loads are issued one unit ahead, so they fly through the other buffer's chain.
+      // Every lane loads (an invalid unit reads a safe address) so the loads are one straight-line group, and no
+      // load sits in a branch of the loop (the compiler then waits for every load in flight, both buffers'): the
+      // unit that is not "fast" -- the workgroup's partial last unit, or one at the segment's end -- is set aside
+      // and done after the loop with bounds-checked loads.
+      // ABL & 8192 (kbench): lane-per-window loads instead of the quad-coalesced ones
+      // 8 KiB every lane may read: the segment's start, or the table image (97 KiB) for a segment shorter than that
+      // (whose units are then all slow ones)
+      const uint8_t* safe_unit =
+          seg_len >= 64 * kWin ? seg : reinterpret_cast<const uint8_t*>(tabs.lds_image);
       auto issue = [&](uint32_t u, uint32_t (&w)[32]) {
+        if (!(ABL & 8192)) {
+          load_unit_quad(fast(u) ? seg + (m0 + 64ull * u) * kWin : safe_unit, lane, w);
+          return;
+        }
         const uint4* q = reinterpret_cast<const uint4*>(fast(u) ? seg + win_of(u) * kWin : safe_win);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
@@ -1639,68 +1800,80 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
           w[4 * g + 0] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
         }
       };
-      auto finish = [&](uint32_t u, uint32_t (&w)[32], bool valid) {
-        const uint64_t m = win_of(u);
+      uint32_t kb_acc = 0;  // kbench (ABL & 2048): the prefixes folded here instead of stored
+      auto prefix = [&](uint32_t (&w)[32], bool valid) -> uint32_t {
         uint32_t v = (ABL & 1) ? (w[0] ^ w[31]) : crc_window(s_slice, s_half, sl, 0u, w);
         if (!valid) v = 0u;
+        if (ABL & 1024) return v;
         v = apply_fwd(s_fwd, lane, v);
-        const uint32_t P = wave_scan_z(v, [](uint32_t x, uint32_t y) { return x ^ y; });
-        if (valid) pwin[m - mb] = P;
+        return wave_scan_z(v, [](uint32_t x, uint32_t y) { return x ^ y; });
+      };
+      auto store = [&](uint32_t u, uint32_t P, bool valid) {  // the row into the writer's ring (every unit, once)
+        if (ABL & 2048) kb_acc ^= P;
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(&s_rhead, 1u);
+        const uint32_t slot = __builtin_amdgcn_readfirstlane(t) % kRing;
+        Spin sp;
+        while (__hip_atomic_load(&s_rstate[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u)
+          if (!sp.go(misc, 5)) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        s_ring[slot * 64 + lane] = P;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&s_rstate[slot], u + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        (void)valid;
       };
       uint32_t deferred = nunits;  // this wave's slow unit, if it took one
+      // a unit's prefixes, stored right away (fast units); a slow unit is only noted
       auto process = [&](uint32_t u, uint32_t (&w)[32]) {
         if (u < nunits) {
-          if (fast(u)) finish(u, w, true);
-          else deferred = u;
+          if (fast(u)) {
+            if (!(ABL & 8192)) unit_quad_transpose(w, lane);
+            store(u, prefix(w, true), true);
+          } else {
+            deferred = u;
+          }
         }
       };
       uint32_t wa[32], wb[32];
-      uint32_t ua = (ABL & 4) ? nunits : take();
+      // kbench: ABL & 128 -- only waves 2..9 take units
+      const bool no_units = (ABL & 4) || ((ABL & 128) && (wave < 2 || wave > 9));
+      uint32_t ua = no_units ? nunits : take();
       issue(ua, wa);
-      uint32_t ub = (ABL & 4) ? nunits : take();
+      uint32_t ub = no_units ? nunits : take();
       issue(ub, wb);
-      // no exit between the halves (an exit there made the compiler wait for both buffers' loads): ub > ua, so a
-      // half whose unit is past the end only skips its compute. Before each half, every op but the other buffer's
-      // 8 loads has completed -- the previous half's store among them -- so that unit is marked done there.
-      uint32_t prev = nunits;
+      // Per half: process the buffer (its prefixes into the writer's ring), then its next unit's 8 loads; the
+      // compiler waits for the other buffer's loads (vmcnt(8): this half's loads stay in flight).
+      // No exit between the halves (an exit there made the compiler wait for both buffers' loads): ub > ua, so a
+      // half whose unit is past the end only skips its compute.
       while (ua < nunits) {
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        if (prev != deferred) mark_done(prev);
         process(ua, wa);
-        const uint32_t pa = ua;
         ua = take();
         issue(ua, wa);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        if (pa != deferred) mark_done(pa);
         process(ub, wb);
-        prev = ub;
         ub = take();
         issue(ub, wb);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (prev != deferred) mark_done(prev);
       if (deferred < nunits) {
         const uint64_t m = win_of(deferred);
         load_window(seg, seg_len, (int64_t)(m * kWin), false, wa);
-        finish(deferred, wa, m < m1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        mark_done(deferred);
+        store(deferred, prefix(wa, m < m1), m < m1);
       }
+      if ((ABL & 2048) && kb_acc == 0x9e3779b9u) pw[0] = kb_acc;
       stamp(3);
-
-      // ---- verify: one lane per fragment of the workgroup, items of 64 fragments once their units are done ----
+    } else if (kind == ST_VERIFY) {
+      // ---- verify items (one lane per fragment, 64 consecutive fragments of the workgroup), each once its units
+      // are stored ----
       wait_chase();
       stamp(4);
-      const uint64_t F0 = s_base[0], NF = s_base[2];
-      const uint64_t Fa = F0 < frag_cap ? F0 : frag_cap;
-      const uint64_t Fb = F0 + NF < frag_cap ? F0 + NF : frag_cap;
-      const int64_t M0 = (int64_t)m0;
+      uint64_t Fa, Fb;
+      frag_range(Fa, Fb);
       for (; !(ABL & 2);) {
         uint32_t it = 0;
         if (lane == 0) it = atomicAdd(&s_vq, 1u);
         it = __builtin_amdgcn_readfirstlane(it);
-        const uint64_t g = Fa + 64ull * it + lane;
         if (Fa + 64ull * it >= Fb) break;
+        const uint64_t g = Fa + 64ull * it + lane;
         Frag f{};
         if (g < Fb) {
           const uint4 raw = reinterpret_cast<const uint4*>(frags)[g];
@@ -1708,11 +1881,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
         }
         const int64_t GS = (int64_t)start_off + (int64_t)f.blk * kBlock + f.start, GE = GS + f.len;
         const int64_t a = GS >> 7, j0 = GE >> 7, j1 = (GE + 3) >> 7;
-        {  // wait for the units holding the interior windows (a, j0) of the item's fragments
+        uint32_t mn, mx;
+        if (it < kVItems) {
+          mn = s_vlo[it];
+          mx = s_vhi[it];
+        } else {  // from the descriptors
           const bool has = g < Fb && j0 - 1 > a;
-          const uint32_t ulo = has ? (uint32_t)((a + 1 - M0) >> 6) : 0xffffffffu;
-          const uint32_t uhi = has ? (uint32_t)((j0 - 1 - M0) >> 6) : 0u;
-          uint32_t mn = ulo, mx = uhi;
+          mn = has ? (uint32_t)((a + 1 - M0) >> 6) : 0xffffffffu;
+          mx = has ? (uint32_t)((j0 - 1 - M0) >> 6) : 0u;
 #pragma unroll
           for (int d = 32; d >= 1; d >>= 1) {
             mn = min(mn, (uint32_t)__shfl_xor((int)mn, d, 64));
@@ -1720,16 +1896,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
           }
           mn = __builtin_amdgcn_readfirstlane(mn);
           mx = __builtin_amdgcn_readfirstlane(mx);
-          if (mn <= mx) {
-            for (uint32_t wd = mn >> 5; wd <= (mx >> 5); ++wd) {
-              const uint32_t blo = wd == (mn >> 5) ? (mn & 31u) : 0u, bhi = wd == (mx >> 5) ? (mx & 31u) : 31u;
-              const uint32_t need = (uint32_t)((2ull << bhi) - 1ull) & ~((1u << blo) - 1u);
-              while ((__hip_atomic_load(&s_udone[wd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & need) != need)
-                __builtin_amdgcn_s_sleep(1);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          }
         }
+        {
+          Spin sp;
+          while (!units_done(mn, mx))
+            if (!sp.go(misc, 7)) break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (g < Fb) {
           // the edge windows one at a time (one window of registers)
           uint32_t z[3] = {0u, 0u, 0u};
@@ -1743,31 +1916,28 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
             z[1] = e == 1 ? v : z[1];
             z[2] = e == 2 ? v : z[2];
           }
-          const uint32_t za = z[0], zj0 = z[1], zj1 = z[2];
           const int64_t pa = (a - M0) >> 6, pf = (j1 - M0) >> 6;
           uint32_t T = 0;
           for (int64_t p = pa; p <= pf; ++p) {
             if (p > pa) T = apply_op(s_carry, T);
             const int64_t wlo = M0 + 64 * p, whi = wlo + 63;
             const int64_t lo = a + 1 > wlo ? a + 1 : wlo, hi = j0 - 1 < whi ? j0 - 1 : whi;
-            if (lo <= hi) T ^= pwin[hi - (int64_t)mb] ^ (lo > wlo ? pwin[lo - 1 - (int64_t)mb] : 0u);
-            if (((a - M0) >> 6) == p) T ^= apply_fwd(s_fwd, (uint32_t)((a - M0) & 63), za);
-            if (j0 != a && ((j0 - M0) >> 6) == p) T ^= apply_fwd(s_fwd, (uint32_t)((j0 - M0) & 63), zj0);
-            if (j1 != j0 && j1 != a && ((j1 - M0) >> 6) == p) T ^= apply_fwd(s_fwd, (uint32_t)((j1 - M0) & 63), zj1);
+            if (lo <= hi) T ^= pw[hi - M0] ^ (lo > wlo ? pw[lo - 1 - M0] : 0u);
+            if (((a - M0) >> 6) == p) T ^= apply_fwd(s_fwd, (uint32_t)((a - M0) & 63), z[0]);
+            if (j0 != a && ((j0 - M0) >> 6) == p) T ^= apply_fwd(s_fwd, (uint32_t)((j0 - M0) & 63), z[1]);
+            if (j1 != j0 && j1 != a && ((j1 - M0) >> 6) == p) T ^= apply_fwd(s_fwd, (uint32_t)((j1 - M0) & 63), z[2]);
           }
           frags[g].ok = T == 0u ? 1 : 0;
           if (T != 0u) atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_CRC]), (unsigned long long)g);
         }
       }
       stamp(5);
-    }
-
-    // ---- record emission: items of ~64 fragments over the workgroup's blocks (k_crc's emit_chunks) ----
-    if (!(ABL & 8)) {
+    } else if (!(ABL & 8)) {
+      // ---- record emission: items of ~64 fragments over the workgroup's blocks (k_crc's emit_chunks) ----
       wait_chase();
       const uint64_t nitems = (s_em[1] - s_em[0] + s_em[2] - 1) / s_em[2];
       PredSync ps;
-      ps.B0 = B0; ps.lbw = lbw; ps.wg = wg; ps.epoch = epoch; ps.acq = (wg == 0);
+      ps.B0 = B0; ps.lbw = lbw; ps.wg = wg; ps.epoch = epoch; ps.misc = misc; ps.acq = (wg == 0);
       // the item geometry lives in LDS and is re-read per item: the emission runs at the register limit
       auto meta = [&](uint64_t it) -> ItemMeta {
         const uint64_t b0 = s_em[0], b1 = s_em[1], bpw = s_em[2];
@@ -1858,8 +2028,8 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
     const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
     pr.begin(K_SCAN, stream, ev);
     k_scan<0><<<grid, kScanThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum,
-                                                s.frags, s.frag_cap, s.pwin, s.lb, s.lbe, s.lbw, s.tickets, s.epoch,
-                                                tabs, ea, tail_panic, gen, d_result);
+                                                s.frags, s.frag_cap, s.pwin, scan_unit_stride(nblocks, grid), s.lb,
+                                                s.lbe, s.lbw, s.tickets, s.epoch, tabs, ea, tail_panic, gen, d_result);
     pr.end(K_SCAN, stream, ev);
     s.tickets += grid;
     next_epoch();

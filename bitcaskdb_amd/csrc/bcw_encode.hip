@@ -1430,7 +1430,9 @@ __device__ __forceinline__ void copy_run(uint8_t* dst, const uint8_t* src, uint6
       v[q] = make_uint4(0, 0, 0, 0);
       ok[q] = k < nu && sw >= sbeg && sw + 32 <= send;
       if (ok[q]) {
-        const uint4* w = reinterpret_cast<const uint4*>((uintptr_t)sw);
+        // addresses as offsets from the segment / output pointers (not integer-to-pointer casts): the compiler then
+        // knows they are global memory and emits global_ (not flat_) loads and stores
+        const uint4* w = reinterpret_cast<const uint4*>(seg + (sw - sbeg));
         v[q] = shift16(w[0], w[1], (uint32_t)(sa & 15u));
       }
     }
@@ -1439,7 +1441,7 @@ __device__ __forceinline__ void copy_run(uint8_t* dst, const uint8_t* src, uint6
       const uint64_t k = k0 + (uint64_t)q * 64 + lane;
       if (k >= nu) continue;
       const uint64_t ua = (u0 + k) << 4;
-      uint8_t* d = reinterpret_cast<uint8_t*>((uintptr_t)ua);
+      uint8_t* d = dst + (int64_t)(ua - da);
       if (ok[q] && ua >= da && ua + 16 <= de) {
         __builtin_nontemporal_store(v[q].x, reinterpret_cast<uint32_t*>(d));
         __builtin_nontemporal_store(v[q].y, reinterpret_cast<uint32_t*>(d) + 1);
@@ -1450,7 +1452,7 @@ __device__ __forceinline__ void copy_run(uint8_t* dst, const uint8_t* src, uint6
         if (ok[q]) {
           for (uint32_t b = b0; b < b1; ++b) d[b] = (uint8_t)sel_byte(v[q], b);
         } else {  // the source window touches the segment's ends: bytewise
-          for (uint32_t b = b0; b < b1; ++b) d[b] = *reinterpret_cast<const uint8_t*>((uintptr_t)(ua + b + delta));
+          for (uint32_t b = b0; b < b1; ++b) d[b] = seg[(int64_t)(ua + b + delta - sbeg)];
         }
       }
     }

@@ -61,7 +61,12 @@ constexpr int kCrcThreads = kCrcWaves * 64;
 #endif
 constexpr int kScanWaves = BCW_SCAN_WAVES;  // waves per k_scan workgroup (one workgroup per CU; 170 VGPRs at 12)
 constexpr int kScanThreads = kScanWaves * 64;
-constexpr uint32_t kScanMaxBlocks = 64u * kScanWaves;  // k_scan: blocks per workgroup at most (one chaser lane each)
+// k_scan: blocks per workgroup at most (one chaser lane each; the last wave is the prefix writer, never a chaser)
+constexpr uint32_t kScanMaxBlocks = 64u * (kScanWaves - 1);
+// k_scan prefix rows per workgroup (units of 64 windows: 4 per block, +1 for a window straddling the range start)
+inline uint32_t scan_unit_stride(uint64_t nblocks, uint64_t grid) {
+  return (uint32_t)(((nblocks + grid - 1) / grid) * (kBlock / 8192) + 2);
+}
 
 struct Scratch {
   uint64_t nblocks_cap = 0;
@@ -79,7 +84,7 @@ struct Scratch {
   uint32_t* equeue = nullptr;  // [8 x 32] k_crc emission work-queue heads, one 128 B line per XCD
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
   uint64_t* lbw = nullptr;     // [nlb] k_scan: per-workgroup "written" words (zeroed at allocation)
-  uint32_t* pwin = nullptr;    // [nblocks * 256 + 4] k_scan: per-window prefixes (window m at m - start_off / 128)
+  uint32_t* pwin = nullptr;    // k_scan: per-window prefixes, [workgroups][scan_unit_stride][64]
   uint32_t scan = 0;           // BCW_OPT_DECODE_PATH: 1 = one launch (k_scan) when the segment fits, 0 = k_chase + k_crc
 };
 

@@ -68,6 +68,7 @@ extern "C" {
 #define BCW_ERR_CRC 1   /* ErrWalMismatchCRC */
 #define BCW_ERR_TYPE 2  /* ErrWalUnknownRecordType */
 #define BCW_ERR_PANIC 3 /* startOff > file size: the reference panics slicing i.buf[:negative] */
+#define BCW_ERR_INTERNAL 4 /* the one-launch decode gave up on an internal wait (a library bug): no valid result */
 
 /* ---- super block load result (wal.go:362-398) ---- */
 #define BCW_SB_OK 0

@@ -21,7 +21,7 @@ namespace bcw {
 // 4a + (g & 3): 64 contiguous bytes per quad. Two lane-bit <-> register-bit exchanges (DPP
 // quad_perm) then leave piece p of window W in w[4p..4p+3] of lane W.
 template <int K>
-__device__ __forceinline__ void swap_lane_reg_bit(uint32_t (&w)[32], uint32_t lane) {
+__device__ __forceinline__ void kb_swap_lane_reg_bit(uint32_t (&w)[32], uint32_t lane) {
   constexpr int CTRL = K == 0 ? 0xB1 : 0x4E;  // quad_perm partner lane ^ 1 / lane ^ 2
   const bool hi = (lane >> K) & 1u;
 #pragma unroll
@@ -39,8 +39,8 @@ __device__ __forceinline__ void swap_lane_reg_bit(uint32_t (&w)[32], uint32_t la
   }
 }
 __device__ __forceinline__ void quad_windows_transpose(uint32_t (&w)[32], uint32_t lane) {
-  swap_lane_reg_bit<0>(w, lane);
-  swap_lane_reg_bit<1>(w, lane);
+  kb_swap_lane_reg_bit<0>(w, lane);
+  kb_swap_lane_reg_bit<1>(w, lane);
 }
 // loads of the quad layout; woff/act: this lane's window offset (from wbase) and active flag;
 // SAFE: bounds-checked 16 B loads (windows touching the segment's ends)
@@ -327,7 +327,8 @@ int main(int argc, char** argv) {
     auto run_scan = [&](auto kern, const EmitArgs& a) {
       return timeit([&] {
         kern<<<grid, kScanThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags, s.frag_cap, s.pwin,
-                                            s.lb, s.lbe, s.lbw, s.tickets, s.epoch, ctx->tabs, a, 0u, 0ull, dres);
+                                            scan_unit_stride(nblocks, grid), s.lb, s.lbe, s.lbw, s.tickets, s.epoch,
+                                            ctx->tabs, a, 0u, 0ull, dres);
         s.tickets += grid;
         if ((++s.epoch & 0xffffffull) == 0) {
           hipMemsetAsync(s.lb, 0, s.nlb * 8, st); hipMemsetAsync(s.lbe, 0, s.nlb * 8, st);
@@ -364,6 +365,20 @@ int main(int argc, char** argv) {
         case 10: return run_scan(k_scan<10>, ea);
         case 14: return run_scan(k_scan<14>, ea);
         case 42: return run_scan(k_scan<42>, ea);
+        case 138: return run_scan(k_scan<138>, ea);
+        case 1034: return run_scan(k_scan<1034>, ea);
+        case 65536: return run_scan(k_scan<65536>, ea);
+        case 8202: return run_scan(k_scan<8202>, ea);
+        case 16394: return run_scan(k_scan<16394>, ea);
+        case 7211: return run_scan(k_scan<7211>, ea);
+        case 15371: return run_scan(k_scan<15371>, ea);
+        case 2058: return run_scan(k_scan<2058>, ea);
+        case 4106: return run_scan(k_scan<4106>, ea);
+        case 7178: return run_scan(k_scan<7178>, ea);
+        case 7179: return run_scan(k_scan<7179>, ea);
+        case 266: return run_scan(k_scan<266>, ea);
+        case 139: return run_scan(k_scan<139>, ea);
+        case 267: return run_scan(k_scan<267>, ea);
         case 74: return run_scan(k_scan<74>, ea);
         case 106: return run_scan(k_scan<106>, ea);
         case 11: return run_scan(k_scan<11>, ea);
