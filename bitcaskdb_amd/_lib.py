@@ -98,7 +98,7 @@ HEADER_SIZE = 7
 SUPER_BLOCK_SIZE = 40
 MODE_RECORD, MODE_HINT = 0, 1
 ST_OK, ST_INVALID, ST_PANIC, ST_UNSUPPORTED = 0, 1, 2, 3
-ERR_NONE, ERR_CRC, ERR_TYPE, ERR_PANIC = 0, 1, 2, 3
+ERR_NONE, ERR_CRC, ERR_TYPE, ERR_PANIC, ERR_INTERNAL = 0, 1, 2, 3, 4
 SB_OK, SB_SHORT, SB_CRC, SB_MAGIC, SB_BLOCKSIZE = 0, 1, 2, 3, 4
 E_CAPACITY = -4
 OPT_CHASE_DIRECT = 1  # bcw_ctx_set_option: k_chase direct-sum workgroup limit (0 forces the look-back)

@@ -1496,10 +1496,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
   // (vmcnt retires in order per wave, so a streaming wave's own store would hold up the waits for its later loads
   // until the store is acknowledged -- slow under a read-saturated load: 35-50 us of a config-B decode, kbench)
   constexpr uint32_t kRing = 32;
-  __shared__ uint32_t s_ring[kRing * 64];
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[kRing * 64];
   __shared__ uint32_t s_rstate[kRing];  // 0: free, else the unit + 1 whose row the slot holds
-  constexpr uint32_t kWDepth = 48;  // the writer's stores in flight (vmcnt(47) below)
-  __shared__ uint32_t s_rhead, s_wunit[kWDepth];
+  constexpr uint32_t kWDepth = 56;  // each writer's rows in flight (7 batches of 2 stores: vmcnt(12) below)
+  __shared__ uint32_t s_rhead, s_wunit[kScanWriters][kWDepth];
   uint32_t* s_slice = lds;
   uint32_t* s_fwd = lds + kLdsSlice;
   uint32_t* s_carry = s_fwd + kLdsFwd;  // A_{8*8192}: one unit
@@ -1727,41 +1727,77 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
   // verify work is left when the streaming ends. Every other wave: window units, then the verify and emission
   // items left.
   enum { ST_UNITS = 0, ST_VERIFY = 1, ST_EMIT = 2, ST_WRITE = 3 };
-  const bool writer = wave == kScanWaves - 1;  // never a chaser (kScanMaxBlocks)
+  const bool writer = wave >= kScanWaves - kScanWriters;  // never a chaser (kScanMaxBlocks)
+  const uint32_t wid = writer ? wave - (kScanWaves - kScanWriters) : 0u;
   const int nsteps = chaser ? 2 : 3;
   for (int st = 0; st < nsteps; ++st) {
     const int kind = chaser ? (st == 0 ? ST_EMIT : ST_VERIFY)
                             : (st == 0 ? (writer ? ST_WRITE : ST_UNITS) : (st == 1 ? ST_VERIFY : ST_EMIT));
     if (kind == ST_WRITE) {
-      // ---- the writer: every unit's prefix row, ring slot by slot in ticket order, to HBM; a unit is marked done
-      // once its store has retired (8 rows later, or at the end) ----
-      for (uint32_t t = 0; t < nunits; ++t) {
-        const uint32_t slot = t % kRing;
-        uint32_t v;
-        Spin sp;
-        while ((v = __hip_atomic_load(&s_rstate[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0u)
-          if (!sp.go(misc, 6)) { v = 1u; break; }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const uint32_t u = v - 1u;
-        const uint32_t P = s_ring[slot * 64 + lane];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the row is read before the slot is freed
-        if (lane == 0) __hip_atomic_store(&s_rstate[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // kWDepth stores in flight (write acks take microseconds under this read load: at 8 in flight the writer fell
-        // behind and the ring stalled the streaming waves). The store of row t - kWDepth (slot t % kWDepth, read
-        // before row t takes it over) has retired at vmcnt(kWDepth - 1); its unit is then marked done.
-        if (t >= kWDepth) {
-          asm volatile("s_waitcnt vmcnt(47)" ::: "memory");
-          const uint32_t ud = s_wunit[t % kWDepth];
-          if (lane == 0) atomicOr(&s_udone[ud >> 5], 1u << (ud & 31u));
+      // ---- the writers: the prefix rows to HBM, kWB ring slots (one batch) at a time in ticket order, batches dealt
+      // round-robin to the kScanWriters writer waves. One wave-wide poll and kWB independent row reads per batch (a
+      // row at a time was a chain of LDS round trips); kWDepth stores in flight per writer (write acks take ~25 us
+      // under this read load: one writer with 48 in flight finished ~40 us after the streaming). A unit is marked
+      // done once its store has retired, kWDepth rows later or at the end ----
+      constexpr uint32_t kWB = 8;
+      // (ABL & 65536, kbench: 16 rows in flight per writer; ABL & 512: the writer's wait time in stamp slot 7)
+      constexpr uint32_t kD = (ABL & 65536) ? 16u : kWDepth;
+      uint64_t kb_wait = 0;
+      uint32_t nrow = 0;  // rows this writer has issued
+      for (uint32_t t = wid * kWB; t < nunits; t += kScanWriters * kWB) {
+        const uint32_t nb = nunits - t < kWB ? nunits - t : kWB;
+        {  // every slot of the batch filled (lanes 0..nb-1 poll one slot each)
+          Spin sp;
+          for (;;) {
+            const uint32_t st = lane < nb ? __hip_atomic_load(&s_rstate[(t + lane) % kRing], __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_WORKGROUP)
+                                          : 1u;
+            if (__ballot(st == 0u) == 0ull) break;
+            if (!sp.go(misc, 6)) break;
+          }
         }
-        if (!(ABL & 2048) && m0 + 64ull * u + lane < m1) pw[64ull * u + lane] = P;
-        if (lane == 0) s_wunit[t % kWDepth] = u;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        // lane l carries 16 B of row 4 h + l / 16 (h = 0, 1): two 1 KiB stores per batch instead of eight 256 B ones
+        // (the store instructions themselves slowed the streaming waves' loads by ~20 us, L2-resident or not)
+        uint4 P[2];
+        uint32_t U[kWB], Ul[2];
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+          const uint32_t j = 4u * h + (lane >> 4), slot = (t + j) % kRing;
+          P[h] = *reinterpret_cast<const uint4*>(&s_ring[slot * 64 + 4u * (lane & 15u)]);
+          Ul[h] = j < nb ? s_rstate[slot] - 1u : nunits;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kWB; ++j) U[j] = j < nb ? s_rstate[(t + j) % kRing] - 1u : nunits;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the rows are read before their slots are freed
+        if (lane < nb) __hip_atomic_store(&s_rstate[(t + lane) % kRing], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (nrow >= kD) {  // this writer's rows nrow - kD .. + kWB have retired once kD - kWB remain
+          const uint64_t tw = (ABL & 512) ? wall_clock64() : 0;
+          if (ABL & 65536) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+          if (ABL & 512) kb_wait += wall_clock64() - tw;
+#pragma unroll
+          for (uint32_t j = 0; j < kWB; ++j) {
+            const uint32_t ud = s_wunit[wid][(nrow + j) % kD];
+            if (ud < nunits && lane == 0) atomicOr(&s_udone[ud >> 5], 1u << (ud & 31u));
+          }
+        }
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h)  // (rows are whole 256 B: past m1 they hold don't-care prefixes)
+          if (Ul[h] < nunits && !(ABL & 2048))
+            *reinterpret_cast<uint4*>(pw + 64ull * Ul[h] + 4u * (lane & 15u)) = P[h];
+#pragma unroll
+        for (uint32_t j = 0; j < kWB; ++j)
+          if (lane == 0) s_wunit[wid][(nrow + j) % kD] = U[j];
+        nrow += kWB;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (uint32_t t = nunits > kWDepth ? nunits - kWDepth : 0; t < nunits; ++t) {
-        const uint32_t ud = s_wunit[t % kWDepth];
-        if (lane == 0) atomicOr(&s_udone[ud >> 5], 1u << (ud & 31u));
+      stamp(3);
+      for (uint32_t r = nrow > kD ? nrow - kD : 0; r < nrow; ++r) {
+        const uint32_t ud = s_wunit[wid][r % kD];
+        if (ud < nunits && lane == 0) atomicOr(&s_udone[ud >> 5], 1u << (ud & 31u));
       }
+      if ((ABL & 512) && lane == 0) ea.kb_stamps[((uint64_t)blockIdx.x * kScanWaves + wave) * 8 + 7] = kb_wait;
     } else if (kind == ST_UNITS) {
       // ---- windows: units of 64 windows from the LDS counter ----
       const uint8_t* safe_win = seg_len >= kWin ? seg : reinterpret_cast<const uint8_t*>(tabs.lds_image);
@@ -1801,6 +1837,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
         }
       };
       uint32_t kb_acc = 0;  // kbench (ABL & 2048): the prefixes folded here instead of stored
+      uint64_t kb_ring_waits = 0;  // kbench (ABL & 512): spins on a full ring
       auto prefix = [&](uint32_t (&w)[32], bool valid) -> uint32_t {
         uint32_t v = (ABL & 1) ? (w[0] ^ w[31]) : crc_window(s_slice, s_half, sl, 0u, w);
         if (!valid) v = 0u;
@@ -1814,8 +1851,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
         if (lane == 0) t = atomicAdd(&s_rhead, 1u);
         const uint32_t slot = __builtin_amdgcn_readfirstlane(t) % kRing;
         Spin sp;
-        while (__hip_atomic_load(&s_rstate[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u)
+        while (__hip_atomic_load(&s_rstate[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) {
+          if (ABL & 512) ++kb_ring_waits;
           if (!sp.go(misc, 5)) break;
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         s_ring[slot * 64 + lane] = P;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1861,6 +1900,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
       }
       if ((ABL & 2048) && kb_acc == 0x9e3779b9u) pw[0] = kb_acc;
       stamp(3);
+      if ((ABL & 512) && lane == 0) ea.kb_stamps[((uint64_t)blockIdx.x * kScanWaves + wave) * 8 + 7] = kb_ring_waits;
     } else if (kind == ST_VERIFY) {
       // ---- verify items (one lane per fragment, 64 consecutive fragments of the workgroup), each once its units
       // are stored ----

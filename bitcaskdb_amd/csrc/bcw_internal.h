@@ -61,8 +61,10 @@ constexpr int kCrcThreads = kCrcWaves * 64;
 #endif
 constexpr int kScanWaves = BCW_SCAN_WAVES;  // waves per k_scan workgroup (one workgroup per CU; 170 VGPRs at 12)
 constexpr int kScanThreads = kScanWaves * 64;
-// k_scan: blocks per workgroup at most (one chaser lane each; the last wave is the prefix writer, never a chaser)
-constexpr uint32_t kScanMaxBlocks = 64u * (kScanWaves - 1);
+// k_scan: blocks per workgroup at most (one chaser lane each; the last kScanWriters waves write the prefix rows and
+// are never chasers)
+constexpr int kScanWriters = 2;
+constexpr uint32_t kScanMaxBlocks = 64u * (kScanWaves - kScanWriters);
 // k_scan prefix rows per workgroup (units of 64 windows: 4 per block, +1 for a window straddling the range start)
 inline uint32_t scan_unit_stride(uint64_t nblocks, uint64_t grid) {
   return (uint32_t)(((nblocks + grid - 1) / grid) * (kBlock / 8192) + 2);

@@ -345,6 +345,8 @@ def _frag_error(res):
         return ErrWalUnknownRecordType()
     if res.err_class == L.ERR_PANIC:
         return RefPanic("slice bounds out of range (startOff beyond file size)")
+    if res.err_class == L.ERR_INTERNAL:
+        raise RuntimeError("bcw decode: a k_scan wait exceeded its bound (device-side protocol failure)")
     return None
 
 

@@ -344,11 +344,25 @@ int main(int argc, char** argv) {
       for (int w = 0; w < nw; ++w) t0 = std::min(t0, q[8 * w]);
       const char* nm[7] = {"entry", "tables", "chased", "units", "barrier", "verify", "emit"};
       for (int k = 0; k < 7; ++k) {
-        std::vector<double> v(nw);
-        for (int w = 0; w < nw; ++w) v[w] = (q[8 * w + k] - t0) / 100.0;
+        std::vector<double> v;  // waves that stamped this phase in this launch (the writers' "units" is their end)
+        for (int w = 0; w < nw; ++w)
+          if (q[8 * w + k] >= t0 && !(k == 3 && (w % kScanWaves) >= kScanWaves - kScanWriters))
+            v.push_back((q[8 * w + k] - t0) / 100.0);
+        if (v.empty()) continue;
         std::sort(v.begin(), v.end());
-        printf("  %-8s p0 %6.1f p10 %6.1f p50 %6.1f p90 %6.1f max %6.1f us\n", nm[k], v[0], v[nw / 10], v[nw / 2],
-               v[nw * 9 / 10], v[nw - 1]);
+        const size_t m = v.size();
+        printf("  %-8s p0 %6.1f p10 %6.1f p50 %6.1f p90 %6.1f max %6.1f us\n", nm[k], v[0], v[m / 10], v[m / 2],
+               v[m * 9 / 10], v[m - 1]);
+      }
+      {  // producer spins on a full ring, and the writer's end (its "units" stamp)
+        uint64_t rw = 0, wmax = 0; double wend = 0, wwait = 0; int nwr = 0;
+        for (int w = 0; w < nw; ++w) {
+          const bool wr = (w % kScanWaves) >= kScanWaves - kScanWriters;
+          if (!wr) { rw += q[8 * w + 7]; wmax = std::max(wmax, q[8 * w + 7]); }
+          else { wend = std::max(wend, (q[8 * w + 3] - t0) / 100.0); wwait += q[8 * w + 7] / 100.0; ++nwr; }
+        }
+        printf("  ring-full spins: total %lu, max per wave %lu | writer done (max) %.1f us, ack waits %.1f us per writer\n",
+               rw, wmax, wend, wwait / nwr);
       }
       std::vector<double> ch;  // chasers only (wave 0 of each workgroup)
       for (int w = 0; w < nw; w += kScanWaves) ch.push_back((q[8 * w + 2] - t0) / 100.0);
@@ -360,30 +374,17 @@ int main(int argc, char** argv) {
       switch (v) {
         case 1: return run_scan(k_scan<1>, ea);
         case 2: return run_scan(k_scan<2>, ea);
-        case 4: return run_scan(k_scan<4>, ea);
         case 8: return run_scan(k_scan<8>, ea);
         case 10: return run_scan(k_scan<10>, ea);
-        case 14: return run_scan(k_scan<14>, ea);
-        case 42: return run_scan(k_scan<42>, ea);
-        case 138: return run_scan(k_scan<138>, ea);
-        case 1034: return run_scan(k_scan<1034>, ea);
-        case 65536: return run_scan(k_scan<65536>, ea);
-        case 8202: return run_scan(k_scan<8202>, ea);
-        case 16394: return run_scan(k_scan<16394>, ea);
-        case 7211: return run_scan(k_scan<7211>, ea);
-        case 15371: return run_scan(k_scan<15371>, ea);
+        case 2048: return run_scan(k_scan<2048>, ea);
         case 2058: return run_scan(k_scan<2058>, ea);
         case 4106: return run_scan(k_scan<4106>, ea);
-        case 7178: return run_scan(k_scan<7178>, ea);
-        case 7179: return run_scan(k_scan<7179>, ea);
-        case 266: return run_scan(k_scan<266>, ea);
-        case 139: return run_scan(k_scan<139>, ea);
-        case 267: return run_scan(k_scan<267>, ea);
-        case 74: return run_scan(k_scan<74>, ea);
-        case 106: return run_scan(k_scan<106>, ea);
-        case 11: return run_scan(k_scan<11>, ea);
-        case 43: return run_scan(k_scan<43>, ea);
+        case 65536: return run_scan(k_scan<65536>, ea);
         case 512: { const float r = run_scan(k_scan<512>, ea_s); scan_report(); return r; }
+        case 522: { const float r = run_scan(k_scan<522>, ea_s); scan_report(); return r; }
+        case 2560: { const float r = run_scan(k_scan<2560>, ea_s); scan_report(); return r; }
+        case 66048: { const float r = run_scan(k_scan<66048>, ea_s); scan_report(); return r; }
+        case 2570: { const float r = run_scan(k_scan<2570>, ea_s); scan_report(); return r; }
         default: return run_scan(k_scan<0>, ea);
       }
     };

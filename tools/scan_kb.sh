@@ -1,10 +1,10 @@
 #!/bin/bash
-# k_scan phase breakdown (tools/kbench scan mode): ablation variants interleaved, per-wave phase stamps.
+# k_scan timing probes (kbench scan mode), config B and C, variants in VARS.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT=gpurun_out/${TAG:-kbs}
 mkdir -p "$OUT"
-timeout -k 10 120 ./tools/kbench/kbench 1073741824 0 scan ${VARS:-0 1 2 4 8 10 14 512} > "$OUT/b.log" 2>&1 || { tail -30 "$OUT/b.log"; exit 1; }
-tail -40 "$OUT/b.log"
-timeout -k 10 120 ./tools/kbench/kbench 1073741824 1 scan ${VARS:-0 1 2 4 8 10 14 512} > "$OUT/c.log" 2>&1 || { tail -30 "$OUT/c.log"; exit 1; }
-tail -40 "$OUT/c.log"
+for m in 0 1; do
+  timeout -k 10 120 ./tools/kbench/kbench 1073741824 $m scan ${VARS:-0 2058 512} > "$OUT/kb_$m.log" 2>&1 || { tail -30 "$OUT/kb_$m.log"; exit 1; }
+  echo "== config $m"; grep "k_scan<" "$OUT/kb_$m.log"; grep -A8 "entry" "$OUT/kb_$m.log" | tail -9
+done
