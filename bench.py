@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--decode-path", type=int, default=1, choices=[0, 1],
                     help="0: one launch per segment (k_scan, the default); 1: k_chase + k_crc (BCW_OPT_DECODE_PATH)")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_v6_k_crc_pmc.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03_v3_k_crc_pmc.json"),
                     help="PMC traffic summary (rocprofv3 --pmc of this command) to report as roofline.traffic")
     return ap.parse_args()
 

@@ -1498,7 +1498,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
   constexpr uint32_t kRing = 32;
   __shared__ __attribute__((aligned(16))) uint32_t s_ring[kRing * 64];
   __shared__ uint32_t s_rstate[kRing];  // 0: free, else the unit + 1 whose row the slot holds
-  constexpr uint32_t kWDepth = 56;  // each writer's rows in flight (7 batches of 2 stores: vmcnt(12) below)
+  constexpr uint32_t kWDepth = 16;  // each writer's stores in flight (vmcnt(8) below; 56 in flight: 309 vs 303 us, B)
   __shared__ uint32_t s_rhead, s_wunit[kScanWriters][kWDepth];
   uint32_t* s_slice = lds;
   uint32_t* s_fwd = lds + kLdsSlice;
@@ -1736,12 +1736,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
     if (kind == ST_WRITE) {
       // ---- the writers: the prefix rows to HBM, kWB ring slots (one batch) at a time in ticket order, batches dealt
       // round-robin to the kScanWriters writer waves. One wave-wide poll and kWB independent row reads per batch (a
-      // row at a time was a chain of LDS round trips); kWDepth stores in flight per writer (write acks take ~25 us
-      // under this read load: one writer with 48 in flight finished ~40 us after the streaming). A unit is marked
-      // done once its store has retired, kWDepth rows later or at the end ----
+      // row at a time was a chain of LDS round trips); kWDepth stores in flight per writer (the writers hardly ever
+      // wait on their stores: kbench measures ~0.1 us of ack waits per writer). A unit is marked done once its store
+      // has retired, kWDepth rows later or at the end (a shorter lag leaves fewer verify items for the tail) ----
       constexpr uint32_t kWB = 8;
-      // (ABL & 65536, kbench: 16 rows in flight per writer; ABL & 512: the writer's wait time in stamp slot 7)
-      constexpr uint32_t kD = (ABL & 65536) ? 16u : kWDepth;
+      // (ABL & 512, kbench: the writer's wait time in stamp slot 7)
+      constexpr uint32_t kD = kWDepth;
       uint64_t kb_wait = 0;
       uint32_t nrow = 0;  // rows this writer has issued
       for (uint32_t t = wid * kWB; t < nunits; t += kScanWriters * kWB) {
@@ -1757,24 +1757,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        // lane l carries 16 B of row 4 h + l / 16 (h = 0, 1): two 1 KiB stores per batch instead of eight 256 B ones
-        // (the store instructions themselves slowed the streaming waves' loads by ~20 us, L2-resident or not)
-        uint4 P[2];
-        uint32_t U[kWB], Ul[2];
+        uint32_t P[kWB], U[kWB];
 #pragma unroll
-        for (uint32_t h = 0; h < 2; ++h) {
-          const uint32_t j = 4u * h + (lane >> 4), slot = (t + j) % kRing;
-          P[h] = *reinterpret_cast<const uint4*>(&s_ring[slot * 64 + 4u * (lane & 15u)]);
-          Ul[h] = j < nb ? s_rstate[slot] - 1u : nunits;
+        for (uint32_t j = 0; j < kWB; ++j) {
+          const uint32_t slot = (t + j) % kRing;
+          P[j] = j < nb ? s_ring[slot * 64 + lane] : 0u;
+          U[j] = j < nb ? s_rstate[slot] - 1u : nunits;
         }
-#pragma unroll
-        for (uint32_t j = 0; j < kWB; ++j) U[j] = j < nb ? s_rstate[(t + j) % kRing] - 1u : nunits;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the rows are read before their slots are freed
         if (lane < nb) __hip_atomic_store(&s_rstate[(t + lane) % kRing], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (nrow >= kD) {  // this writer's rows nrow - kD .. + kWB have retired once kD - kWB remain
           const uint64_t tw = (ABL & 512) ? wall_clock64() : 0;
-          if (ABL & 65536) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+          static_assert(kWDepth == 16 && kWB == 8, "vmcnt below");
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
           if (ABL & 512) kb_wait += wall_clock64() - tw;
 #pragma unroll
           for (uint32_t j = 0; j < kWB; ++j) {
@@ -1782,13 +1777,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
             if (ud < nunits && lane == 0) atomicOr(&s_udone[ud >> 5], 1u << (ud & 31u));
           }
         }
+        // (one 256 B row per store: 1 KiB stores of four rows each were slower, 338 vs 309 us at config B)
 #pragma unroll
-        for (uint32_t h = 0; h < 2; ++h)  // (rows are whole 256 B: past m1 they hold don't-care prefixes)
-          if (Ul[h] < nunits && !(ABL & 2048))
-            *reinterpret_cast<uint4*>(pw + 64ull * Ul[h] + 4u * (lane & 15u)) = P[h];
-#pragma unroll
-        for (uint32_t j = 0; j < kWB; ++j)
+        for (uint32_t j = 0; j < kWB; ++j) {
+          if (j < nb && !(ABL & 2048) && m0 + 64ull * U[j] + lane < m1) pw[64ull * U[j] + lane] = P[j];
           if (lane == 0) s_wunit[wid][(nrow + j) % kD] = U[j];
+        }
         nrow += kWB;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -1406,7 +1406,7 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_re
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
 }
-constexpr int kCU = 4;  // units per lane in flight (4 KiB per wave: a copy needs ~64-96 KiB in flight per CU)
+constexpr int kCU = 2;  // units per lane in flight (8 waves per SIMD: the wave count hides the latency; 4: 35.9 ms)
 
 
 // copy m bytes from src to dst (global pointers, any alignment), one wave. Every unit (16 B aligned to

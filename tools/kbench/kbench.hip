@@ -379,11 +379,9 @@ int main(int argc, char** argv) {
         case 2048: return run_scan(k_scan<2048>, ea);
         case 2058: return run_scan(k_scan<2058>, ea);
         case 4106: return run_scan(k_scan<4106>, ea);
-        case 65536: return run_scan(k_scan<65536>, ea);
         case 512: { const float r = run_scan(k_scan<512>, ea_s); scan_report(); return r; }
         case 522: { const float r = run_scan(k_scan<522>, ea_s); scan_report(); return r; }
         case 2560: { const float r = run_scan(k_scan<2560>, ea_s); scan_report(); return r; }
-        case 66048: { const float r = run_scan(k_scan<66048>, ea_s); scan_report(); return r; }
         case 2570: { const float r = run_scan(k_scan<2570>, ea_s); scan_report(); return r; }
         default: return run_scan(k_scan<0>, ea);
       }
