@@ -192,9 +192,10 @@ const char* bcw_kernel_name(int kernel_id);
  *                         0..BCW_CHASE_DIRECT_MAX (default BCW_CHASE_DIRECT_MAX); 0 forces the look-back at
  *                         every size (the tests drive that branch on small segments with it; with
  *                         BCW_OPT_DECODE_PATH 1, since only k_chase has it).
- *   BCW_OPT_DECODE_PATH   0 (default): a segment of at most 1024 blocks per CU (8 GiB on 256 CUs) decodes in one
- *                         launch (k_scan), larger ones in two (k_chase + k_crc); 1: always the two launches.
- *                         Both give identical tables and results. */
+ *   BCW_OPT_DECODE_PATH   1 (default): two launches (k_chase + k_crc); 0: a segment of at most 640 blocks per CU
+ *                         (5 GiB on 256 CUs) decodes in one launch (k_scan), larger ones in two. Both give
+ *                         identical tables and results; k_scan is faster on long header chains (config C) and
+ *                         slower on short ones (config B), DESIGN.md section 3. */
 #define BCW_OPT_CHASE_DIRECT 1
 #define BCW_OPT_DECODE_PATH 2
 #define BCW_CHASE_DIRECT_MAX 1024
