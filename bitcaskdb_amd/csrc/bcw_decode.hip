@@ -135,8 +135,7 @@ constexpr int kDirect = BCW_CHASE_DIRECT_MAX;  // k_chase workgroups up to which
 // visit(k, start, len, crc, type) for every header of the block; returns the fragment count
 template <typename V>
 __device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg, uint64_t seg_len, uint64_t boff,
-                                                uint32_t bufsize, V&& visit) {
-  uint32_t n = 0, h = 0;
+                                                uint32_t bufsize, V&& visit, uint32_t h = 0, uint32_t n = 0) {
   uint32_t s = 0;      // predicted distance to the next header (0: read one header)
   uint32_t lfull = 0;  // length of the last Full fragment (+1; 0: none)
   while (h + kHdr <= bufsize) {
@@ -206,8 +205,10 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                               uint32_t direct_max, uint32_t* __restrict__ equeue) {
   // {crc, start | len << 16} and type of each lane's headers: 9 KiB, so a k_chase workgroup fits beside a k_crc
   // workgroup (which leaves 11 KiB of the CU's LDS) when another segment's decode is in flight
-  __shared__ uint32_t s_hold[kChaseHold][2][64];
-  __shared__ uint8_t s_type[kChaseHold][64];
+  // (ABL & 256, kbench: 64 held headers per lane)
+  constexpr int kHold = (ABL & 256) ? 64 : kChaseHold;
+  __shared__ uint32_t s_hold[kHold][2][64];
+  __shared__ uint8_t s_type[kHold][64];
   const uint32_t lane = threadIdx.x;
   const uint64_t tc0 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t wg = 0;
@@ -223,13 +224,15 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   }
   // record-state summary of the block (see kSumHasE) and its first unknown-type fragment
   uint32_t ne = 0, tacc = 0, tnz = 0xffffu, tst = 0, badk = 0xffffffffu;
+  uint32_t hres = 0;  // where the first header past the held ones starts (the table pass resumes there)
   const uint32_t n = chase_block(seg, seg_len, boff, bufsize,
                                  [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
-                                   if (k < (uint32_t)kChaseHold) {
+                                   if (k < (uint32_t)kHold) {
                                      s_hold[k][0][lane] = crc;
                                      s_hold[k][1][lane] = start | (len << 16);
                                      s_type[k][lane] = (uint8_t)type;
                                    }
+                                   if (k == (uint32_t)kHold - 1u) hres = start + len;
                                    if (type == BCW_RECORD_FULL || type == BCW_RECORD_LAST) {
                                      ++ne;
                                      tacc = 0;
@@ -334,16 +337,16 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     bsum[b] = make_uint2(tacc | (tnz << 16), tst | (ne ? kSumHasE : 0u));
     if (badk != 0xffffffffu)  // the first unknown-type fragment of the segment (reset by the previous finalize)
       atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_TYPE]), (unsigned long long)(g0 + badk));
-    const uint32_t nh = n < (uint32_t)kChaseHold ? n : (uint32_t)kChaseHold;
+    const uint32_t nh = n < (uint32_t)kHold ? n : (uint32_t)kHold;
     for (uint32_t k = 0; k < nh; ++k) {
       const uint32_t sl = s_hold[k][1][lane];
       put_frag(frags, g0 + k, frag_cap, (uint32_t)b, sl & 0xffffu, sl >> 16, s_hold[k][0][lane], s_type[k][lane],
                initc);
     }
-    if (n > (uint32_t)kChaseHold)  // the tail of a block with more headers than held
+    if (n > (uint32_t)kHold)  // the tail of a block with more headers than held, chased again from the first of them
       chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
-        if (k >= (uint32_t)kChaseHold) put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, initc);
-      });
+        put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, initc);
+      }, hres, (uint32_t)kHold);
   }
   if (ABL & 16) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1570,6 +1573,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
       bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
     }
     uint32_t ne = 0, tacc = 0, tnz = 0xffffu, tst = 0, badk = 0xffffffffu;
+    uint32_t hres = 0;  // where the first header past the held ones starts (the table pass resumes there)
     const uint32_t n = chase_block(seg, seg_len, boff, (ABL & 4096) ? 0u : bufsize,
                                    [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
                                      if (k < H) {
@@ -1578,6 +1582,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
                                        e[1] = start | (len << 16);
                                        e[2] = type;
                                      }
+                                     if (k == H - 1u) hres = start + len;
                                      if (type == BCW_RECORD_FULL || type == BCW_RECORD_LAST) {
                                        ++ne;
                                        tacc = 0;
@@ -1667,13 +1672,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t* __restrict
         put_frag(frags, g0 + k, frag_cap, (uint32_t)b, e[1] & 0xffffu, e[1] >> 16, e[0], e[2], tabs.initc);
         vrange(g0 + k, e[1] & 0xffffu, e[1] >> 16);
       }
-      if (n > H)  // the tail of a block with more headers than held
+      if (n > H)  // the tail of a block with more headers than held, chased again from the first of them
         chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
-          if (k >= H) {
-            put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, tabs.initc);
-            vrange(g0 + k, start, len);
-          }
-        });
+          put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, tabs.initc);
+          vrange(g0 + k, start, len);
+        }, hres, H);
     }
     if (wg == G - 1u && wave == 0u && lane == 0u) {  // the segment totals
       const uint64_t total = s_base[0] + s_base[2], total_e = s_base[1] + s_base[3];
