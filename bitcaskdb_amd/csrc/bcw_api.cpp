@@ -335,7 +335,10 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.equeue);
   (void)hipFree(s.lbw);
   (void)hipFree(s.pwin);
-  s = Scratch{};
+  Scratch z{};  // the chunk streams and events live as long as the context (bcw_ctx_destroy)
+  for (int i = 0; i < 2; ++i) z.cs[i] = s.cs[i];
+  for (int i = 0; i < 4; ++i) z.cev[i] = s.cev[i];
+  s = z;
 }
 
 static void free_enc_scratch(EncScratch& e) {
@@ -356,7 +359,13 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   if (!c) return BCW_E_INVAL;
   DeviceGuard dg(c->device);
   if (c->cur) (void)hipStreamSynchronize(c->cur);
+  for (hipStream_t cs : c->s.cs)
+    if (cs) (void)hipStreamSynchronize(cs);
   free_scratch(c->s);
+  for (hipEvent_t& e : c->s.cev)
+    if (e) { (void)hipEventDestroy(e); e = nullptr; }
+  for (hipStream_t& cs : c->s.cs)
+    if (cs) { (void)hipStreamDestroy(cs); cs = nullptr; }
   free_enc_scratch(c->es);
   if (c->es.aux) (void)hipStreamSynchronize(c->es.aux);
   if (c->es.ev_scan) (void)hipEventDestroy(c->es.ev_scan);
@@ -420,6 +429,7 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   s.epoch = 1;
   s.chase_direct = c->chase_direct;
   s.scan = c->scan;
+  s.chunks = c->chunks;
   // on the codec's stream: a null-stream hipMemset is not ordered before kernels on a non-blocking
   // stream, and a look-back word zeroed after k_chase published it would never be seen again
   // misc[15] (the first unknown-type fragment, an atomicMin in k_chase) starts at UINT64_MAX; every decode's
@@ -514,6 +524,11 @@ int bcw_ctx_set_option(bcw_ctx* c, int option, uint64_t value) {
       if (value > 1) return BCW_E_INVAL;
       c->s.scan = value == 0 ? 1u : 0u;
       c->scan = c->s.scan;
+      return BCW_OK;
+    case BCW_OPT_DECODE_CHUNKS:
+      if (value < 1 || value > 3) return BCW_E_INVAL;
+      c->s.chunks = (uint32_t)value;
+      c->chunks = (uint32_t)value;
       return BCW_OK;
     default:
       return BCW_E_INVAL;

@@ -26,7 +26,7 @@ enum { M_FIRST_BAD = 0,  // first record whose parse fails (atomicMin in k_crc's
        M_T_CRC0 = 10, M_T_FIN = 11,  // wall_clock64 stamps (diagnostics)
        M_ABORT = 12,     // k_scan: the wait site that timed out (0: none); reported as BCW_ERR_INTERNAL
        M_TICKET = 13,    // k_chase workgroup tickets (monotonic across launches)
-       M_BAD_CRC = 14,   // first fragment failing its CRC (atomicMin in k_crc; reset by k_chase)
+       M_BAD_CRC = 14,   // first fragment failing its CRC (atomicMin in k_crc; reset by the finalize)
        M_BAD_TYPE = 15 };  // first fragment of an unknown type (atomicMin in k_chase; reset by k_crc's finalize)
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -358,15 +358,18 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     }
   }
   const uint64_t nwg = (nblocks + 63) / 64;
-  if (wg == nwg - 1 && lane == 63) {
+  if (lane == 63 && !(ABL & 2)) {
+    // the bases at the end of the workgroup's blocks (the next workgroup's first block writes the same values): a
+    // k_crc over a leading chunk of the segment reads them before the rest is chased. k_crc's completion counter and
+    // first-failure words were reset by the previous decode's finalize (or the scratch setup).
     const uint64_t total = excl + tot, total_e = excl_e + tot_e;
-    fbase[nblocks] = (uint32_t)(total < 0xffffffffull ? total : 0xffffffffull);
-    rbase[nblocks] = (uint32_t)(total_e < 0xffffffffull ? total_e : 0xffffffffull);
-    misc[M_NFRAGS] = total;
-    misc[M_NE] = total_e;
-    misc[M_DONE_CRC] = 0;         // k_crc's workgroup completion counter
-    misc[M_BAD_CRC] = ~0ull;      // k_crc: first fragment failing its CRC
-    misc[M_FIRST_BAD] = ~0ull;    // k_crc: first record whose RecordFromBytes / Decode fails
+    const uint64_t be = wg * 64 + 64 < nblocks ? wg * 64 + 64 : nblocks;
+    fbase[be] = (uint32_t)(total < 0xffffffffull ? total : 0xffffffffull);
+    rbase[be] = (uint32_t)(total_e < 0xffffffffull ? total_e : 0xffffffffull);
+    if (wg == nwg - 1) {
+      misc[M_NFRAGS] = total;
+      misc[M_NE] = total_e;
+    }
   }
   if (wg == 0 && lane < 8u) equeue[lane * kEqStride] = 0;  // k_crc's emission queues
 }
@@ -920,11 +923,12 @@ struct ItemMeta {
   uint2 s;  // emit_prefetch of block bb
   uint32_t f0, f1, rec;
 };
-__device__ __forceinline__ ItemMeta item_meta(const EmitArgs& A, uint64_t it, uint64_t bpw, uint64_t nblocks,
+// item `it` of a chunk [cb0, cb1) of the segment's blocks: blocks [cb0 + it bpw, + bpw), cut at cb1
+__device__ __forceinline__ ItemMeta item_meta(const EmitArgs& A, uint64_t it, uint64_t bpw, uint64_t cb0, uint64_t cb1,
                                               uint32_t lane) {
   ItemMeta m;
-  m.bb = it * bpw < nblocks ? it * bpw : nblocks - 1;  // a clamped (unconditional) load for an exhausted queue
-  const uint64_t be = m.bb + bpw < nblocks ? m.bb + bpw : nblocks;
+  m.bb = cb0 + it * bpw < cb1 ? cb0 + it * bpw : cb1 - 1;  // a clamped (unconditional) load for an exhausted queue
+  const uint64_t be = m.bb + bpw < cb1 ? m.bb + bpw : cb1;
   m.s = emit_prefetch(A, m.bb, lane);
   m.f0 = A.fbase[m.bb];
   m.f1 = A.fbase[be];
@@ -996,7 +1000,7 @@ __device__ __forceinline__ void finalize(const EmitArgs& A, uint64_t nblocks, ui
   r.retry_frag_capacity = nfr > frag_cap ? nfr : 0;
   r.generation = gen;
   *res = r;
-  // for the next decode (k_chase resets the first three again; k_scan relies on these)
+  // for the next decode (both paths rely on these; the scratch setup sets them first)
   misc[M_DONE_CRC] = 0;
   misc[M_BAD_CRC] = ~0ull;
   misc[M_FIRST_BAD] = ~0ull;
@@ -1015,7 +1019,11 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
                                                      uint64_t frag_cap, Tables tabs, EmitArgs ea,
                                                      uint32_t tail_panic, uint64_t gen,
                                                      bcw_decode_result* __restrict__ res,
-                                                     uint64_t* __restrict__ misc) {
+                                                     uint64_t* __restrict__ misc, uint64_t cb0, uint64_t cb1,
+                                                     uint32_t nwg_total) {
+  // [cb0, cb1): the chunk of the segment's blocks this launch verifies and emits (the whole segment, or one of the
+  // chunks launched as their chase ends); nwg_total: the workgroups of every chunk's launch, the last of which
+  // writes the segment result
   __shared__ __attribute__((aligned(16))) uint32_t lds[kCrcLds / 4];
   const uint64_t t_entry = (ABL & 512) ? wall_clock64() : 0;
   uint32_t* s_slice = lds;
@@ -1036,14 +1044,16 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const bool emitter = kEm && wave == kCrcWaves - 1;
   const uint64_t nw = (uint64_t)gridDim.x * kNCrc;
   const uint64_t gw = (uint64_t)blockIdx.x * kNCrc + (emitter ? kNCrc - 1 : wave);
-  const uint64_t b0 = emitter ? nblocks * (gw + 1) / nw : nblocks * gw / nw, b1 = nblocks * (gw + 1) / nw;
+  const uint64_t cn = cb1 - cb0;
+  const uint64_t b0 = cb0 + (emitter ? cn * (gw + 1) / nw : cn * gw / nw), b1 = cb0 + cn * (gw + 1) / nw;
   // the wave's fragment range and its first descriptors are loaded while the table image crosses into LDS
   // (that chain of dependent loads no longer follows the image copy)
   const uint64_t f0 = fbase[b0];
   uint64_t f1 = fbase[b1];
-  // the emission work items (blocks per item for ~64 fragments each; see emit_item)
-  const uint64_t nf_all = misc[M_NFRAGS] < frag_cap ? misc[M_NFRAGS] : frag_cap;
-  uint64_t bpw = nf_all ? (64 * nblocks) / nf_all : nblocks;
+  // the emission work items (blocks per item for ~64 fragments each of the chunk; see emit_item)
+  const uint64_t fc0 = fbase[cb0], fc1 = fbase[cb1];
+  const uint64_t nf_all = fc1 > fc0 ? (fc1 - fc0 < frag_cap ? fc1 - fc0 : frag_cap) : 0;
+  uint64_t bpw = nf_all ? (64 * cn) / nf_all : cn;
   if (bpw < 1) bpw = 1;
   uint4 pf = make_uint4(0, 0, 0, 0);  // the next group's 64 fragment descriptors (raw; see load_win)
   {  // table image -> LDS: all 16 B loads in flight before the first store
@@ -1317,8 +1327,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   // item is taken and its block data requested while this item's fragment descriptors are in flight, so an item
   // costs two dependent round trips (descriptors, record prefixes) ----
   if (!(ABL & 8) && !(ea.kb_flags & 1u)) {
-    const uint64_t B0 = nblocks * ((uint64_t)blockIdx.x * kNCrc) / nw;
-    const uint64_t B1 = nblocks * ((uint64_t)(blockIdx.x + 1) * kNCrc) / nw;
+    const uint64_t B0 = cn * ((uint64_t)blockIdx.x * kNCrc) / nw;  // chunk-relative
+    const uint64_t B1 = cn * ((uint64_t)(blockIdx.x + 1) * kNCrc) / nw;
     const uint64_t i0 = (B0 + bpw - 1) / bpw, nitems = (!kEm || emitter) ? (B1 + bpw - 1) / bpw : 0;
     uint32_t taken = 0;  // the dedicated emitter takes every item in order
     auto deq = [&]() -> uint64_t {
@@ -1334,7 +1344,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     const uint64_t t_crc = ea.kb_stamps ? wall_clock64() : 0;
     uint64_t n_items = 0;
     uint64_t it = deq();
-    ItemMeta m = item_meta(ea, it, bpw, nblocks, lane);
+    ItemMeta m = item_meta(ea, it, bpw, cb0, cb1, lane);
     PredSync ps;  // k_chase's tables: nothing to acquire
     while (it < nitems) {
       ++n_items;
@@ -1344,7 +1354,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       ItemMeta mn;
       emit_chunks<ABL & (4096 | 8192)>(ea, es, m.f0, f1, lane, [&]() {
         nx = deq();
-        mn = item_meta(ea, nx, bpw, nblocks, lane);
+        mn = item_meta(ea, nx, bpw, cb0, cb1, lane);
       });
       it = nx;
       m = mn;
@@ -1369,7 +1379,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   if (lane == 0)
     gorder = __hip_atomic_fetch_add(&misc[M_DONE_CRC], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   gorder = (uint64_t)__shfl((long long)gorder, 0, 64);
-  if (gorder != gridDim.x - 1u) return;
+  if (gorder != nwg_total - 1u) return;
   if (lane == 0) misc[M_T_FIN] = wall_clock64();
   finalize(ea, nblocks, frag_cap, tail_panic, gen, res, lane);
 }
@@ -2073,18 +2083,60 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
     return hipGetLastError();
   }
   const uint32_t nb_grid = (uint32_t)((nblocks + 63) / 64);
+  const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
+  // Two chunks for a segment of at least 128 blocks per CU: k_chase over the second chunk runs beside k_crc over the
+  // first, and the second k_crc's workgroups take the CUs the first one's finishing workgroups free (each k_crc on a
+  // stream of its own; the call's stream waits for both). The chunks split at a multiple of 64 blocks, a k_chase
+  // workgroup's range, whose end bases that workgroup writes. A k_crc's emission items stay inside its chunk; a
+  // record that began in an earlier chunk reads that chunk's (finished) tables.
+  const bool two = (s.chunks == 2 && nblocks >= 128ull * (uint64_t)num_cus) || (s.chunks == 3 && nblocks >= 128);
+  if (two && !s.cs[0]) {
+    for (auto& c : s.cs)
+      if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) return hipErrorOutOfMemory;
+    for (auto& e : s.cev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return hipErrorOutOfMemory;
+  }
+  const uint64_t cut = two ? (nblocks / 2 + 63) / 64 * 64 : nblocks;  // blocks of the first chunk
+  const uint32_t g0n = (uint32_t)((cut + 63) / 64);
   pr.begin(K_CHASE, stream, ev);
-  k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
-                                       s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch, tabs.initc,
-                                       s.chase_direct, s.equeue);
+  k_chase<0><<<g0n, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
+                                    s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch, tabs.initc, s.chase_direct,
+                                    s.equeue);
+  if (!two) {
+    pr.end(K_CHASE, stream, ev);
+    s.tickets += nb_grid;
+    next_epoch();
+    pr.begin(K_CRC, stream, ev);
+    k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
+                                                           s.frag_cap, tabs, ea, tail_panic, gen, d_result, s.misc,
+                                                           0ull, nblocks, (uint32_t)num_cus);
+    pr.end(K_CRC, stream, ev);
+    return hipGetLastError();
+  }
+  (void)hipEventRecord(s.cev[0], stream);
+  // (the second chase continues the first one's tickets: its workgroups are g0n.. of the segment's)
+  k_chase<0><<<nb_grid - g0n, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum,
+                                              s.frags, s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch,
+                                              tabs.initc, s.chase_direct, s.equeue);
   pr.end(K_CHASE, stream, ev);
+  (void)hipEventRecord(s.cev[1], stream);
   s.tickets += nb_grid;
   next_epoch();
-  const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
-  pr.begin(K_CRC, stream, ev);
-  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
-                                                         s.frag_cap, tabs, ea, tail_panic, gen, d_result, s.misc);
-  pr.end(K_CRC, stream, ev);
+  // profiling: one K_CRC interval from the first chunk's k_crc start to the second's end (events on both streams)
+  (void)hipStreamWaitEvent(s.cs[0], s.cev[0], 0);
+  (void)hipStreamWaitEvent(s.cs[1], s.cev[1], 0);
+  pr.begin(K_CRC, s.cs[0], ev);
+  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, s.cs[0]>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
+                                                          s.frag_cap, tabs, ea, tail_panic, gen, d_result, s.misc,
+                                                          0ull, cut, 2u * (uint32_t)num_cus);
+  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, s.cs[1]>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
+                                                          s.frag_cap, tabs, ea, tail_panic, gen, d_result, s.misc,
+                                                          cut, nblocks, 2u * (uint32_t)num_cus);
+  (void)hipEventRecord(s.cev[2], s.cs[0]);
+  (void)hipStreamWaitEvent(s.cs[1], s.cev[2], 0);  // the interval's end (and the join) after both
+  pr.end(K_CRC, s.cs[1], ev);
+  (void)hipEventRecord(s.cev[3], s.cs[1]);
+  (void)hipStreamWaitEvent(stream, s.cev[3], 0);
   return hipGetLastError();
 }
 

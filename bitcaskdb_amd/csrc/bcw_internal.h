@@ -88,6 +88,9 @@ struct Scratch {
   uint64_t* lbw = nullptr;     // [nlb] k_scan: per-workgroup "written" words (zeroed at allocation)
   uint32_t* pwin = nullptr;    // k_scan: per-window prefixes, [workgroups][scan_unit_stride][64]
   uint32_t scan = 0;           // BCW_OPT_DECODE_PATH: 1 = one launch (k_scan) when the segment fits, 0 = k_chase + k_crc
+  uint32_t chunks = 1;         // BCW_OPT_DECODE_CHUNKS: 1 one chunk, 2 / 3 two (see bcw.h)
+  hipStream_t cs[2] = {};      // the chunks' k_crc streams, and their events (chase done, k_crc done)
+  hipEvent_t cev[4] = {};
 };
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
@@ -235,6 +238,7 @@ struct bcw_ctx {
   uint32_t last_start_off = 0;
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // BCW_OPT_CHASE_DIRECT
   uint32_t scan = 0;                             // BCW_OPT_DECODE_PATH
+  uint32_t chunks = 1;                           // BCW_OPT_DECODE_CHUNKS
   uint64_t last_nfrag_cap = 0;
   bcw::Prof prof;
 };

@@ -195,9 +195,15 @@ const char* bcw_kernel_name(int kernel_id);
  *   BCW_OPT_DECODE_PATH   1 (default): two launches (k_chase + k_crc); 0: a segment of at most 640 blocks per CU
  *                         (5 GiB on 256 CUs) decodes in one launch (k_scan), larger ones in two. Both give
  *                         identical tables and results; k_scan is faster on long header chains (config C) and
- *                         slower on short ones (config B), DESIGN.md section 3. */
+ *                         slower on short ones (config B), DESIGN.md section 3.
+ *   BCW_OPT_DECODE_CHUNKS 1 (default): one chunk. 2: on the two-launch path a segment of at least 128 blocks per CU
+ *                         is chased and verified as two chunks, the second chunk's chase running beside the first
+ *                         chunk's k_crc on the context's own streams (the call's stream waits for both); 3: two
+ *                         chunks from 128 blocks on (tests). Identical results; 2 is slower on MI355X (the second
+ *                         chase's header reads wait behind the first k_crc's stream: DESIGN.md section 7). */
 #define BCW_OPT_CHASE_DIRECT 1
 #define BCW_OPT_DECODE_PATH 2
+#define BCW_OPT_DECODE_CHUNKS 3
 #define BCW_CHASE_DIRECT_MAX 1024
 int bcw_ctx_set_option(bcw_ctx* ctx, int option, uint64_t value);
 /* Size the context's fragment scratch for at least n fragments on the next decode (after a decode

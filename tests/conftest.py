@@ -40,6 +40,20 @@ def ctx_two():
     from bitcaskdb_amd import Context, _lib
     c = Context(0)
     c.set_option(_lib.OPT_DECODE_PATH, 1)
+    c.set_option(_lib.OPT_DECODE_CHUNKS, 1)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="session")
+def ctx_chunks():
+    """the two-launch decode over two chunks from 128 blocks on (BCW_OPT_DECODE_CHUNKS 3)"""
+    if not gpu_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    from bitcaskdb_amd import Context, _lib
+    c = Context(0)
+    c.set_option(_lib.OPT_DECODE_PATH, 1)
+    c.set_option(_lib.OPT_DECODE_CHUNKS, 3)
     yield c
     c.close()
 
@@ -56,7 +70,7 @@ def ctx_scan():
     c.close()
 
 
-@pytest.fixture(params=["scan", "two"])
-def ctx_path(request, ctx_scan, ctx_two):
-    """both decode paths: the one-launch k_scan and k_chase + k_crc"""
-    return ctx_scan if request.param == "scan" else ctx_two
+@pytest.fixture(params=["scan", "two", "chunks"])
+def ctx_path(request, ctx_scan, ctx_two, ctx_chunks):
+    """both decode paths: the one-launch k_scan, and k_chase + k_crc over one chunk and over two"""
+    return {"scan": ctx_scan, "two": ctx_two, "chunks": ctx_chunks}[request.param]

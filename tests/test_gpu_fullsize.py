@@ -203,9 +203,20 @@ def test_config_e_compaction_2m_rebase(ctx):
 
 
 def test_config_b_two_launch(ctx_two, config_b):
-    """config B on the two-launch path (k_chase + k_crc, BCW_OPT_DECODE_PATH 1): every column equals the
-    oracle's, as on the default one-launch k_scan."""
-    got, _ = full_parity(ctx_two, config_b, cases.params(), "B two-launch")
+    """config B on the two-launch path in one chunk (BCW_OPT_DECODE_CHUNKS 1): every column equals the oracle's"""
+    got, _ = full_parity(ctx_two, config_b, cases.params(), "B one chunk")
+    assert got.result.err_class == 0 and got.n_records > 250000
+
+
+def test_config_b_two_chunks(ctx_chunks, config_b):
+    """config B on the two-launch path over two chunks (BCW_OPT_DECODE_CHUNKS 3)"""
+    got, _ = full_parity(ctx_chunks, config_b, cases.params(), "B two chunks")
+    assert got.result.err_class == 0 and got.n_records > 250000
+
+
+def test_config_b_one_launch(ctx_scan, config_b):
+    """config B on the one-launch path (k_scan, BCW_OPT_DECODE_PATH 0)"""
+    got, _ = full_parity(ctx_scan, config_b, cases.params(), "B k_scan")
     assert got.result.err_class == 0 and got.n_records > 250000
 
 

@@ -296,7 +296,7 @@ int main(int argc, char** argv) {
   };
   auto run = [&](auto kern, int grid, const EmitArgs& a) {
     return timeit([&] { hipMemsetAsync(s.equeue, 0, 1024, st);  // the emission queues (k_chase resets them)
-                        kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc); },
+                        kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid); },
                   reps, st);
   };
   const int cus = ctx->num_cus;
@@ -538,7 +538,7 @@ int main(int argc, char** argv) {
     hipMemsetAsync(&s.misc[M_DONE_CRC], 0, 8, st);  // the last workgroup finalizes
     hipMemsetAsync(s.equeue, 0, 1024, st);
     k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
-                                          s.misc);
+                                          s.misc, 0ull, nblocks, (uint32_t)cus);
   }, reps, st);
   printf("k_crc + finalize %.4f ms\n", as);
   {
