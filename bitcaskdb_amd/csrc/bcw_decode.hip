@@ -127,6 +127,24 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 // next one starts from the true position. Without that evidence a round reads one header. (Speculating
 // right after the first Full fragment, until a prediction fails, measured slower: config B k_chase
 // 27.4 -> 28.2 us, config C 83 -> 91 us.)
+// A bounded wait (k_chase, k_scan): every spin gives up after 200 ms (a correct wait lasts microseconds)
+// or once another wave has given up, records its site in misc[M_ABORT] and lets the kernel run to its end; the decode
+// then reports BCW_ERR_INTERNAL instead of hanging the device.
+struct Spin {
+  uint64_t t0 = 0;
+  __device__ __forceinline__ bool go(uint64_t* misc, uint32_t site) {  // true: keep waiting
+    const uint64_t t = wall_clock64();
+    if (t0 == 0) t0 = t;
+    if (t - t0 < 20000000ull &&
+        __hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull) {
+      __builtin_amdgcn_s_sleep(1);
+      return true;
+    }
+    atomicMax(reinterpret_cast<unsigned long long*>(&misc[M_ABORT]), (unsigned long long)site);
+    return false;
+  }
+};
+
 constexpr int kSpec = 8;
 constexpr int kChaseHold = 16;
 constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
@@ -271,8 +289,9 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
 #pragma unroll
     for (int k = 0; k < kDirect / 64; ++k) {
       const uint64_t q = lane + 64u * k;
+      Spin sp;  // bounded (BCW_ERR_INTERNAL), like every k_scan wait
       while ((v[k] >> 40) != epoch) {
-        __builtin_amdgcn_s_sleep(1);
+        if (!sp.go(misc, 9)) break;
         v[k] = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (q < wg) {
@@ -300,12 +319,13 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
       const uint64_t q = top - 1 - lane;  // lane 0: the nearest
       uint64_t vn = 0, ve = 0;
       if (top > lane) {
+        Spin sp;
         if (!dn)
           while (((vn = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
-            __builtin_amdgcn_s_sleep(1);
+            if (!sp.go(misc, 10)) break;
         if (!de)
           while (((ve = __hip_atomic_load(&lbe[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
-            __builtin_amdgcn_s_sleep(1);
+            if (!sp.go(misc, 11)) break;
       }
       auto step = [&](uint64_t v, bool& done, uint64_t& acc) {
         if (done) return;
@@ -673,6 +693,7 @@ struct EmitArgs {
   uint64_t* kb_stamps;  // tools/kbench only (null in the product): per wave {CRC done, emission done, items}
 };
 
+
 // The iterator state entering block b0 (wave-uniform): the pending record's length, its first non-empty
 // fragment as (block, block-local index, block-relative start), and the record row of block b0.
 struct EmitState {
@@ -685,23 +706,6 @@ struct EmitState {
 __device__ __forceinline__ uint2 emit_prefetch(const EmitArgs& A, uint64_t b0, uint32_t lane) {
   return b0 > lane ? A.bsum[b0 - 1 - lane] : make_uint2(0xffff0000u, kSumHasE);
 }
-// A bounded wait (k_scan): every spin of the one-launch decode gives up after 200 ms (a correct wait lasts microseconds)
-// or once another wave has given up, records its site in misc[M_ABORT] and lets the kernel run to its end; the decode
-// then reports BCW_ERR_INTERNAL instead of hanging the device.
-struct Spin {
-  uint64_t t0 = 0;
-  __device__ __forceinline__ bool go(uint64_t* misc, uint32_t site) {  // true: keep waiting
-    const uint64_t t = wall_clock64();
-    if (t0 == 0) t0 = t;
-    if (t - t0 < 20000000ull &&
-        __hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull) {
-      __builtin_amdgcn_s_sleep(1);
-      return true;
-    }
-    atomicMax(reinterpret_cast<unsigned long long*>(&misc[M_ABORT]), (unsigned long long)site);
-    return false;
-  }
-};
 
 // k_scan: the block summaries, fragment table and block bases of an earlier workgroup's blocks (blocks < B0) were
 // written inside the same launch by another CU. A wave reads them only after every predecessor has published its
