@@ -50,11 +50,11 @@ def parse():
                          "(own stream, segment, record table); the headline value is one segment at a time")
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events bracket every N-th k_crc launch of the timed region")
-    ap.add_argument("--decode-path", type=int, default=1, choices=[0, 1],
-                    help="0: one launch per segment (k_scan, the default); 1: k_chase + k_crc (BCW_OPT_DECODE_PATH)")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03_v3_k_crc_pmc.json"),
-                    help="PMC traffic summary (rocprofv3 --pmc of this command) to report as roofline.traffic")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04_k_crc_pmc.json"),
+                    help="PMC traffic summary (tools/pmc_summary.py over rocprofv3 --pmc passes of this command) to "
+                         "report as roofline.traffic; used only when its decode_src_sha16 matches this build's "
+                         "decode sources (bitcaskdb_amd/build.py decode_src_sha16)")
     return ap.parse_args()
 
 
@@ -293,7 +293,6 @@ def main():
         d_res = torch.zeros(C.sizeof(L.DecodeResult), dtype=torch.uint8, device=dev)
         params = L.DecodeParams(seg_len, BASE_TIME, 40, 20, 20, L.MODE_RECORD)
         sctx = Context(torch.cuda.current_device())
-        sctx.set_option(L.OPT_DECODE_PATH, args.decode_path)
         sstream = torch.cuda.Stream()  # dedicated stream: the codec's kernels and the timing events share it
         sctx.set_stream(sstream.cuda_stream)
         slots.append(dict(host=host, seg_len=seg_len, n_rec=n_rec, d_seg=d_seg, cols=cols, table=table, d_res=d_res,
@@ -342,8 +341,8 @@ def main():
     # kernel ids by name (the pipeline's kernel list is the library's)
     nk = int(L.lib.bcw_ctx_kernel_times(ctx.handle, None, None, 0))
     names = [L.lib.bcw_kernel_name(k).decode() for k in range(nk)]
-    # the dominant kernel: the whole one-launch decode (k_scan), or k_crc of the two-launch path
-    roof_name = "k_crc" if args.decode_path == 1 else "k_scan"
+    # the dominant kernel: k_crc (the CRC stream + record emission)
+    roof_name = "k_crc"
     roof_k = names.index(roof_name)
 
     def kernel_times(ctxs):
@@ -360,7 +359,7 @@ def main():
 
     all_ctx = [sl["ctx"] for sl in slots]
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks ----
-    # HIP events bracket only the roofline kernel (k_scan / k_crc) on each codec stream
+    # HIP events bracket only the roofline kernel (k_crc) on each codec stream
     # (every --event-every-th launch: an event pair idles that stream for a few microseconds)
     for cx in all_ctx:
         L.lib.bcw_ctx_set_profiling(cx.handle, 1 << roof_k)
@@ -390,8 +389,7 @@ def main():
                                                                                args.steps), 2),
                      "unit": "GiB/s", "ms_per_step": round(wall_p / args.steps * 1e3, 4),
                      "note": "steps rotate over independent segments on their own contexts/streams (a multi-file "
-                             "scan): one segment's k_chase / k_records and the kernel boundaries overlap the next "
-                             "one's k_crc"}
+                             "scan): one segment's k_chase and the kernel boundaries overlap the next one's k_crc"}
     # every kernel's average, one segment at a time (untimed repeat, events around each kernel)
     L.lib.bcw_ctx_set_profiling_sample(ctx.handle, 1)
     L.lib.bcw_ctx_set_profiling(ctx.handle, -1)
@@ -424,20 +422,25 @@ def main():
             dist.destroy_process_group()
         return
 
-    # ---- roofline of the dominant kernel (k_scan: the whole decode; k_crc on the two-launch path): algorithmic
-    # bytes per launch / avg duration ----
+    # ---- roofline of the dominant kernel (k_crc): algorithmic bytes per launch / avg duration ----
     alg_bytes = seg_len + 17 * n_frags  # segment read once + fragment descriptors (16 B read, 1 B verdict)
     achieved = alg_bytes / (crc_ms * 1e-3) / 1e9
-    traffic = None
+    # traffic: HBM bytes per launch from a committed PMC summary measured on THIS build's k_crc (same decode-source
+    # hash, same segment), else null
+    traffic, traffic_src = None, None
     if args.pmc and os.path.exists(args.pmc):
+        from bitcaskdb_amd.build import decode_src_sha16
         try:
             pm = json.load(open(args.pmc))
-            if pm.get("seg_bytes") == seg_len and pm.get("kernel") == roof_name:
+            if (pm.get("seg_bytes") == seg_len and pm.get("kernel") == roof_name
+                    and pm.get("decode_src_sha16") == decode_src_sha16()):
                 traffic = pm.get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(args.pmc, ROOT)
         except Exception:
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": roof_name,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
+                "kernel": roof_name,
                 "kernel_ms": round(crc_ms, 4), "kernel_launches_timed": crc_samples, "alg_bytes": alg_bytes,
                 "pipeline_GBs": round(bytes_total / args.steps / (ms_per_step * 1e-3) / 1e9, 1),
                 "kernel_ms_all": {k: round(v, 4) for k, v in kern.items()}}

@@ -102,8 +102,8 @@ ERR_NONE, ERR_CRC, ERR_TYPE, ERR_PANIC, ERR_INTERNAL = 0, 1, 2, 3, 4
 SB_OK, SB_SHORT, SB_CRC, SB_MAGIC, SB_BLOCKSIZE = 0, 1, 2, 3, 4
 E_CAPACITY = -4
 OPT_CHASE_DIRECT = 1  # bcw_ctx_set_option: k_chase direct-sum workgroup limit (0 forces the look-back)
-OPT_DECODE_CHUNKS = 3  # bcw_ctx_set_option: 1 one chunk (default), 2 two for large segments, 3 two from 128 blocks
-OPT_DECODE_PATH = 2  # bcw_ctx_set_option: 0 one launch (k_scan) when the segment fits, 1 k_chase + k_crc (default)
+OPT_DECODE_CHUNKS = 3  # bcw_ctx_set_option: retired (only 1 accepted)
+OPT_DECODE_PATH = 2  # bcw_ctx_set_option: retired (only 1 accepted: k_chase + k_crc)
 E_IO = -6
 ENC_COMPACT, ENC_HINT = 0, 1
 ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC, ENC_ERR_TABLE, ENC_ERR_STALE = 0, 1, 2, 3, 4, 5

@@ -300,7 +300,36 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
     image[kLdsSlice + kLdsFwd + i] = carry[i];
     image[kLdsSlice + kLdsFwd + 128 + i] = half[i];
   }
-  bool ok = hipMalloc(&c->tabs.slice, slice.size() * 4) == hipSuccess &&
+  std::vector<uint32_t> image2(kS2Image);
+  {  // stream verify (bcw_internal.h kS2*): slice rows with the shifted tables, lane operators, split operators
+    uint32_t tk[4][256], t0[256], img[32], nib[128], step[32], m[32];
+    byte_table(t0);
+    memcpy(tk[0], t0, sizeof t0);
+    for (int k = 1; k < 4; ++k)
+      for (int e = 0; e < 256; ++e) tk[k][e] = (tk[k - 1][e] >> 8) ^ t0[tk[k - 1][e] & 0xffu];
+    uint32_t sh[32];
+    shift_basis(t0, kSChunk - kSPiece, sh);
+    for (int e = 0; e < 256; ++e)
+      for (int s = 0; s < 4; ++s)
+        for (int cp = 0; cp < 8; ++cp) {
+          image2[e * 64 + s * 8 + cp] = tk[3 - s][e];
+          image2[e * 64 + 32 + s * 8 + cp] = apply_basis(sh, tk[3 - s][e]);
+        }
+    shift_basis(t0, kSPiece, step);
+    for (int i = 0; i < 32; ++i) m[i] = 1u << i;  // identity for lane 63
+    for (int l = 63; l >= 0; --l) {
+      nibble_image(m, nib);
+      for (int k = 0; k < 128; ++k) image2[kS2Slice + k * 64 + l] = nib[k];
+      for (int i = 0; i < 32; ++i) m[i] = apply_basis(step, m[i]);
+    }
+    for (int k = 0; k < kSPW; ++k) {
+      shift_basis(t0, 4u * (kSPW - k) + (kSChunk - kSPiece), img);
+      nibble_image(img, image2.data() + kS2Slice + kS2Lop + k * 128);
+    }
+  }
+  bool ok = hipMalloc(&c->tabs.lds_image2, image2.size() * 4) == hipSuccess &&
+            hipMemcpy(c->tabs.lds_image2, image2.data(), image2.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+  ok = ok && hipMalloc(&c->tabs.slice, slice.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.fwd, fwd.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.carry, carry.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.half, half.size() * 4) == hipSuccess &&
@@ -333,12 +362,7 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.frags);
   (void)hipFree(s.misc);
   (void)hipFree(s.equeue);
-  (void)hipFree(s.lbw);
-  (void)hipFree(s.pwin);
-  Scratch z{};  // the chunk streams and events live as long as the context (bcw_ctx_destroy)
-  for (int i = 0; i < 2; ++i) z.cs[i] = s.cs[i];
-  for (int i = 0; i < 4; ++i) z.cev[i] = s.cev[i];
-  s = z;
+  s = Scratch{};
 }
 
 static void free_enc_scratch(EncScratch& e) {
@@ -359,13 +383,7 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   if (!c) return BCW_E_INVAL;
   DeviceGuard dg(c->device);
   if (c->cur) (void)hipStreamSynchronize(c->cur);
-  for (hipStream_t cs : c->s.cs)
-    if (cs) (void)hipStreamSynchronize(cs);
   free_scratch(c->s);
-  for (hipEvent_t& e : c->s.cev)
-    if (e) { (void)hipEventDestroy(e); e = nullptr; }
-  for (hipStream_t& cs : c->s.cs)
-    if (cs) { (void)hipStreamDestroy(cs); cs = nullptr; }
   free_enc_scratch(c->es);
   if (c->es.aux) (void)hipStreamSynchronize(c->es.aux);
   if (c->es.ev_scan) (void)hipEventDestroy(c->es.ev_scan);
@@ -383,6 +401,7 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   (void)hipFree(c->tabs.half);
   (void)hipFree(c->tabs.initc);
   (void)hipFree(c->tabs.lds_image);
+  (void)hipFree(c->tabs.lds_image2);
   (void)hipFree(c->d_seg);
   (void)hipFree(c->d_tab_mem);
   (void)hipFree(c->d_result);
@@ -413,14 +432,12 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   const uint64_t nb = std::max(nblocks, s.nblocks_cap);
   const uint64_t fc = std::max(frag_cap, s.frag_cap);
   free_scratch(s);
-  // look-back words: one per 64-block k_chase workgroup, or one per k_scan workgroup (one per CU)
+  // look-back words: one per 64-block k_chase workgroup
   const uint64_t nwg = std::max<uint64_t>(nb / 64 + 2, (uint64_t)c->num_cus + 2);
   bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.rbase, (nb + 1) * 4) == hipSuccess &&
             hipMalloc(&s.bsum, (nb + 1) * sizeof(uint2)) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
             hipMalloc(&s.lbe, nwg * 8) == hipSuccess && hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
-            hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess && hipMalloc(&s.equeue, 8 * 128) == hipSuccess &&
-            hipMalloc(&s.lbw, nwg * 8) == hipSuccess &&
-            hipMalloc(&s.pwin, (uint64_t)c->num_cus * scan_unit_stride(nb, (uint64_t)c->num_cus) * 256) == hipSuccess;
+            hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess && hipMalloc(&s.equeue, 8 * 128) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;
   s.frag_cap = fc;
@@ -428,16 +445,12 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   s.tickets = 0;
   s.epoch = 1;
   s.chase_direct = c->chase_direct;
-  s.scan = c->scan;
-  s.chunks = c->chunks;
   // on the codec's stream: a null-stream hipMemset is not ordered before kernels on a non-blocking
   // stream, and a look-back word zeroed after k_chase published it would never be seen again
   // misc[15] (the first unknown-type fragment, an atomicMin in k_chase) starts at UINT64_MAX; every decode's
   // finalizer resets it for the next one
-  // k_scan has no k_chase in front to reset misc[0] (first bad record) and misc[14] (first CRC failure): they start
-  // at UINT64_MAX too
+  // misc[0] (first bad record) and misc[14] (first CRC failure) start at UINT64_MAX too
   if (hipMemsetAsync(s.lb, 0, nwg * 8, c->cur) != hipSuccess || hipMemsetAsync(s.lbe, 0, nwg * 8, c->cur) != hipSuccess ||
-      hipMemsetAsync(s.lbw, 0, nwg * 8, c->cur) != hipSuccess ||
       hipMemsetAsync(s.misc, 0, 16 * sizeof(uint64_t), c->cur) != hipSuccess ||
       hipMemsetAsync(s.misc + 14, 0xff, 2 * sizeof(uint64_t), c->cur) != hipSuccess ||
       hipMemsetAsync(s.misc, 0xff, sizeof(uint64_t), c->cur) != hipSuccess) {
@@ -503,7 +516,7 @@ int bcw_decode_fragments_async(bcw_ctx* c, const bcw_frag_table* d_frags) {
                                                                                                   : BCW_E_HIP;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "k_scan", "k_enc_prep", "k_enc_scan", "k_events",
+static const char* kKernelNames[K_NUM] = {"k_chase", "k_crc", "(retired)", "k_enc_prep", "k_enc_scan", "k_events",
                                           "k_write", "k_hint_layout", "k_events_hint"};
 
 int bcw_ctx_reserve_fragments(bcw_ctx* c, uint64_t n) {
@@ -520,16 +533,9 @@ int bcw_ctx_set_option(bcw_ctx* c, int option, uint64_t value) {
       c->s.chase_direct = (uint32_t)value;
       c->chase_direct = (uint32_t)value;
       return BCW_OK;
-    case BCW_OPT_DECODE_PATH:
-      if (value > 1) return BCW_E_INVAL;
-      c->s.scan = value == 0 ? 1u : 0u;
-      c->scan = c->s.scan;
-      return BCW_OK;
+    case BCW_OPT_DECODE_PATH:    // retired options (bcw.h): only their one remaining value is accepted
     case BCW_OPT_DECODE_CHUNKS:
-      if (value < 1 || value > 3) return BCW_E_INVAL;
-      c->s.chunks = (uint32_t)value;
-      c->chunks = (uint32_t)value;
-      return BCW_OK;
+      return value == 1 ? BCW_OK : BCW_E_INVAL;
     default:
       return BCW_E_INVAL;
   }

@@ -37,6 +37,7 @@ struct Tables {
   uint32_t* half;    // [8][16] A_{8*64} (nibble images)
   uint32_t* initc;   // [kBlock+1] A_{8L}(0xFFFFFFFF)
   uint32_t* lds_image;  // k_crc's LDS table image, laid out exactly as in LDS (see kLdsImage)
+  uint32_t* lds_image2; // the stream verify's LDS image (kS2Image)
   uint32_t* enc_ops;    // [kEncOpsWords] encode shift operators (nibble images, see build_enc_ops)
   uint32_t* pow2;       // [kPow2Ops][8][16] A_{8 * 2^k} (nibble images), k < 16: shifts by any distance < 64 KiB
 };
@@ -51,24 +52,20 @@ constexpr int kLdsSlice = 256 * 64;  // slice-by-4 rows (crc_window)
 constexpr int kLdsFwd = 8 * 16 * 64;
 constexpr int kLdsOps = 2 * 8 * 16;
 constexpr int kLdsImage = kLdsSlice + kLdsFwd + kLdsOps;
+// k_crc stream verify (bcw_decode.hip, stream_verify): absolute 1 KiB chunks, 16 B per lane (one fully contiguous
+// load per chunk). LDS image (dwords): slice-by-4 rows of 256 B {T3, T2, T1, T0} x 8 copies then the shifted tables
+// T'_k (a byte followed by k + 1008 zero bytes) x 8 copies; the lane operators G_l = A_{8*16*(63-l)} transposed to
+// [8][16][64 lanes]; the split operators A_{8*(4*(4-k) + 1008)} for k = 0..3.
+constexpr int kSPiece = 16;
+constexpr int kSChunk = 64 * kSPiece;
+constexpr int kSPW = kSPiece / 4;  // words per lane
+constexpr int kS2Slice = 256 * 64, kS2Lop = 8 * 16 * 64, kS2Kop = kSPW * 128;
+constexpr int kS2Image = kS2Slice + kS2Lop + kS2Kop;
 #ifndef BCW_CRC_WAVES
 #define BCW_CRC_WAVES 16
 #endif
 constexpr int kCrcWaves = BCW_CRC_WAVES;  // waves per k_crc workgroup (one workgroup per CU)
 constexpr int kCrcThreads = kCrcWaves * 64;
-#ifndef BCW_SCAN_WAVES
-#define BCW_SCAN_WAVES 12
-#endif
-constexpr int kScanWaves = BCW_SCAN_WAVES;  // waves per k_scan workgroup (one workgroup per CU; 170 VGPRs at 12)
-constexpr int kScanThreads = kScanWaves * 64;
-// k_scan: blocks per workgroup at most (one chaser lane each; the last kScanWriters waves write the prefix rows and
-// are never chasers)
-constexpr int kScanWriters = 2;
-constexpr uint32_t kScanMaxBlocks = 64u * (kScanWaves - kScanWriters);
-// k_scan prefix rows per workgroup (units of 64 windows: 4 per block, +1 for a window straddling the range start)
-inline uint32_t scan_unit_stride(uint64_t nblocks, uint64_t grid) {
-  return (uint32_t)(((nblocks + grid - 1) / grid) * (kBlock / 8192) + 2);
-}
 
 struct Scratch {
   uint64_t nblocks_cap = 0;
@@ -85,17 +82,11 @@ struct Scratch {
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
   uint32_t* equeue = nullptr;  // [8 x 32] k_crc emission work-queue heads, one 128 B line per XCD
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
-  uint64_t* lbw = nullptr;     // [nlb] k_scan: per-workgroup "written" words (zeroed at allocation)
-  uint32_t* pwin = nullptr;    // k_scan: per-window prefixes, [workgroups][scan_unit_stride][64]
-  uint32_t scan = 0;           // BCW_OPT_DECODE_PATH: 1 = one launch (k_scan) when the segment fits, 0 = k_chase + k_crc
-  uint32_t chunks = 1;         // BCW_OPT_DECODE_CHUNKS: 1 one chunk, 2 / 3 two (see bcw.h)
-  hipStream_t cs[2] = {};      // the chunks' k_crc streams, and their events (chase done, k_crc done)
-  hipEvent_t cev[4] = {};
 };
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
 // stream around every kernel of the pipeline.
-enum KernelId { K_CHASE = 0, K_CRC, K_SCAN, K_ENC_PREP, K_ENC_SCAN, K_ENC_EVENTS, K_ENC_WRITE, K_ENC_HINT_LAYOUT,
+enum KernelId { K_CHASE = 0, K_CRC, K_RETIRED, K_ENC_PREP, K_ENC_SCAN, K_ENC_EVENTS, K_ENC_WRITE, K_ENC_HINT_LAYOUT,
                 K_ENC_EVENTS_HINT, K_NUM };
 struct Prof {
   uint32_t mask = 0;   // bit k: time kernel id k
@@ -237,8 +228,6 @@ struct bcw_ctx {
   bcw_index_result* d_ires = nullptr;  // sync index calls
   uint32_t last_start_off = 0;
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // BCW_OPT_CHASE_DIRECT
-  uint32_t scan = 0;                             // BCW_OPT_DECODE_PATH
-  uint32_t chunks = 1;                           // BCW_OPT_DECODE_CHUNKS
   uint64_t last_nfrag_cap = 0;
   bcw::Prof prof;
 };

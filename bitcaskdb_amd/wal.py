@@ -346,7 +346,7 @@ def _frag_error(res):
     if res.err_class == L.ERR_PANIC:
         return RefPanic("slice bounds out of range (startOff beyond file size)")
     if res.err_class == L.ERR_INTERNAL:
-        raise RuntimeError("bcw decode: a k_scan wait exceeded its bound (device-side protocol failure)")
+        raise RuntimeError("bcw decode: a k_chase wait exceeded its bound (device-side protocol failure); no row was delivered")
     return None
 
 

@@ -190,17 +190,10 @@ const char* bcw_kernel_name(int kernel_id);
  *   BCW_OPT_CHASE_DIRECT  k_chase workgroups (64 blocks = 2 MiB each) up to which every workgroup sums all of its
  *                         predecessors' fragment counts directly; larger segments use the decoupled look-back.
  *                         0..BCW_CHASE_DIRECT_MAX (default BCW_CHASE_DIRECT_MAX); 0 forces the look-back at
- *                         every size (the tests drive that branch on small segments with it; with
- *                         BCW_OPT_DECODE_PATH 1, since only k_chase has it).
- *   BCW_OPT_DECODE_PATH   1 (default): two launches (k_chase + k_crc); 0: a segment of at most 640 blocks per CU
- *                         (5 GiB on 256 CUs) decodes in one launch (k_scan), larger ones in two. Both give
- *                         identical tables and results; k_scan is faster on long header chains (config C) and
- *                         slower on short ones (config B), DESIGN.md section 3.
- *   BCW_OPT_DECODE_CHUNKS 1 (default): one chunk. 2: on the two-launch path a segment of at least 128 blocks per CU
- *                         is chased and verified as two chunks, the second chunk's chase running beside the first
- *                         chunk's k_crc on the context's own streams (the call's stream waits for both); 3: two
- *                         chunks from 128 blocks on (tests). Identical results; 2 is slower on MI355X (the second
- *                         chase's header reads wait behind the first k_crc's stream: DESIGN.md section 7). */
+ *                         every size (the tests drive that branch on small segments with it).
+ *   BCW_OPT_DECODE_PATH,  retired in round 4 (the one-launch k_scan and the two-chunk decode lost to k_chase +
+ *   BCW_OPT_DECODE_CHUNKS the stream-verify k_crc on every configuration): only the value 1
+ *                         is accepted (BCW_OK, no effect), any other returns BCW_E_INVAL. */
 #define BCW_OPT_CHASE_DIRECT 1
 #define BCW_OPT_DECODE_PATH 2
 #define BCW_OPT_DECODE_CHUNKS 3

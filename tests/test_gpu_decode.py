@@ -1,7 +1,7 @@
 """GPU decode parity: libbcw.so on the MI355X against the CPU oracle, bit-exact.
 
 Every comparison goes through the C-ABI (bcw_decode_segment / bcw_decode_fragments) on cuda:0; the ctx_path tests
-run both decode paths (the one-launch k_scan and k_chase + k_crc)."""
+run on a context of their own (k_chase + k_crc)."""
 from __future__ import annotations
 
 import random

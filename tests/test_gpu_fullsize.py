@@ -13,42 +13,11 @@ import pytest
 
 import _oracle as O
 import cases
+from _parity import full_parity
 from bitcaskdb_amd import _lib as L
 
 pytestmark = pytest.mark.gpu
 BASE = cases.BASE
-
-
-def full_parity(ctx, data, p, name):
-    ref = O.decode(data, p["start_off"], p["base_time"], p["ns_size"], p["etag_size"], p["mode"], want_bytes=False,
-                   want_hashes=True)
-    seg = np.frombuffer(data, dtype=np.uint8)
-    got = ctx.decode(seg, p["start_off"], p["base_time"], p["ns_size"], p["etag_size"], p["mode"], with_frags=True)
-    res = got.result
-    assert res.err_class == ref.err_class, (name, res.err_class, ref.err_class)
-    if ref.err_class in (L.ERR_CRC, L.ERR_TYPE):
-        assert res.err_frag == ref.err_frag, (name, res.err_frag, ref.err_frag)
-    assert res.n_records == len(ref.recs), (name, res.n_records, len(ref.recs))
-    nf = len(ref.frags)
-    gf = got.frags
-    assert len(gf["data_off"]) >= nf
-    for col in ("data_off", "len", "stored_crc", "type", "crc_ok"):
-        np.testing.assert_array_equal(gf[col][:nf], ref.frags[col], err_msg=f"{name}: frag {col}")
-    t, r = got.table, ref.recs
-    for col in ("foff", "size", "first_frag", "emit_frag", "status", "hdr_size", "flags", "etag_off", "expire"):
-        np.testing.assert_array_equal(t[col].astype(np.uint64), r[col].astype(np.uint64), err_msg=f"{name}: {col}")
-    if p["mode"] == 0:
-        for col in ("key_len", "val_len", "meta_len"):
-            np.testing.assert_array_equal(t[col].astype(np.uint64), r[col] & 0xFFFFFFFF, err_msg=f"{name}: {col}")
-    else:
-        np.testing.assert_array_equal(t["aux0"], r["val_len"], err_msg=f"{name}: hint off")
-        np.testing.assert_array_equal(t["aux1"], r["meta_len"], err_msg=f"{name}: hint size")
-    h = O.gather_payload_hashes(seg, gf, t)
-    bad = np.nonzero(h != ref.hashes)[0]
-    assert bad.size == 0, f"{name}: {bad.size} payloads differ, first at record {bad[:1]}"
-    st = np.nonzero(r["status"] != 0)[0]
-    assert res.first_bad_record == (int(st[0]) if len(st) else -1)
-    return got, ref
 
 
 def test_config_a_64mib(ctx):
@@ -202,28 +171,16 @@ def test_config_e_compaction_2m_rebase(ctx):
     np.testing.assert_array_equal(goffs[:n], offs[:n])
 
 
-def test_config_b_two_launch(ctx_two, config_b):
-    """config B on the two-launch path in one chunk (BCW_OPT_DECODE_CHUNKS 1): every column equals the oracle's"""
-    got, _ = full_parity(ctx_two, config_b, cases.params(), "B one chunk")
-    assert got.result.err_class == 0 and got.n_records > 250000
-
-
-def test_config_b_two_chunks(ctx_chunks, config_b):
-    """config B on the two-launch path over two chunks (BCW_OPT_DECODE_CHUNKS 3)"""
-    got, _ = full_parity(ctx_chunks, config_b, cases.params(), "B two chunks")
-    assert got.result.err_class == 0 and got.n_records > 250000
-
-
-def test_config_b_one_launch(ctx_scan, config_b):
-    """config B on the one-launch path (k_scan, BCW_OPT_DECODE_PATH 0)"""
-    got, _ = full_parity(ctx_scan, config_b, cases.params(), "B k_scan")
+def test_config_b_second_context(ctx_path, config_b):
+    """config B decoded by a second context (its own scratch and tables): every column equals the oracle's"""
+    got, _ = full_parity(ctx_path, config_b, cases.params(), "B second context")
     assert got.result.err_class == 0 and got.n_records > 250000
 
 
 @pytest.mark.parametrize("where", [0.0001, 0.5])
 def test_config_c_corruption(ctx, where):
-    """config C with a flipped byte near the start (workgroup 0) and in the middle: k_scan's edge windows and
-    per-window prefixes decide the same first failing fragment as the oracle."""
+    """config C with a flipped byte near the start (workgroup 0) and in the middle: the stream verify's masked
+    chunks decide the same first failing fragment as the oracle."""
     data = bytearray(O.synth(1 << 30, 0, 42, value_mode=1))
     data[int(len(data) * where)] ^= 0x24
     got, ref = full_parity(ctx, bytes(data), cases.params(), f"C flip@{where}")

@@ -9,6 +9,7 @@ import csv
 import glob
 import json
 import os
+import importlib.util
 import statistics
 
 
@@ -34,7 +35,12 @@ def main():
     wr = per_dispatch(a.write, a.kernel, "WRITE_SIZE")
     fetch_b = 2 * statistics.median(fe) * 1024
     write_b = statistics.median(wr) * 1024
-    out = {"kernel": a.kernel, "seg_bytes": a.seg_bytes, "alg_bytes_per_launch": a.alg_bytes,
+    spec = importlib.util.spec_from_file_location(
+        "_bcw_build", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "bitcaskdb_amd", "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    out = {"kernel": a.kernel, "decode_src_sha16": b.decode_src_sha16(), "seg_bytes": a.seg_bytes,
+           "alg_bytes_per_launch": a.alg_bytes,
            "fetch_bytes_per_launch": round(fetch_b), "write_bytes_per_launch": round(write_b),
            "hbm_bytes_per_launch": round(fetch_b + write_b),
            "traffic_over_alg": round((fetch_b + write_b) / a.alg_bytes, 4),
