@@ -322,9 +322,37 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
       for (int k = 0; k < 128; ++k) image2[kS2Slice + k * 64 + l] = nib[k];
       for (int i = 0; i < 32; ++i) m[i] = apply_basis(step, m[i]);
     }
-    for (int k = 0; k < kSPW; ++k) {
+    for (int k = 0; k < kSPW; ++k) {  // split operators as byte tables: [k][t][e] = A(e << 8t)
       shift_basis(t0, 4u * (kSPW - k) + (kSChunk - kSPiece), img);
-      nibble_image(img, image2.data() + kS2Slice + kS2Lop + k * 128);
+      for (int t = 0; t < 4; ++t)
+        for (uint32_t e = 0; e < 256; ++e)
+          image2[kS2Slice + kS2Lop + (k * 4 + t) * 256 + e] = apply_basis(img, e << (8 * t));
+    }
+    auto put_bytes = [&](int at, const uint8_t (&b)[16]) {
+      for (int w = 0; w < 4; ++w)
+        image2[at + w] = b[4 * w] | b[4 * w + 1] << 8 | b[4 * w + 2] << 16 | (uint32_t)b[4 * w + 3] << 24;
+    };
+    for (int n = 0; n < kS2GeN; ++n) {  // GE[n]: bytes q >= n
+      uint8_t b[16];
+      for (int q = 0; q < 16; ++q) b[q] = q >= n ? 0xff : 0x00;
+      put_bytes(kS2Ge + 4 * n, b);
+    }
+    for (int m = 0; m < kS2JselN; ++m) {  // JSEL[m]: perm selectors, J byte q - o at q in [o, o + 4) (o = m - 3), else 0
+      uint8_t b[16];
+      for (int q = 0; q < 16; ++q) {
+        const int p = q - (m - 3);
+        b[q] = (m < kS2JselN - 1 && p >= 0 && p < 4) ? (uint8_t)(4 + p) : 0x0c;
+      }
+      put_bytes(kS2Jsel + 4 * m, b);
+    }
+    for (int g = 0; g < kS2GapN; ++g) {  // GAP[g]: J at [o, o + 4) (o = g - 6), zeros at [o + 4, o + 7), else the byte
+      uint8_t b[16];
+      for (int q = 0; q < 16; ++q) {
+        const int p = q - (g - 6);
+        b[q] = g == kS2GapN - 1 ? (uint8_t)(q & 3) : (p >= 0 && p < 4) ? (uint8_t)(4 + p) : (p >= 4 && p < 7) ? 0x0c
+                                                                                            : (uint8_t)(q & 3);
+      }
+      put_bytes(kS2Gap + 4 * g, b);
     }
   }
   bool ok = hipMalloc(&c->tabs.lds_image2, image2.size() * 4) == hipSuccess &&
@@ -500,6 +528,8 @@ int bcw_decode_segment_async(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_
   want = std::min<uint64_t>(want, 0xfffffff0ull);
   int rc = ensure_scratch(c, nblocks, want);
   if (rc != BCW_OK) return rc;
+  c->s.test_abort_wg = c->test_abort_wg;  // one-shot (launch_decode clears the scratch copy)
+  c->test_abort_wg = 0;
   if (launch_decode(d_seg, *p, *t, d_result, c->tabs, c->s, nblocks, gen, c->cur, c->num_cus, &c->prof) !=
       hipSuccess)
     return BCW_E_HIP;
@@ -536,6 +566,10 @@ int bcw_ctx_set_option(bcw_ctx* c, int option, uint64_t value) {
     case BCW_OPT_DECODE_PATH:    // retired options (bcw.h): only their one remaining value is accepted
     case BCW_OPT_DECODE_CHUNKS:
       return value == 1 ? BCW_OK : BCW_E_INVAL;
+    case BCW_OPT_TEST_ABORT_WAIT:
+      if (value > 0xffffffffull) return BCW_E_INVAL;
+      c->test_abort_wg = value;
+      return BCW_OK;
     default:
       return BCW_E_INVAL;
   }

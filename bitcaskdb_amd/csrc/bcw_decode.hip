@@ -128,13 +128,16 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 // 27.4 -> 28.2 us, config C 83 -> 91 us.)
 // A bounded wait (k_chase's predecessor waits): every spin gives up after 200 ms (a correct wait lasts microseconds)
 // or once another wave has given up, records its site in misc[M_ABORT] and lets the kernel run to its end; the decode
-// then reports BCW_ERR_INTERNAL instead of hanging the device.
+// then reports BCW_ERR_INTERNAL instead of hanging the device. k_crc skips its CRC pass and emission over the
+// unreliable bases, and the finalizer delivers no row. A wait that gave up counts its word as 0. (BCW_OPT_TEST_ABORT_WAIT
+// makes one workgroup's Spin give up at its first step, with lim = 0.)
 struct Spin {
   uint64_t t0 = 0;
+  uint64_t lim = 20000000ull;  // 200 ms of the 100 MHz wall clock
   __device__ __forceinline__ bool go(uint64_t* misc, uint32_t site) {  // true: keep waiting
     const uint64_t t = wall_clock64();
     if (t0 == 0) t0 = t;
-    if (t - t0 < 20000000ull &&
+    if (t - t0 < lim &&
         __hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull) {
       __builtin_amdgcn_s_sleep(1);
       return true;
@@ -219,7 +222,8 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                               Frag* __restrict__ frags, uint64_t frag_cap, uint64_t* __restrict__ lb,
                                               uint64_t* __restrict__ lbe, uint64_t* __restrict__ misc,
                                               uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc,
-                                              uint32_t direct_max, uint32_t* __restrict__ equeue) {
+                                              uint32_t direct_max, uint32_t* __restrict__ equeue,
+                                              uint64_t test_abort_wg) {
   // {crc, start | len << 16} and type of each lane's headers: 9 KiB, so a k_chase workgroup fits beside a k_crc
   // workgroup (which leaves 11 KiB of the CU's LDS) when another segment's decode is in flight
   // (ABL & 256, kbench: 64 held headers per lane)
@@ -272,6 +276,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   // inclusive prefixes would otherwise serialize the workgroups.
   const uint64_t tag = epoch << 40;
   const uint64_t nwg_all = (nblocks + 63) / 64;
+  const bool force = wg + 1 == test_abort_wg;  // BCW_OPT_TEST_ABORT_WAIT (wave-uniform)
   uint64_t excl = 0, excl_e = 0;
   if (ABL & 1) {
   } else if (nwg_all <= (uint64_t)direct_max) {  // direct_max <= kDirect (bcw_ctx_set_option)
@@ -289,8 +294,9 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     for (int k = 0; k < kDirect / 64; ++k) {
       const uint64_t q = lane + 64u * k;
       Spin sp;  // bounded (BCW_ERR_INTERNAL)
-      while ((v[k] >> 40) != epoch) {
-        if (!sp.go(misc, 9)) break;
+      if (force) sp.lim = 0;
+      while (force || (v[k] >> 40) != epoch) {
+        if (!sp.go(misc, 9)) { v[k] = 0; break; }
         v[k] = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (q < wg) {
@@ -319,12 +325,13 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
       uint64_t vn = 0, ve = 0;
       if (top > lane) {
         Spin sp;
+        if (force) sp.lim = 0;
         if (!dn)
-          while (((vn = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
-            if (!sp.go(misc, 10)) break;
+          while (((vn = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch || force)
+            if (!sp.go(misc, 10)) { vn = 0; break; }
         if (!de)
-          while (((ve = __hip_atomic_load(&lbe[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch)
-            if (!sp.go(misc, 11)) break;
+          while (((ve = __hip_atomic_load(&lbe[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch || force)
+            if (!sp.go(misc, 11)) { ve = 0; break; }
       }
       auto step = [&](uint64_t v, bool& done, uint64_t& acc) {
         if (done) return;
@@ -750,11 +757,12 @@ __device__ __forceinline__ void finalize(const EmitArgs& A, uint64_t nblocks, ui
   const uint64_t bad_type = __hip_atomic_load(&misc[M_BAD_TYPE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t fb = __hip_atomic_load(&misc[M_FIRST_BAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t nfr = __hip_atomic_load(&misc[M_NFRAGS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t abort_site = __hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t err = bad_crc < bad_type ? bad_crc : bad_type;
   // records before fragment `lim` (the first failing one, or the fragment capacity of a decode to be retried)
   uint64_t lim = err < frag_cap ? err : frag_cap;
   uint64_t nrec = __hip_atomic_load(&misc[M_NE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (lim < nfr) {
+  if (lim < nfr && abort_site == 0ull) {
     // the block holding fragment lim: the last b with fbase[b] <= lim (64-ary search)
     uint64_t lo = 0, hi = nblocks;
     while (hi - lo > 1) {
@@ -784,7 +792,6 @@ __device__ __forceinline__ void finalize(const EmitArgs& A, uint64_t nblocks, ui
   // a last block of 1..6 bytes makes the reference iterator panic after every earlier record
   // (wal_iterator.go:62-76 re-slices a header from its stale buffer, then buf[7:7+negative])
   if (r.err_class == BCW_ERR_NONE && tail_panic) r.err_class = BCW_ERR_PANIC;
-  const uint64_t abort_site = __hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (abort_site != 0ull) {
     // a wait gave up: the bases (and so every row) may come from stale look-back words. Deliver no row at all, so
     // that no consumer (the index puts, the compaction filter and encode, the host replay) applies one.
@@ -794,7 +801,7 @@ __device__ __forceinline__ void finalize(const EmitArgs& A, uint64_t nblocks, ui
     nrec = 0;
   }
   r.err_file_off = 0;
-  if (err != ~0ull && err < frag_cap) {
+  if (err != ~0ull && err < frag_cap && abort_site == 0ull) {
     const Frag f = A.frags[err];
     r.err_file_off = (uint64_t)A.p.start_off + (uint64_t)f.blk * kBlock + f.start - kHdr;
   }
@@ -869,86 +876,64 @@ __device__ __forceinline__ uint32_t slice4_step2(const uint8_t* __restrict__ tb,
   const uint32_t a3 = *reinterpret_cast<const uint32_t*>(tb + __builtin_amdgcn_perm(x, sl.base, sl.sel[3]) + o);
   return xor3(xor3(a0, a1, a2), a3, next);
 }
-// A_{8*1008}(A_128(seed) ^ R(piece)); CAP: also the unshifted state after word K (1 <= K < kSPW, wave-uniform) in cap
+// A_{8*1008}(A_128(seed) ^ R(piece)); CAP: also the unshifted state after word K (1 <= K < kSPW, wave-uniform)
 template <bool CAP>
 __device__ __forceinline__ uint32_t chain_piece2(const uint8_t* __restrict__ tb, const SliceLane2& sl, uint32_t seed,
                                                  const uint32_t (&w)[kSPW], uint32_t K = 0, uint32_t* cap = nullptr) {
   uint32_t x = seed ^ w[0];
+  uint32_t st[kSPW - 1];
 #pragma unroll
   for (int q = 0; q < kSPW - 1; ++q) {
     x = slice4_step2<false>(tb, sl, x, w[q + 1]);
-    if (CAP && K == (uint32_t)q + 1u) *cap = x ^ w[q + 1];
+    if (CAP) st[q] = x ^ w[q + 1];
   }
+  if (CAP) *cap = K == 1u ? st[0] : (K == 2u ? st[1] : st[2]);  // (uniform K: two selects, no branch)
   return slice4_step2<true>(tb, sl, x, 0u);
 }
 
 // chunks that can hold a fragment's data or check word: every byte of them lies before seg_len + 4
 __device__ __forceinline__ uint64_t c_safe_bound(uint64_t seg_len) { return (seg_len + 4u + kSChunk - 1u) / kSChunk; }
 
-// x = w with only the bytes of [pa, pb) and [pc, kSChunk) kept and J written at [pb, pb + 4) (chunk-relative, wave-
-// uniform, clamped to [-64, 4096]). Whole words by a keep pattern per lane, then the (at most four) words that hold
-// a boundary fixed in the one lane that owns each.
+// the 16 B select entry of lane l for a boundary at chunk-relative byte P (table of n entries, index clamped)
+__device__ __forceinline__ uint4 lds_entry(const uint32_t* __restrict__ tab, uint32_t idx) {
+  return *reinterpret_cast<const uint4*>(tab + 4u * idx);
+}
+// Fragment-end masks: x_j = v_perm(J, w_j, S_j), byte selectors S from LDS tables indexed by the boundary's offset in
+// the lane's piece (no lane compares, no branches). The usual end: data on both sides of the 7 bytes [pb, pb + 7)
+// (J over the next header's CRC field, its length and type bytes zeroed).
+__device__ __forceinline__ void mask_gap(uint32_t (&x)[kSPW], const uint32_t (&w)[kSPW], int32_t pb, uint32_t J,
+                                         uint32_t lane, const uint32_t* __restrict__ lds) {
+  const uint32_t g = min((uint32_t)(pb - (int32_t)(kSPiece * lane) + 6), (uint32_t)(kS2GapN - 1));
+  const uint4 S = lds_entry(lds + kS2Gap, g);
+  x[0] = __builtin_amdgcn_perm(J, w[0], S.x);
+  x[1] = __builtin_amdgcn_perm(J, w[1], S.y);
+  x[2] = __builtin_amdgcn_perm(J, w[2], S.z);
+  x[3] = __builtin_amdgcn_perm(J, w[3], S.w);
+}
+// The general end: only the bytes of [pa, pb) and [pc, kSChunk) kept and J written at [pb, pb + 4) (chunk-relative,
+// wave-uniform, clamped to [-64, 4096]): keep = (GE[pa] & ~GE[pb]) | GE[pc], the others J's bytes or 0 (JSEL).
 __device__ __forceinline__ void mask_chunk(uint32_t (&x)[kSPW], const uint32_t (&w)[kSPW], int32_t pa, int32_t pb,
-                                           int32_t pc, uint32_t J, uint32_t lane) {
-  const int32_t u = (int32_t)(kSPW * lane);
-  const int32_t ga = pa >> 2, gb = (pb + 7) >> 2, gc = pc >> 2;  // word ranges [ga, gb) and [gc, ...)
-  const uint32_t lo1 = (uint32_t)min(max(ga - u, 0), kSPW), hi1 = (uint32_t)min(max(gb - u, 0), kSPW);
-  const uint32_t lo2 = (uint32_t)min(max(gc - u, 0), kSPW);
-  const uint32_t keep = (((1u << hi1) - 1u) & ~((1u << lo1) - 1u)) | (0xffu << lo2);
-#pragma unroll
-  for (int j = 0; j < kSPW; ++j) x[j] = w[j] & (uint32_t)__builtin_amdgcn_sbfe((int32_t)keep, j, 1);
-  auto fix = [&](int32_t wi, auto f) {  // word wi of the chunk (uniform) in its lane
-    const uint32_t L = (uint32_t)wi / kSPW, jj = (uint32_t)wi % kSPW;
-    const bool me = lane == L;
-#pragma unroll
-    for (int j = 0; j < kSPW; ++j)
-      if (jj == (uint32_t)j) x[j] = me ? f(x[j]) : x[j];
+                                           int32_t pc, uint32_t J, uint32_t lane, const uint32_t* __restrict__ lds) {
+  const int32_t q = (int32_t)(kSPiece * lane);
+  const uint4 A = lds_entry(lds + kS2Ge, (uint32_t)min(max(pa - q, 0), kS2GeN - 1));
+  const uint4 B = lds_entry(lds + kS2Ge, (uint32_t)min(max(pb - q, 0), kS2GeN - 1));
+  const uint4 C = lds_entry(lds + kS2Ge, (uint32_t)min(max(pc - q, 0), kS2GeN - 1));
+  const uint4 Js = lds_entry(lds + kS2Jsel, min((uint32_t)(pb - q + 3), (uint32_t)(kS2JselN - 1)));
+  auto one = [&](uint32_t wj, uint32_t a, uint32_t b, uint32_t c, uint32_t js) {
+    const uint32_t keep = __builtin_amdgcn_bitop3_b32(a, b, c, 0xBA);               // (a & ~b) | c
+    const uint32_t sel = __builtin_amdgcn_bitop3_b32(keep, 0x03020100u, js, 0xCA);  // keep ? identity : js
+    return __builtin_amdgcn_perm(J, wj, sel);
   };
-  if (pa > 0 && pa < kSChunk && (pa & 3)) {
-    const uint32_t m = ~0u << (8 * (pa & 3));
-    fix(pa >> 2, [&](uint32_t v) { return v & m; });
-  }
-  const uint32_t r = (uint32_t)pb & 3u;
-  if (pb >= 0 && pb < kSChunk) {
-    const uint32_t m = (1u << (8 * r)) - 1u, jl = J << (8 * r);
-    fix(pb >> 2, [&](uint32_t v) { return (v & m) | jl; });
-  }
-  if (r != 0u && pb >= -4 && pb < kSChunk - 4) {  // J's high bytes start the next word (header bytes after it: 0)
-    const uint32_t jh = J >> (32 - 8 * r);
-    fix((pb >> 2) + 1, [&](uint32_t) { return jh; });
-  }
-  if (pc > 0 && pc < kSChunk && (pc & 3)) {
-    const uint32_t m = ~0u << (8 * (pc & 3));
-    fix(pc >> 2, [&](uint32_t v) { return v & m; });
-  }
+  x[0] = one(w[0], A.x, B.x, C.x, Js.x);
+  x[1] = one(w[1], A.y, B.y, C.y, Js.y);
+  x[2] = one(w[2], A.z, B.z, C.z, Js.z);
+  x[3] = one(w[3], A.w, B.w, C.w, Js.w);
 }
-
-// word wi of the chunk (wave-uniform) replaced by f(word) in the lane that holds it
-template <typename F>
-__device__ __forceinline__ void fix_word(uint32_t (&x)[kSPW], int32_t wi, uint32_t lane, F&& f) {
-  const uint32_t L = (uint32_t)wi / kSPW, jj = (uint32_t)wi % kSPW;
-  const bool me = lane == L;
-#pragma unroll
-  for (int j = 0; j < kSPW; ++j)
-    if (jj == (uint32_t)j) x[j] = me ? f(x[j]) : x[j];
-}
-// the usual fragment end: data on both sides of the 7 bytes [pb, pb + 7) (J over the next header's CRC field, then
-// its length and type bytes zeroed); 0 <= pb, pb + 7 <= kSChunk
-__device__ __forceinline__ void mask_gap(uint32_t (&x)[kSPW], int32_t pb, uint32_t J, uint32_t lane) {
-  const uint32_t r = (uint32_t)pb & 3u;
-  const int32_t wb = pb >> 2;
-  const uint32_t lo = (1u << (8 * r)) - 1u, jl = J << (8 * r);
-  fix_word(x, wb, lane, [&](uint32_t v) { return (v & lo) | jl; });
-  if (r == 0u) {
-    fix_word(x, wb + 1, lane, [&](uint32_t v) { return v & 0xff000000u; });
-  } else {
-    const uint32_t jh = J >> (32 - 8 * r);
-    fix_word(x, wb + 1, lane, [&](uint32_t) { return jh; });
-    if (r >= 2u) {
-      const uint32_t keep = ~((1u << (8 * (r - 1u))) - 1u);
-      fix_word(x, wb + 2, lane, [&](uint32_t v) { return v & keep; });
-    }
-  }
+// a split operator of the byte tables (kS2Kop): 4 lookups
+__device__ __forceinline__ uint32_t apply_op_b(const uint32_t* __restrict__ t, uint32_t x) {
+  const uint32_t a0 = t[x & 0xffu], a1 = t[256 + ((x >> 8) & 0xffu)];
+  const uint32_t a2 = t[512 + ((x >> 16) & 0xffu)], a3 = t[768 + (x >> 24)];
+  return xor3(a0, a1, a2) ^ a3;
 }
 
 // Verify fragments [f0, f0 + nfr) of the fragment table (one wave). lds: the kS2Image tables; frd: the fragment
@@ -1038,13 +1023,10 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
       const bool next_in = closes && fn.gs < C1 && fn.ge >= C1;
       uint32_t x[kSPW];
       const int32_t pa = rel(fc.gs), pb = rel(fc.ge);
-      if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr) {  // the usual case: a header between two data runs
-#pragma unroll
-        for (int k = 0; k < kSPW; ++k) x[k] = w[k];
-        mask_gap(x, pb, fc.J, lane);
-      } else {
-        mask_chunk(x, w, pa, pb, next_in ? rel(fn.gs) : 4096, fc.J, lane);
-      }
+      if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr)  // the usual case: a header between two data runs
+        mask_gap(x, w, pb, fc.J, lane, lds);
+      else
+        mask_chunk(x, w, pa, pb, next_in ? rel(fn.gs) : 4096, fc.J, lane, lds);
       if (!closes) {
         H = chain_piece2<false>(tb, sl, H, x);
         return;
@@ -1057,7 +1039,7 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
       // K == kSPW: lane Lf's part ends with its piece (A = s8, as for the lanes before it)
       const bool full = lane < Lf || (lane == Lf && K == (uint32_t)kSPW);
       const bool split = lane == Lf && K != 0u;  // (K == 0: the lanes from Lf on hold none of its bytes)
-      const uint32_t A = full ? s8 : apply_op(s_kop + (split ? K : 0u) * 128u, split ? cap : H);
+      const uint32_t A = full ? s8 : apply_op_b(s_kop + (split ? K : 0u) * 1024u, split ? cap : H);
       const uint32_t T = wave_scan_z(apply_fwd(s_lop, lane, A), [](uint32_t a, uint32_t b) { return a ^ b; });
       const bool ok = __builtin_amdgcn_readlane(T, 63) == 0u;
       okm |= (uint64_t)(ok ? 1u : 0u) << (i & 63u);
@@ -1155,6 +1137,10 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint64_t f0 = fbase[b0];
   uint64_t f1 = fbase[b1];
   if (f1 > frag_cap) f1 = frag_cap;
+  // a k_chase wait gave up (Spin): the bases are unreliable, so no fragment is read and no row written
+  const bool aborted = __builtin_amdgcn_readfirstlane(
+                           (uint32_t)__hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+  if (aborted) f1 = f0;
   {  // table image -> LDS: all 16 B loads in flight before the first store
     constexpr uint32_t kVec = kS2Image / 4;
     constexpr int kFull = (int)(kVec / kCrcThreads);
@@ -1195,7 +1181,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   // its waves as they finish their CRC passes, so the early finishers emit for the late ones (ItemMeta). The next
   // item is taken and its block data requested while this item's fragment descriptors are in flight, so an item
   // costs two dependent round trips (descriptors, record prefixes) ----
-  if (!(ABL & 8) && !(A.kb_flags & 1u)) {
+  if (!(ABL & 8) && !(A.kb_flags & 1u) &&
+      __builtin_amdgcn_readfirstlane(
+          (uint32_t)__hip_atomic_load(&T.misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
     const uint64_t cb0t = T.cb0, cb1t = T.cb1, cnt = cb1t - cb0t, fcap = T.frag_cap;
     // blocks per item for ~64 fragments each
     const uint64_t fc0 = A.fbase[cb0t], fc1 = A.fbase[cb1t];
@@ -1283,7 +1271,8 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   pr.begin(K_CHASE, stream, ev);
   k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
                                         s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch, tabs.initc, s.chase_direct,
-                                        s.equeue);
+                                        s.equeue, s.test_abort_wg);
+  s.test_abort_wg = 0;
   pr.end(K_CHASE, stream, ev);
   s.tickets += nb_grid;
   if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse

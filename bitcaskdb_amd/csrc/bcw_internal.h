@@ -55,12 +55,16 @@ constexpr int kLdsImage = kLdsSlice + kLdsFwd + kLdsOps;
 // k_crc stream verify (bcw_decode.hip, stream_verify): absolute 1 KiB chunks, 16 B per lane (one fully contiguous
 // load per chunk). LDS image (dwords): slice-by-4 rows of 256 B {T3, T2, T1, T0} x 8 copies then the shifted tables
 // T'_k (a byte followed by k + 1008 zero bytes) x 8 copies; the lane operators G_l = A_{8*16*(63-l)} transposed to
-// [8][16][64 lanes]; the split operators A_{8*(4*(4-k) + 1008)} for k = 0..3.
+// [8][16][64 lanes]; the split operators A_{8*(4*(4-k) + 1008)} (k = 0..3) as byte tables [k][byte t][256]; and the
+// per-lane byte-select tables of the fragment-end masks (16 B entries, one per lane offset): GE (bytes >= n), JSEL
+// (the check word's bytes at piece offset m - 3), GAP (check word at piece offset g - 6, then 3 zero bytes).
 constexpr int kSPiece = 16;
 constexpr int kSChunk = 64 * kSPiece;
 constexpr int kSPW = kSPiece / 4;  // words per lane
-constexpr int kS2Slice = 256 * 64, kS2Lop = 8 * 16 * 64, kS2Kop = kSPW * 128;
-constexpr int kS2Image = kS2Slice + kS2Lop + kS2Kop;
+constexpr int kS2Slice = 256 * 64, kS2Lop = 8 * 16 * 64, kS2Kop = kSPW * 4 * 256;
+constexpr int kS2GeN = 17, kS2JselN = 20, kS2GapN = 23;  // entries (4 dwords each)
+constexpr int kS2Ge = kS2Slice + kS2Lop + kS2Kop, kS2Jsel = kS2Ge + 4 * kS2GeN, kS2Gap = kS2Jsel + 4 * kS2JselN;
+constexpr int kS2Image = kS2Gap + 4 * kS2GapN + 4;  // (+ pad to 16 B)
 #ifndef BCW_CRC_WAVES
 #define BCW_CRC_WAVES 16
 #endif
@@ -82,6 +86,7 @@ struct Scratch {
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
   uint32_t* equeue = nullptr;  // [8 x 32] k_crc emission work-queue heads, one 128 B line per XCD
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
+  uint64_t test_abort_wg = 0;  // BCW_OPT_TEST_ABORT_WAIT for the next launch only (k_chase workgroup + 1; 0: none)
 };
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
@@ -228,6 +233,7 @@ struct bcw_ctx {
   bcw_index_result* d_ires = nullptr;  // sync index calls
   uint32_t last_start_off = 0;
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // BCW_OPT_CHASE_DIRECT
+  uint64_t test_abort_wg = 0;                    // BCW_OPT_TEST_ABORT_WAIT (one-shot)
   uint64_t last_nfrag_cap = 0;
   bcw::Prof prof;
 };

@@ -68,7 +68,7 @@ extern "C" {
 #define BCW_ERR_CRC 1   /* ErrWalMismatchCRC */
 #define BCW_ERR_TYPE 2  /* ErrWalUnknownRecordType */
 #define BCW_ERR_PANIC 3 /* startOff > file size: the reference panics slicing i.buf[:negative] */
-#define BCW_ERR_INTERNAL 4 /* the one-launch decode gave up on an internal wait (a library bug): no valid result */
+#define BCW_ERR_INTERNAL 4 /* the decode gave up on an internal wait (a library bug): no valid result, no rows */
 
 /* ---- super block load result (wal.go:362-398) ---- */
 #define BCW_SB_OK 0
@@ -193,10 +193,14 @@ const char* bcw_kernel_name(int kernel_id);
  *                         every size (the tests drive that branch on small segments with it).
  *   BCW_OPT_DECODE_PATH,  retired in round 4 (the one-launch k_scan and the two-chunk decode lost to k_chase +
  *   BCW_OPT_DECODE_CHUNKS the stream-verify k_crc on every configuration): only the value 1
- *                         is accepted (BCW_OK, no effect), any other returns BCW_E_INVAL. */
+ *                         is accepted (BCW_OK, no effect), any other returns BCW_E_INVAL.
+ *   BCW_OPT_TEST_ABORT_WAIT  test only: in the NEXT decode on the context, the k_chase workgroup value - 1 gives up
+ *                         its predecessor wait at once (0: none, the default), as a wait that ran past its 200 ms
+ *                         bound would; that decode reports BCW_ERR_INTERNAL with no rows. One-shot. */
 #define BCW_OPT_CHASE_DIRECT 1
 #define BCW_OPT_DECODE_PATH 2
 #define BCW_OPT_DECODE_CHUNKS 3
+#define BCW_OPT_TEST_ABORT_WAIT 4
 #define BCW_CHASE_DIRECT_MAX 1024
 int bcw_ctx_set_option(bcw_ctx* ctx, int option, uint64_t value);
 /* Size the context's fragment scratch for at least n fragments on the next decode (after a decode

@@ -185,3 +185,32 @@ def test_config_c_corruption(ctx, where):
     data[int(len(data) * where)] ^= 0x24
     got, ref = full_parity(ctx, bytes(data), cases.params(), f"C flip@{where}")
     assert got.result.err_class in (L.ERR_CRC, L.ERR_TYPE)
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_forced_wait_abort(direct):
+    """a k_chase predecessor wait that gives up (BCW_OPT_TEST_ABORT_WAIT makes workgroup 5 of a 64 MiB segment give
+    up at its first step, as a wait past its 200 ms bound would; its bases are then computed from zeroed words):
+    the decode reports BCW_ERR_INTERNAL at the wait site with no row, k_crc reads no fragment over the bad bases,
+    and the next decode on the same context is bit-exact against the oracle (wal_iterator.go:44,79-82: no partial
+    result is ever delivered as valid)."""
+    from bitcaskdb_amd import Context
+    c = Context(0)
+    try:
+        if not direct:
+            c.set_option(L.OPT_CHASE_DIRECT, 0)
+        data = O.synth(64 << 20, 0, 46)
+        p = cases.params()
+        seg = np.frombuffer(data, dtype=np.uint8)
+        c.set_option(L.OPT_TEST_ABORT_WAIT, 6)
+        got = c.decode(seg, p["start_off"], p["base_time"], p["ns_size"], p["etag_size"], p["mode"])
+        r = got.result
+        assert r.err_class == L.ERR_INTERNAL
+        assert r.err_frag == 9 if direct else r.err_frag in (10, 11)  # the site (the largest one that gave up)
+        assert r.n_records == 0 and r.n_records_total == 0 and r.retry_frag_capacity == 0
+        assert r.first_bad_record == -1 and r.err_file_off == 0
+        # one-shot: the next decode on the same context is exact
+        full_parity(c, data, p, "after abort")
+        c.sync()
+    finally:
+        c.close()
