@@ -943,12 +943,13 @@ __device__ __forceinline__ uint32_t apply_op_b(const uint32_t* __restrict__ t, u
 // merge the paths' counts pessimistically: it then drained nearly every chunk load in flight, vmcnt(1)).
 // Positions are 32-bit, relative to the wave's first chunk (a wave's blocks span far less than 1 GiB).
 // SV: kbench ablations (0 in the product): 1 no chains (words folded by xor), 2 no loads, 4 every chunk takes the
-// fast path (verdicts meaningless)
-template <int D, int SV = 0>
+// fast path (verdicts meaningless). PB: issue-priority balancing (below).
+template <int D, int SV = 0, bool PB = true>
 __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
                                               Frag* __restrict__ frags, const uint4* __restrict__ frd, uint64_t f0,
                                               uint32_t nfr, const uint32_t* __restrict__ lds, uint32_t lane,
-                                              uint64_t* __restrict__ misc) {
+                                              uint64_t* __restrict__ misc, uint32_t* __restrict__ s_rem,
+                                              uint32_t wslot) {
   if (nfr == 0) return;
   const uint8_t* tb = reinterpret_cast<const uint8_t*>(lds);
   const uint32_t* s_lop = lds + kS2Slice;
@@ -1068,6 +1069,17 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
 #pragma unroll
     for (int k = 0; k < D; ++k) issue((uint32_t)k, buf[k]);
     for (uint32_t c = 0; c < nl; c += D) {
+      if (PB) {
+        // issue-priority balancing: a SIMD's issue arbiter serves its oldest wave first, so with equal shares the four
+        // waves of a SIMD finished up to 50 us apart and the last of them streamed alone. Each wave publishes its
+        // chunks left (s_rem[simd][age]) and runs at priority 2 while it has (nearly) the most left on its SIMD.
+        const uint32_t left = nl - c;
+        if (lane == 0) s_rem[wslot] = left;
+        const uint4 r = *reinterpret_cast<const uint4*>(s_rem + (wslot & ~3u));
+        const uint32_t mx = max(max(r.x, r.y), max(r.z, r.w));
+        if (left + (uint32_t)D >= mx) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
+      }
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         // chunk c + k, then its registers take chunk c + k + D (no copy: a copy would make the loop carry two sets
@@ -1121,10 +1133,12 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   __shared__ CrcTail s_tail;
   __shared__ uint32_t s_wdone;  // waves of this workgroup done
   __shared__ uint32_t s_eq;     // the workgroup's emission items taken
+  __shared__ __attribute__((aligned(16))) uint32_t s_rem[kCrcWaves];  // chunks left per wave [simd][age] (stream_verify)
   const uint64_t t_entry = (ABL & 512) ? wall_clock64() : 0;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid < (uint32_t)kCrcWaves) s_rem[tid] = 0;
   if (tid == 0) {
     s_wdone = 0;
     s_eq = 0;
@@ -1132,8 +1146,15 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   }
   const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
   const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
+  // the CRC stream runs on the first SW waves of the workgroup; the last kCrcWaves - SW (the youngest wave of each
+  // SIMD, the one its issue arbiter serves last) take record-emission items from the start, so the latency-bound
+  // emission overlaps the stream instead of following it (ABL bits 28-30, kbench: v != 0 -> v - 1 emission waves)
+  constexpr int EW = ((ABL >> 28) & 7) ? ((ABL >> 28) & 7) - 1 : kCrcEmitWaves;
+  constexpr int SW = kCrcWaves - EW;
+  const bool streams = wave < (uint32_t)SW;
+  const uint64_t nsw = (uint64_t)gridDim.x * SW, gsw = (uint64_t)blockIdx.x * SW + (streams ? wave : 0u);
   const uint64_t cn = cb1 - cb0;
-  const uint64_t b0 = cb0 + cn * gw / nw, b1 = cb0 + cn * (gw + 1) / nw;
+  const uint64_t b0 = cb0 + cn * gsw / nsw, b1 = streams ? cb0 + cn * (gsw + 1) / nsw : b0;
   const uint64_t f0 = fbase[b0];
   uint64_t f1 = fbase[b1];
   if (f1 > frag_cap) f1 = frag_cap;
@@ -1160,30 +1181,27 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   if (blockIdx.x == 0 && tid == 0) misc[M_T_CRC0] = wall_clock64();
   const uint64_t t_tables = (ABL & 512) ? wall_clock64() : 0;
   const uint32_t nfr = f1 > f0 ? (uint32_t)(f1 - f0) : 0u;
-  if (!(ABL & 32768))
-    stream_verify<(ABL >> 24) & 15 ? (ABL >> 24) & 15 : 8, (ABL >> 21) & 7>(seg, seg_len, start_off, frags, frags_ro,
-                                                                            f0, nfr, lds, lane, misc);
-  asm volatile("" ::: "memory");  // (reload the tail arguments from LDS, see CrcTail)
-  CrcTail T;
-  {  // wave-uniform: into SGPRs
-    static_assert(sizeof(CrcTail) % 4 == 0, "CrcTail words");
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&s_tail);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(CrcTail) / 4); ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
-  }
-  const EmitArgs& A = T.ea;
-  if ((ABL & 512) && lane == 0) {
-    uint64_t* q = A.tab.expire + 4 * gw;  // kbench only (the table is overwritten by the emission unless ABL & 8)
-    q[0] = t_entry; q[1] = t_tables; q[2] = wall_clock64(); q[3] = nfr;
-  }
   // ---- record emission: the workgroup's work items (those starting in its blocks), taken from an LDS counter by
-  // its waves as they finish their CRC passes, so the early finishers emit for the late ones (ItemMeta). The next
-  // item is taken and its block data requested while this item's fragment descriptors are in flight, so an item
-  // costs two dependent round trips (descriptors, record prefixes) ----
-  if (!(ABL & 8) && !(A.kb_flags & 1u) &&
-      __builtin_amdgcn_readfirstlane(
-          (uint32_t)__hip_atomic_load(&T.misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+  // its waves as they finish their CRC streams (ItemMeta). The next item is taken and its block data requested while
+  // this item's fragment descriptors are in flight, so an item costs two dependent round trips (descriptors, record
+  // prefixes). The arguments are reloaded from LDS (CrcTail). (One item per wave part of the way through its stream,
+  // staggered by wave, measured slower: 261-271 vs 209 us on B.)
+  uint64_t n_items = 0;
+  auto emit_items = [&](uint64_t max_items) {
+    asm volatile("" ::: "memory");
+    CrcTail T;
+    {  // wave-uniform: into SGPRs
+      static_assert(sizeof(CrcTail) % 4 == 0, "CrcTail words");
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(&s_tail);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(CrcTail) / 4); ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
+    }
+    const EmitArgs& A = T.ea;
+    if ((ABL & 8) || (A.kb_flags & 1u) ||
+        __builtin_amdgcn_readfirstlane(
+            (uint32_t)__hip_atomic_load(&T.misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u)
+      return;
     const uint64_t cb0t = T.cb0, cb1t = T.cb1, cnt = cb1t - cb0t, fcap = T.frag_cap;
     // blocks per item for ~64 fragments each
     const uint64_t fc0 = A.fbase[cb0t], fc1 = A.fbase[cb1t];
@@ -1199,27 +1217,48 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       j = __builtin_amdgcn_readfirstlane(j);
       return i0 + j;
     };
-    const uint64_t t_crc = A.kb_stamps ? wall_clock64() : 0;
-    uint64_t n_items = 0;
+    uint64_t taken = 0;
     uint64_t it = deq();
     ItemMeta m = item_meta(A, it, bpw, cb0t, cb1t, lane);
     while (it < nitems) {
-      ++n_items;
+      ++taken;
       const EmitState es = emit_state(A, m.bb, lane, m.s, m.rec);
       const uint64_t mf1 = m.f1 < fcap ? m.f1 : fcap;
-      uint64_t nx = 0;
-      ItemMeta mn;
+      uint64_t nx = ~0ull;
+      ItemMeta mn = m;
       emit_chunks<ABL & (4096 | 8192)>(A, es, m.f0, mf1, lane, [&]() {
-        nx = deq();
-        mn = item_meta(A, nx, bpw, cb0t, cb1t, lane);
+        if (taken < max_items) {
+          nx = deq();
+          mn = item_meta(A, nx, bpw, cb0t, cb1t, lane);
+        }
       });
       it = nx;
       m = mn;
     }
-    if (A.kb_stamps && lane == 0) {
-      uint64_t* q = A.kb_stamps + 4 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
-      q[0] = t_crc; q[1] = wall_clock64(); q[2] = n_items; q[3] = nfr;
-    }
+    n_items += taken;
+  };
+  if (!(ABL & 32768))
+    stream_verify<(ABL >> 24) & 15 ? (ABL >> 24) & 15 : 8, (ABL >> 21) & 7, !(ABL & 1048576)>(
+        seg, seg_len, start_off, frags, frags_ro, f0, nfr, lds, lane, misc, s_rem, (wave & 3u) * 4u + (wave >> 2));
+  __builtin_amdgcn_s_setprio(0);
+  const uint64_t t_crc = (ABL & 512) || ea.kb_stamps ? wall_clock64() : 0;
+  emit_items(~0ull);
+  asm volatile("" ::: "memory");  // (reload the tail arguments from LDS, see CrcTail)
+  CrcTail T;
+  {  // wave-uniform: into SGPRs
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&s_tail);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(CrcTail) / 4); ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
+  }
+  const EmitArgs& A = T.ea;
+  if ((ABL & 512) && lane == 0) {
+    uint64_t* q = A.tab.expire + 4 * gw;  // kbench only (the table is overwritten by the emission unless ABL & 8)
+    q[0] = t_entry; q[1] = t_tables; q[2] = t_crc; q[3] = nfr;
+  }
+  if (A.kb_stamps && lane == 0) {
+    uint64_t* q = A.kb_stamps + 4 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
+    q[0] = t_crc; q[1] = wall_clock64(); q[2] = n_items; q[3] = nfr;
   }
   // ---- completion: each wave's stores and atomics are done (vmcnt(0)) before it counts itself done in LDS;
   // the last wave of a workgroup adds the workgroup to the agent-scope counter, and the last workgroup's

@@ -198,6 +198,8 @@ int main(int argc, char** argv) {
       case 10485760: return run(k_crc<10485760>, cus, ea);  // stream: fast path only, no chains
       case 8: return run(k_crc<8>, cus, ea);              // no emission
       case 8388616: return run(k_crc<8388616>, cus, ea);  // fast path only, no emission
+      case 10485768: return run(k_crc<10485768>, cus, ea);  // fast path only, no chains, no emission
+      case 10486280: return run(k_crc<10486280>, cus, ea);  // the same with per-wave stamps
       case 33554432: return run(k_crc<33554432>, cus, ea);  // D = 2
       case 100663296: return run(k_crc<100663296>, cus, ea);  // D = 6
       case 67108864: return run(k_crc<67108864>, cus, ea);  // D = 4
@@ -209,6 +211,16 @@ int main(int argc, char** argv) {
       case 32776: return run(k_crc<32768 | 8>, cus, ea);
       case 36864: return run(k_crc<32768 | 4096>, cus, ea);
       case 98: { const float r = run(k_crc<0>, cus, ea_st); stamp_report(); return r; }
+      case 97: { const float r = run(k_crc<10485760>, cus, ea_st); stamp_report(); return r; }  // fast, no chain
+      case 520: return run(k_crc<520>, cus, ea);
+      case 1048576: return run(k_crc<1048576>, cus, ea);  // no priority balancing
+      case 1048584: return run(k_crc<1048584>, cus, ea);  // no priority balancing, no emission
+      case 1049096: return run(k_crc<1049096>, cus, ea);  // the same with per-wave stamps
+      case 268435456: return run(k_crc<268435456>, cus, ea);    // no emission-first waves
+      case 536870912: return run(k_crc<536870912>, cus, ea);    // 1
+      case 805306368: return run(k_crc<805306368>, cus, ea);    // 2
+      case 1342177280: return run(k_crc<1342177280>, cus, ea);  // 4
+      case 1879048192: return run(k_crc<1879048192>, cus, ea);  // 6
       case 4096: return run(k_crc<4096>, cus, ea);
       case 8192: return run(k_crc<8192>, cus, ea);
       default: return run(k_crc<0>, cus, ea);
@@ -251,7 +263,7 @@ int main(int argc, char** argv) {
     }
     CK(hipStreamSynchronize(st));
     printf("k_crc<%d> x%d done, %.4f ms\n", v, k, tm);
-    if (v == 520 || v == 1544) {  // per-wave stamps of the last launch: start / tables / loop end, by XCD (blockIdx % 8)
+    if (v == 520 || v == 1544 || v == 10486280 || v == 1049096) {  // per-wave stamps of the last launch: start / tables / loop end, by XCD (blockIdx % 8)
       const int nw = cus * kCrcWaves;
       std::vector<uint64_t> q(4 * (size_t)nw);
       CK(hipMemcpy(q.data(), t.expire, q.size() * 8, hipMemcpyDeviceToHost));

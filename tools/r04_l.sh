@@ -1,0 +1,11 @@
+#!/bin/bash
+# k_crc: mid-stream emission on/off (B and C), stamps
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+OUT=gpurun_out; mkdir -p $OUT
+timeout -k 10 200 ./tools/kbench/kbench 1073741824 0 cmp 0 524288 8 > $OUT/r04l_cmp_b.log 2>&1 || { tail -20 $OUT/r04l_cmp_b.log; exit 1; }
+grep "k_crc<\|full pipeline" $OUT/r04l_cmp_b.log
+timeout -k 10 200 ./tools/kbench/kbench 1073741824 1 cmp 0 524288 8 > $OUT/r04l_cmp_c.log 2>&1 || { tail -20 $OUT/r04l_cmp_c.log; exit 1; }
+grep "k_crc<\|full pipeline" $OUT/r04l_cmp_c.log
+timeout -k 10 100 ./tools/kbench/kbench 1073741824 0 3 98 > $OUT/r04l_98.log 2>&1 || { tail -20 $OUT/r04l_98.log; exit 1; }
+grep -A1 "emission stamps" $OUT/r04l_98.log | tail -2
