@@ -423,7 +423,9 @@ def main():
         return
 
     # ---- roofline of the dominant kernel (k_crc): algorithmic bytes per launch / avg duration ----
-    alg_bytes = seg_len + 17 * n_frags  # segment read once + fragment descriptors (16 B read, 1 B verdict)
+    # segment read once + per fragment its descriptor (16 B read) and verdict (1 B written) + per record its row of
+    # the record table (48 B written: k_crc emits the records)
+    alg_bytes = seg_len + 17 * n_frags + 48 * n_rec
     achieved = alg_bytes / (crc_ms * 1e-3) / 1e9
     # traffic: HBM bytes per launch from a committed PMC summary measured on THIS build's k_crc (same decode-source
     # hash, same segment), else null

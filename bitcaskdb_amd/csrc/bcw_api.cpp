@@ -388,6 +388,7 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.lb);
   (void)hipFree(s.lbe);
   (void)hipFree(s.frags);
+  (void)hipFree(s.fok);
   (void)hipFree(s.misc);
   (void)hipFree(s.equeue);
   s = Scratch{};
@@ -465,6 +466,7 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.rbase, (nb + 1) * 4) == hipSuccess &&
             hipMalloc(&s.bsum, (nb + 1) * sizeof(uint2)) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
             hipMalloc(&s.lbe, nwg * 8) == hipSuccess && hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
+            hipMalloc(&s.fok, fc) == hipSuccess &&
             hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess && hipMalloc(&s.equeue, 8 * 128) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;

@@ -944,12 +944,12 @@ __device__ __forceinline__ uint32_t apply_op_b(const uint32_t* __restrict__ t, u
 // Positions are 32-bit, relative to the wave's first chunk (a wave's blocks span far less than 1 GiB).
 // SV: kbench ablations (0 in the product): 1 no chains (words folded by xor), 2 no loads, 4 every chunk takes the
 // fast path (verdicts meaningless). PB: issue-priority balancing (below).
-template <int D, int SV = 0, bool PB = true>
+template <int D, int SV = 0, bool PB = true, int SX = 0>  // SX (kbench): 1 no close, 2 no split op, 4 no masks
 __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
-                                              Frag* __restrict__ frags, const uint4* __restrict__ frd, uint64_t f0,
+                                              uint8_t* __restrict__ fok, const uint4* __restrict__ frd, uint64_t f0,
                                               uint32_t nfr, const uint32_t* __restrict__ lds, uint32_t lane,
                                               uint64_t* __restrict__ misc, uint32_t* __restrict__ s_rem,
-                                              uint32_t wslot) {
+                                              uint32_t wslot, const uint8_t* __restrict__ dummy) {
   if (nfr == 0) return;
   const uint8_t* tb = reinterpret_cast<const uint8_t*>(lds);
   const uint32_t* s_lop = lds + kS2Slice;
@@ -971,6 +971,9 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
   const uint32_t nch = (uint32_t)(c_end - c_first);
   struct G32 { int32_t gs, ge; uint32_t J; };  // wave-relative data range, check word
   constexpr int32_t kFar = 0x40000000;
+  // (readfirstlane: the fragment state is wave-uniform; without it the compiler kept parts of it in VGPRs and moved
+  // them back and forth at every fragment end)
+  auto uni = [](int32_t x) -> int32_t { return __builtin_amdgcn_readfirstlane(x); };
   auto geo = [&](uint4 v, bool valid) -> G32 {
     G32 g{kFar, kFar, 0u};
     if (valid) {
@@ -979,6 +982,9 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
       g.gs = gs < 0 ? -64 : (gs > kFar ? kFar : (int32_t)gs);
       g.ge = g.gs + (int32_t)(v.y >> 16);
     }
+    g.gs = uni(g.gs);
+    g.ge = uni(g.ge);
+    g.J = (uint32_t)uni((int32_t)g.J);
     return g;
   };
   uint32_t i = 0;  // the current fragment (wave-relative): open (H holds its state) or not begun (H = 0)
@@ -988,15 +994,15 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
   uint32_t fs_lo = 0, fs_n = 0;
   auto set_fast = [&]() {
     const int32_t lo = (fc.gs + kSChunk - 1) / kSChunk, hi = fc.ge / kSChunk;
-    fs_lo = (uint32_t)lo;
-    fs_n = hi > lo ? (uint32_t)(hi - lo) : 0u;
+    fs_lo = (uint32_t)uni(lo);
+    fs_n = (uint32_t)uni(hi > lo ? hi - lo : 0);
   };
   set_fast();
   uint32_t H = 0;
   uint64_t okm = 0;            // verdicts of fragments (i & ~63) + j, bit j
   uint32_t bad = 0xffffffffu;  // first failing fragment (wave-relative)
   auto flush = [&](uint32_t from, uint32_t n) {  // verdicts of fragments [from, from + n) (n <= 64)
-    if (lane < n) frags[f0 + from + lane].ok = (uint8_t)((okm >> lane) & 1u);
+    if (lane < n) fok[f0 + from + lane] = (uint8_t)((okm >> lane) & 1u);
   };
   auto advance = [&]() {
     ++i;
@@ -1024,7 +1030,10 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
       const bool next_in = closes && fn.gs < C1 && fn.ge >= C1;
       uint32_t x[kSPW];
       const int32_t pa = rel(fc.gs), pb = rel(fc.ge);
-      if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr)  // the usual case: a header between two data runs
+      if (SX & 4) {
+#pragma unroll
+        for (int q = 0; q < kSPW; ++q) x[q] = w[q];
+      } else if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr)  // the usual case: a header between two data runs
         mask_gap(x, w, pb, fc.J, lane, lds);
       else
         mask_chunk(x, w, pa, pb, next_in ? rel(fn.gs) : 4096, fc.J, lane, lds);
@@ -1040,11 +1049,13 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
       // K == kSPW: lane Lf's part ends with its piece (A = s8, as for the lanes before it)
       const bool full = lane < Lf || (lane == Lf && K == (uint32_t)kSPW);
       const bool split = lane == Lf && K != 0u;  // (K == 0: the lanes from Lf on hold none of its bytes)
-      const uint32_t A = full ? s8 : apply_op_b(s_kop + (split ? K : 0u) * 1024u, split ? cap : H);
-      const uint32_t T = wave_scan_z(apply_fwd(s_lop, lane, A), [](uint32_t a, uint32_t b) { return a ^ b; });
+      const uint32_t A = full ? s8 : ((SX & 2) ? (split ? cap : H) : apply_op_b(s_kop + (split ? K : 0u) * 1024u, split ? cap : H));
+      const uint32_t T = (SX & 1) ? A : wave_scan_z(apply_fwd(s_lop, lane, A), [](uint32_t a, uint32_t b) { return a ^ b; });
       const bool ok = __builtin_amdgcn_readlane(T, 63) == 0u;
       okm |= (uint64_t)(ok ? 1u : 0u) << (i & 63u);
+      okm = (uint64_t)(uint32_t)uni((int32_t)(uint32_t)okm) | ((uint64_t)(uint32_t)uni((int32_t)(okm >> 32)) << 32);
       if (!ok && bad == 0xffffffffu) bad = i;
+      bad = (uint32_t)uni((int32_t)bad);
       H = s8 ^ A;
       advance();
       if (next_in) return;
@@ -1054,8 +1065,11 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
   const uint32_t nl = c_safe > c_first ? (uint32_t)min(c_safe - c_first, (uint64_t)nch) : 0u;  // pipelined chunks
   if (nl > 0u) {
     const uint8_t* sbase = seg + c_first * kSChunk + lane * kSPiece;
+    // the loads issued past the last chunk read 1 KiB of the table image instead, which every workgroup has just
+    // read (an L2 hit): reloading the wave's own first chunk cost 8 KiB of HBM reads per wave (32 MB per launch)
+    const uint8_t* dbase = dummy + lane * kSPiece;
     uint32_t buf[D][kSPW];
-    auto issue = [&](uint32_t c, uint32_t (&w)[kSPW]) {  // unconditional: a chunk past the loop reloads the first
+    auto issue = [&](uint32_t c, uint32_t (&w)[kSPW]) {  // unconditional (no branch around a load)
       if (SV & 2) {
 #pragma unroll
         for (int k = 0; k < kSPW; ++k) w[k] = c * 2654435761u + lane * 40503u + k;
@@ -1063,7 +1077,7 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
       }
       // non-temporal: the segment is read once (kbench spat: 185 -> 160 us for the whole segment)
       typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-      const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(sbase + (size_t)(c < nl ? c : 0u) * kSChunk));
+      const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(c < nl ? sbase + (size_t)c * kSChunk : dbase));
       w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
     };
 #pragma unroll
@@ -1120,7 +1134,7 @@ struct CrcTail {
 template <int ABL = 0>
 __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                      uint32_t start_off, uint64_t nblocks,
-                                                     const uint32_t* __restrict__ fbase, Frag* __restrict__ frags,
+                                                     const uint32_t* __restrict__ fbase, uint8_t* __restrict__ fok,
                                                      const uint4* __restrict__ frags_ro,
                                                      uint64_t frag_cap, Tables tabs, EmitArgs ea,
                                                      uint32_t tail_panic, uint64_t gen,
@@ -1238,8 +1252,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     n_items += taken;
   };
   if (!(ABL & 32768))
-    stream_verify<(ABL >> 24) & 15 ? (ABL >> 24) & 15 : 8, (ABL >> 21) & 7, !(ABL & 1048576)>(
-        seg, seg_len, start_off, frags, frags_ro, f0, nfr, lds, lane, misc, s_rem, (wave & 3u) * 4u + (wave >> 2));
+    stream_verify<(ABL >> 24) & 15 ? (ABL >> 24) & 15 : 8, (ABL >> 21) & 7, !(ABL & 1048576), (ABL >> 16) & 15>(
+        seg, seg_len, start_off, fok, frags_ro, f0, nfr, lds, lane, misc, s_rem, (wave & 3u) * 4u + (wave >> 2),
+        reinterpret_cast<const uint8_t*>(tabs.lds_image2));
   __builtin_amdgcn_s_setprio(0);
   const uint64_t t_crc = (ABL & 512) || ea.kb_stamps ? wall_clock64() : 0;
   emit_items(~0ull);
@@ -1280,7 +1295,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   finalize(A, T.nblocks, T.frag_cap, T.tail_panic, T.gen, T.res, lane);
 }
 
-__global__ void k_export_frags(const Frag* __restrict__ frags, const uint64_t* __restrict__ misc, uint64_t cap,
+__global__ void k_export_frags(const Frag* __restrict__ frags, const uint8_t* __restrict__ fok,
+                               const uint64_t* __restrict__ misc, uint64_t cap,
                                uint32_t start_off, bcw_frag_table out, const uint32_t* __restrict__ initc) {
   const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t n = misc[M_NFRAGS];
@@ -1291,7 +1307,7 @@ __global__ void k_export_frags(const Frag* __restrict__ frags, const uint64_t* _
   const uint32_t u = ~(f.chk ^ initc[f.len]);  // unmask(stored), from J
   out.stored_crc[g] = ((u >> 15) | (u << 17)) + 0xa282ead8u;
   out.type[g] = f.type;
-  out.crc_ok[g] = f.ok;
+  out.crc_ok[g] = fok[g];
 }
 
 
@@ -1320,7 +1336,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
     s.epoch = 1;
   }
   pr.begin(K_CRC, stream, ev);
-  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.frags,
+  k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.fok,
                                                          reinterpret_cast<const uint4*>(s.frags), s.frag_cap, tabs, ea,
                                                          tail_panic, gen, d_result, s.misc, 0ull, nblocks,
                                                          (uint32_t)num_cus);
@@ -1331,7 +1347,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
 hipError_t launch_export_frags(const Scratch& s, const bcw_frag_table& out, uint32_t start_off, hipStream_t stream,
                                uint64_t n, const uint32_t* initc) {
   if (n == 0) return hipSuccess;
-  k_export_frags<<<(uint32_t)((n + 255) / 256), 256, 0, stream>>>(s.frags, s.misc, s.frag_cap, start_off, out,
+  k_export_frags<<<(uint32_t)((n + 255) / 256), 256, 0, stream>>>(s.frags, s.fok, s.misc, s.frag_cap, start_off, out,
                                                                     initc);
   return hipGetLastError();
 }

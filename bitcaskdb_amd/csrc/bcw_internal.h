@@ -84,6 +84,7 @@ struct Scratch {
   uint64_t tickets = 0;        // k_chase tickets issued so far (misc[M_TICKET] mirrors it)
   uint64_t epoch = 1;          // look-back epoch of the next launch
   Frag* frags = nullptr;       // [frag_cap]
+  uint8_t* fok = nullptr;      // [frag_cap] CRC verdict per fragment (k_crc; dense: 64 verdicts are one 64 B store)
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
   uint32_t* equeue = nullptr;  // [8 x 32] k_crc emission work-queue heads, one 128 B line per XCD
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups

@@ -186,7 +186,7 @@ int main(int argc, char** argv) {
   };
   auto run = [&](auto kern, int grid, const EmitArgs& a) {
     return timeit([&] { hipMemsetAsync(s.equeue, 0, 1024, st);  // the emission queues (k_chase resets them)
-                        kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, (const uint4*)s.frags, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid); },
+                        kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, (const uint4*)s.frags, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid); },
                   reps, st);
   };
   const int cus = ctx->num_cus;
@@ -213,6 +213,10 @@ int main(int argc, char** argv) {
       case 98: { const float r = run(k_crc<0>, cus, ea_st); stamp_report(); return r; }
       case 97: { const float r = run(k_crc<10485760>, cus, ea_st); stamp_report(); return r; }  // fast, no chain
       case 520: return run(k_crc<520>, cus, ea);
+      case 65544: return run(k_crc<65544>, cus, ea);    // no emission, no close
+      case 131080: return run(k_crc<131080>, cus, ea);  // no emission, no split op
+      case 262152: return run(k_crc<262152>, cus, ea);  // no emission, no masks
+      case 458760: return run(k_crc<458760>, cus, ea);  // no emission, none of the three
       case 1048576: return run(k_crc<1048576>, cus, ea);  // no priority balancing
       case 1048584: return run(k_crc<1048584>, cus, ea);  // no priority balancing, no emission
       case 1049096: return run(k_crc<1049096>, cus, ea);  // the same with per-wave stamps
@@ -315,7 +319,7 @@ int main(int argc, char** argv) {
   const float as = timeit([&] {
     hipMemsetAsync(&s.misc[M_DONE_CRC], 0, 8, st);  // the last workgroup finalizes
     hipMemsetAsync(s.equeue, 0, 1024, st);
-    k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.frags, (const uint4*)s.frags, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
+    k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, (const uint4*)s.frags, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
                                           s.misc, 0ull, nblocks, (uint32_t)cus);
   }, reps, st);
   printf("k_crc + finalize %.4f ms\n", as);

@@ -1,0 +1,50 @@
+#!/bin/bash
+# round-4 evidence run: full GPU suite, smoke, bench (B), bench (C), rocprof kernel stats, FETCH/WRITE PMC passes.
+# Results under gpurun_out/r04/ (copied into profiles/ by hand).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+OUT=$R/gpurun_out/r04
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+STEPS=${STEPS:-tests,smoke,bench,benchc,prof,pmc}
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
+if has tests; then
+  echo "== tests $(date +%T)"
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
+  tail -1 "$OUT/gpu_tests.log"
+fi
+if has smoke; then
+  echo "== smoke $(date +%T)"
+  timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -30 "$OUT/smoke.log"; exit 1; }
+  tail -1 "$OUT/smoke.log"
+fi
+if has bench; then
+  echo "== bench $(date +%T)"
+  timeout -k 10 400 python bench.py > "$OUT/bench.log" 2>&1 || { tail -30 "$OUT/bench.log"; exit 1; }
+  tail -1 "$OUT/bench.log" > "$OUT/bench.json"; cut -c1-400 "$OUT/bench.json"
+fi
+if has benchc; then
+  echo "== bench C $(date +%T)"
+  timeout -k 10 400 python bench.py --config C --no-extras > "$OUT/bench_c.log" 2>&1 || { tail -30 "$OUT/bench_c.log"; exit 1; }
+  tail -1 "$OUT/bench_c.log" > "$OUT/bench_c.json"; cut -c1-300 "$OUT/bench_c.json"
+fi
+if has prof; then
+  echo "== prof $(date +%T)"
+  rm -rf "$OUT/prof"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras --inflight 1 > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 1; }
+  find "$OUT/prof" -name "*kernel_stats*"
+fi
+if has pmc; then
+  echo "== pmc $(date +%T)"
+  for c in RDREQ WRITE_SIZE; do
+    set_=$c; [[ $c == RDREQ ]] && set_="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+    rm -rf "$OUT/pmc_$c"
+    timeout -k 10 300 rocprofv3 --pmc $set_ -d "$OUT/pmc_$c" -o run --output-format csv -- \
+      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --inflight 1 > "$OUT/pmc_$c.log" 2>&1 || { tail -30 "$OUT/pmc_$c.log"; exit 1; }
+  done
+  python3 tools/pmc_summary.py --rdreq "$OUT/pmc_RDREQ" --write "$OUT/pmc_WRITE_SIZE" --kernel "k_crc" \
+    --seg-bytes 1073743514 --alg-bytes 1090796956 -o "$OUT/k_crc_pmc.json"
+fi
+echo "== done $(date +%T)"
