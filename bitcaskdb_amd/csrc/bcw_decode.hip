@@ -1015,6 +1015,27 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
     fnn = fd[i + 2u < nfr ? i + 2u : 0u];
     set_fast();
   };
+  // the closing fragment's zero test over the masked chunk words x (its data and J end at pb + 4, chunk-relative),
+  // then the next fragment's state
+  auto close = [&](const uint32_t (&x)[kSPW], int32_t pb) {
+    const uint32_t e = (uint32_t)(pb + 4);  // the closing fragment's bytes end here (1 <= e <= kSChunk)
+    // lanes < Lf: all theirs; lane Lf: split at word K
+    const uint32_t Lf = e / kSPiece, K = ((e % kSPiece) + 3u) >> 2;
+    uint32_t cap = 0;
+    const uint32_t s8 = chain_piece2<true>(tb, sl, H, x, K, &cap);
+    // K == kSPW: lane Lf's part ends with its piece (A = s8, as for the lanes before it)
+    const bool full = lane < Lf || (lane == Lf && K == (uint32_t)kSPW);
+    const bool split = lane == Lf && K != 0u;  // (K == 0: the lanes from Lf on hold none of its bytes)
+    const uint32_t A = full ? s8 : ((SX & 2) ? (split ? cap : H) : apply_op_b(s_kop + (split ? K : 0u) * 1024u, split ? cap : H));
+    const uint32_t T = (SX & 1) ? A : wave_scan_z(apply_fwd(s_lop, lane, A), [](uint32_t a, uint32_t b) { return a ^ b; });
+    const bool ok = __builtin_amdgcn_readlane(T, 63) == 0u;
+    okm |= (uint64_t)(ok ? 1u : 0u) << (i & 63u);
+    okm = (uint64_t)(uint32_t)uni((int32_t)(uint32_t)okm) | ((uint64_t)(uint32_t)uni((int32_t)(okm >> 32)) << 32);
+    if (!ok && bad == 0xffffffffu) bad = i;
+    bad = (uint32_t)uni((int32_t)bad);
+    H = s8 ^ A;
+    advance();
+  };
   auto process = [&](uint32_t c, const uint32_t (&w)[kSPW]) {  // c: wave-relative chunk
     if ((SV & 4) || c - fs_lo < fs_n) {  // inside the current fragment's data
       if (SV & 1) H ^= w[0] ^ w[1] ^ w[2] ^ w[3];
@@ -1022,6 +1043,14 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
       return;
     }
     const int32_t C0 = (int32_t)(c * kSChunk), C1 = C0 + kSChunk;
+    // the usual fragment end, straight-line: the closing fragment began before the chunk, a header follows its data
+    // and the next fragment's data runs on to the chunk's end (config B: nearly every end)
+    if (!(SX & 4) && fc.gs <= C0 && fc.ge + 4 <= C1 && fn.gs - fc.ge == (int32_t)kHdr && fn.gs < C1 && fn.ge >= C1) {
+      uint32_t x[kSPW];
+      mask_gap(x, w, fc.ge - C0, fc.J, lane, lds);
+      close(x, fc.ge - C0);
+      return;
+    }
     auto rel = [&](int32_t p) -> int32_t { return min(max(p - C0, -64), 4096); };
     for (;;) {
       if (fc.gs >= C1) return;  // (also once every fragment is done: fc.gs = kFar)
@@ -1033,7 +1062,7 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
       if (SX & 4) {
 #pragma unroll
         for (int q = 0; q < kSPW; ++q) x[q] = w[q];
-      } else if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr)  // the usual case: a header between two data runs
+      } else if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr)  // a header between two data runs
         mask_gap(x, w, pb, fc.J, lane, lds);
       else
         mask_chunk(x, w, pa, pb, next_in ? rel(fn.gs) : 4096, fc.J, lane, lds);
@@ -1041,23 +1070,7 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
         H = chain_piece2<false>(tb, sl, H, x);
         return;
       }
-      const uint32_t e = (uint32_t)(pb + 4);  // the closing fragment's bytes end here (1 <= e <= kSChunk)
-      // lanes < Lf: all theirs; lane Lf: split at word K
-      const uint32_t Lf = e / kSPiece, K = ((e % kSPiece) + 3u) >> 2;
-      uint32_t cap = 0;
-      const uint32_t s8 = chain_piece2<true>(tb, sl, H, x, K, &cap);
-      // K == kSPW: lane Lf's part ends with its piece (A = s8, as for the lanes before it)
-      const bool full = lane < Lf || (lane == Lf && K == (uint32_t)kSPW);
-      const bool split = lane == Lf && K != 0u;  // (K == 0: the lanes from Lf on hold none of its bytes)
-      const uint32_t A = full ? s8 : ((SX & 2) ? (split ? cap : H) : apply_op_b(s_kop + (split ? K : 0u) * 1024u, split ? cap : H));
-      const uint32_t T = (SX & 1) ? A : wave_scan_z(apply_fwd(s_lop, lane, A), [](uint32_t a, uint32_t b) { return a ^ b; });
-      const bool ok = __builtin_amdgcn_readlane(T, 63) == 0u;
-      okm |= (uint64_t)(ok ? 1u : 0u) << (i & 63u);
-      okm = (uint64_t)(uint32_t)uni((int32_t)(uint32_t)okm) | ((uint64_t)(uint32_t)uni((int32_t)(okm >> 32)) << 32);
-      if (!ok && bad == 0xffffffffu) bad = i;
-      bad = (uint32_t)uni((int32_t)bad);
-      H = s8 ^ A;
-      advance();
+      close(x, pb);
       if (next_in) return;
     }
   };

@@ -1,3 +1,4 @@
+#include <unistd.h>
 // k_crc ablation harness (not product code): one TU with the codec sources, times the full decode
 // pipeline and k_crc variants on a synthetic 1 GiB config-B segment.
 #include "../../bitcaskdb_amd/csrc/bcw_api.cpp"
@@ -230,6 +231,32 @@ int main(int argc, char** argv) {
       default: return run(k_crc<0>, cus, ea);
     }
   };
+  if (argc > 4 && std::string(argv[3]) == "seq") {  // N back-to-back pipelines (k_chase + k_crc), per-launch times
+    const int nrep = atoi(argv[4]);
+    const int gap_us = argc > 5 ? atoi(argv[5]) : 0;  // host sleep between launches (0: queued back to back)
+    std::vector<hipEvent_t> ev(2 * nrep);
+    for (auto& e : ev) CK(hipEventCreate(&e));
+    const uint64_t nb = (n - 40 + kBlock - 1) / kBlock;
+    for (int i = 0; i < nrep; ++i) {
+      if (gap_us >= 0 || i == 0) CK(hipEventRecord(ev[2 * i], st));
+      CK(launch_decode(d, p, t, dres, ctx->tabs, s, nb, 1, st, cus, nullptr));
+      if (gap_us >= 0 || i == nrep - 1) CK(hipEventRecord(ev[2 * i + 1], st));
+      if (gap_us > 0) { CK(hipStreamSynchronize(st)); usleep(gap_us); }
+    }
+    CK(hipStreamSynchronize(st));
+    if (gap_us < 0) {
+      float ms; CK(hipEventElapsedTime(&ms, ev[0], ev[2 * nrep - 1]));
+      printf("seq pipeline (no events between): %.1f us per pipeline\n", ms * 1e3 / nrep);
+      return 0;
+    }
+    printf("seq pipeline us:");
+    for (int i = 0; i < nrep; ++i) {
+      float ms; CK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+      printf(" %.0f", ms * 1e3);
+    }
+    printf("\n");
+    return 0;
+  }
   if (argc > 4 && std::string(argv[3]) == "cmp") {  // k_crc variants interleaved in one process (same buffers)
     const int nv = argc - 4;
     std::vector<std::vector<float>> ts(nv);
