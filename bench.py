@@ -363,12 +363,12 @@ def main():
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks ----
     # HIP events bracket only the roofline kernel (k_crc) on each codec stream
     # (every --event-every-th launch: an event pair idles that stream for a few microseconds)
-    for cx in all_ctx:
-        L.lib.bcw_ctx_set_profiling(cx.handle, 1 << roof_k)
-        L.lib.bcw_ctx_set_profiling_sample(cx.handle, args.event_every)
     # ---- warmup: W untimed steps back to back, right before the timed ones ----
     for _ in range(args.warmup):
         step()
+    for cx in all_ctx:
+        L.lib.bcw_ctx_set_profiling(cx.handle, 1 << roof_k)
+        L.lib.bcw_ctx_set_profiling_sample(cx.handle, args.event_every)
     kernel_times(all_ctx)  # reset (synchronises the codec streams)
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

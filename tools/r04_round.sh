@@ -33,8 +33,8 @@ if has prof; then
   echo "== prof $(date +%T)"
   rm -rf "$OUT/prof"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras --inflight 1 > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 1; }
-  find "$OUT/prof" -name "*kernel_stats*"
+    python3 bench.py --steps 20 --warmup 40 --no-cpu-baseline --no-extras --inflight 1 > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 1; }
+  python3 tools/trace_window.py "$OUT/prof" --skip 41 --steps 20 -o "$OUT/prof_timed.json"
 fi
 if has pmc; then
   echo "== pmc $(date +%T)"
