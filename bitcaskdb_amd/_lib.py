@@ -10,10 +10,13 @@ import re
 # its own libamdhip64 with the soname libamdhip64.so.7; loaded first, it is the runtime libbcw.so binds to. Loaded
 # after libbcw.so it would be a second runtime in the process, and with two processes sharing a GPU the second
 # runtime of each finds no device (measured: tools/probe/runtimes.py). Without PyTorch libbcw.so uses /opt/rocm's.
-try:
-    import torch  # noqa: F401
-except ImportError:
-    pass
+# The preload costs the import time of torch: a process that never uses PyTorch (a CPU-only tool, the Go-side shim's
+# tests) sets BCW_NO_TORCH_PRELOAD=1 to skip it; a process that does use PyTorch must then import torch first itself.
+if os.environ.get("BCW_NO_TORCH_PRELOAD") != "1":
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # BCW_LIB: an alternative build of the same library (A/B measurements of kernel variants only)

@@ -155,8 +155,10 @@ __global__ __launch_bounds__(256) void k_enc_prep(EncDev e, uint64_t rows, uint3
   const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
   const bcw_decode_result* R = e.sres;
   const uint64_t nrec = R->n_records;
-  // the source must be the context's latest decode (its fragment table) and fit the table
-  const uint32_t fail = R->generation != e.gen ? BCW_ENC_ERR_STALE : nrec > rows ? BCW_ENC_ERR_TABLE : 0u;
+  // the source must be the context's latest decode (its fragment table), fit the table and not be a decode that gave
+  // up on an internal wait (BCW_ERR_INTERNAL)
+  const uint32_t fail = R->generation != e.gen ? BCW_ENC_ERR_STALE
+                        : (nrec > rows || R->err_class == BCW_ERR_INTERNAL) ? BCW_ENC_ERR_TABLE : 0u;
   const uint64_t nin = fail ? 0
                        : (R->first_bad_record >= 0 && (uint64_t)R->first_bad_record < nrec)
                            ? (uint64_t)R->first_bad_record : nrec;

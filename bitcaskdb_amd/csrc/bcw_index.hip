@@ -256,9 +256,11 @@ __device__ __forceinline__ uint64_t delivered_rows(const bcw_decode_result* R) {
   return (R->first_bad_record >= 0 && (uint64_t)R->first_bad_record < nrec) ? (uint64_t)R->first_bad_record : nrec;
 }
 
-// the table source is usable: the context's latest decode (its fragment table) and not truncated
+// the table source is usable: the context's latest decode (its fragment table), not truncated, and not a decode
+// that gave up on an internal wait (BCW_ERR_INTERNAL: its rows, if any, are not to be applied)
 __device__ __forceinline__ uint32_t table_fail(const bcw_decode_result* R, uint64_t gen, uint64_t rows) {
-  return R->generation != gen ? BCW_ENC_ERR_STALE : R->n_records > rows ? BCW_ENC_ERR_TABLE : 0u;
+  return R->generation != gen ? BCW_ENC_ERR_STALE
+         : (R->n_records > rows || R->err_class == BCW_ERR_INTERNAL) ? BCW_ENC_ERR_TABLE : 0u;
 }
 
 // wave-aggregated add of v to *ctr; returns this lane's exclusive offset

@@ -369,6 +369,8 @@ def iterate_record(wal: Wal, cb, ns_size: int = 20, etag_size: int = 20, ctx: Co
     """IterateRecord (record.go:242-266): cb(record, foff, size) per record; raises the first error."""
     ctx = ctx or default_context()
     dec = ctx.decode(wal.data, wal.start_off, wal.base_time, ns_size, etag_size, L.MODE_RECORD, with_frags=True)
+    if dec.result.err_class == L.ERR_INTERNAL:  # before any row reaches the callback
+        _frag_error(dec.result)
     for r in range(dec.n_records):
         st = int(dec.table["status"][r])
         if st == L.ST_INVALID:
@@ -390,6 +392,8 @@ def iterate_hint(hint: Wal, cb, ns_size: int = 20, ctx: Context | None = None):
     """IterateHint (hint.go:163-188): cb(HintRecord) per record; raises the first error."""
     ctx = ctx or default_context()
     dec = ctx.decode(hint.data, hint.start_off, hint.base_time, ns_size, 0, L.MODE_HINT, with_frags=True)
+    if dec.result.err_class == L.ERR_INTERNAL:  # before any row reaches the callback
+        _frag_error(dec.result)
     for r in range(dec.n_records):
         st = int(dec.table["status"][r])
         if st == L.ST_INVALID:

@@ -260,7 +260,8 @@ int bcw_synth_segment(uint64_t target_bytes, uint64_t max_records, uint64_t seed
 #define BCW_ENC_ERR_EXPIRE 2 /* Record.Encode: errors.New("invalid expire") (record.go:74) at err_record */
 #define BCW_ENC_ERR_PANIC 3  /* Record.Encode panics at err_record: expire delta >= 2^35 overflows
                                 `var expireBytes [binary.MaxVarintLen32]byte` (record.go:67,78) */
-#define BCW_ENC_ERR_TABLE 4  /* the source table is smaller than the decode's n_records: nothing encoded */
+#define BCW_ENC_ERR_TABLE 4  /* the source table is smaller than the decode's n_records, or the decode reported
+                                BCW_ERR_INTERNAL: nothing encoded / applied */
 #define BCW_ENC_ERR_STALE 5  /* d_src_result is not the context's latest decode (its fragment table was
                                 replaced, e.g. by a hint decode): nothing encoded */
 

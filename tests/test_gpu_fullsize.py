@@ -211,6 +211,13 @@ def test_forced_wait_abort(direct):
         assert r.first_bad_record == -1 and r.err_file_off == 0
         # one-shot: the next decode on the same context is exact
         full_parity(c, data, p, "after abort")
+        # a compaction whose source decode gives up applies nothing (k_enc_prep: BCW_ENC_ERR_TABLE, 0 rows in)
+        if direct:
+            c.set_option(L.OPT_TEST_ABORT_WAIT, 6)
+            res, wal, hb, _ = c.encode(data, L.ENC_COMPACT, 40, BASE, 9, 40, 40, 20, 20,
+                                       np.ones(got.result.n_blocks * 8, dtype=np.uint8))
+            assert res.err_class == L.ENC_ERR_TABLE and res.n_in == 0 and res.n_written == 0
+            assert wal == b"" and hb == b""
         c.sync()
     finally:
         c.close()
