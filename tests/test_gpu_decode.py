@@ -111,3 +111,46 @@ def test_hint_wal_at_scale(ctx):
     ec, _, _, hint = O.hint_by_wal(data, 3, 40, 1_700_000_000, 20, 20)
     assert ec == 0
     assert_parity(ctx, hint, cases.params(mode=1), "hint at scale")
+
+
+def _sweep_segment(step: int, count: int, base_len: int, payload_kind: str):
+    """raw payloads whose lengths grow by `step` bytes: the fragment ends (and with them the check word J, the 7-byte
+    header gap and the next fragment's start) walk through every byte offset of the 16 B lane pieces and the 1 KiB
+    chunks of the stream verify (bcw_decode.hip stream_verify), including J straddling two pieces, two lanes or two
+    chunks, headers split across a chunk boundary and several fragment ends in one chunk"""
+    rng = random.Random(base_len * 31 + step)
+    ps = []
+    for k in range(count):
+        n = base_len + k * step
+        ps.append(bytes(rng.getrandbits(8) for _ in range(n)) if payload_kind == "rand" else bytes(n))
+    data, offs = cases.wal_of(ps)
+    return data, offs
+
+
+@pytest.mark.parametrize("step,count,base_len,kind", [(1, 1100, 1, "rand"), (1, 1100, 1000, "rand"),
+                                                      (3, 700, 3000, "rand"), (1, 600, 0, "zero"),
+                                                      (17, 400, 50, "rand")])
+def test_stream_verify_geometry_sweep(ctx_path, step, count, base_len, kind):
+    """every fragment-end offset within a chunk, clean: all verdicts and rows equal the oracle's (the records are
+    raw payloads, so RecordFromBytes reports them invalid exactly as the reference does)"""
+    data, _ = _sweep_segment(step, count, base_len, kind)
+    assert_parity(ctx_path, data, cases.params(), f"sweep{step}/{base_len}/{kind}")
+
+
+@pytest.mark.parametrize("where", ["last_data", "first_data", "crc_byte", "len_byte"])
+def test_stream_verify_geometry_corrupt(ctx_path, where):
+    """a corrupted byte at a fragment edge (its last data byte, its first data byte, a stored CRC byte, a length byte)
+    of every 37th fragment of the sweep in turn: the first failing fragment and the records before it equal the
+    oracle's"""
+    data, offs = _sweep_segment(1, 1100, 1, "rand")
+    ref = O.decode(data, 40, cases.BASE, 20, 20, 0)
+    for f in range(5, len(ref.frags), 37):
+        fr = ref.frags[f]
+        d0, ln = int(fr["data_off"]), int(fr["len"])
+        if ln == 0:
+            continue
+        pos = {"last_data": d0 + ln - 1, "first_data": d0, "crc_byte": d0 - 7 + (f % 4),
+               "len_byte": d0 - 3}[where]
+        bad = bytearray(data)
+        bad[pos] ^= 0x41
+        assert_parity(ctx_path, bytes(bad), cases.params(), f"corrupt {where} frag {f}")
