@@ -148,7 +148,7 @@ struct Spin {
 };
 
 constexpr int kSpec = 8;
-constexpr int kChaseHold = 16;
+constexpr int kChaseHold = 64;
 constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
 constexpr int kDirect = BCW_CHASE_DIRECT_MAX;  // k_chase workgroups up to which each sums all predecessors' aggregates
 
@@ -224,10 +224,12 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                               uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc,
                                               uint32_t direct_max, uint32_t* __restrict__ equeue,
                                               uint64_t test_abort_wg) {
-  // {crc, start | len << 16} and type of each lane's headers: 9 KiB, so a k_chase workgroup fits beside a k_crc
-  // workgroup (which leaves 11 KiB of the CU's LDS) when another segment's decode is in flight
-  // (ABL & 256, kbench: 64 held headers per lane)
-  constexpr int kHold = (ABL & 256) ? 64 : kChaseHold;
+  // {crc, start | len << 16} and type of each lane's first 64 headers: 36 KiB, so a k_chase workgroup still fits beside
+  // a k_crc workgroup (which leaves 44 KiB of the CU's LDS since round 4) when another segment's decode is in flight.
+  // A block with more headers is chased a second time from the 65th on when its table entries are written (16 held
+  // headers, round 3: config C k_chase 69.5 vs 58.9 us with 64, kbench)
+  // (ABL & 256, kbench: 16 held headers per lane, the round-3 size)
+  constexpr int kHold = (ABL & 256) ? 16 : kChaseHold;
   __shared__ uint32_t s_hold[kHold][2][64];
   __shared__ uint8_t s_type[kHold][64];
   const uint32_t lane = threadIdx.x;
