@@ -188,20 +188,17 @@ __device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg,
   return n;
 }
 
-// the fragment table entry; the stored CRC is kept as the check word J (see Frag)
+// the fragment table entry, one 16 B store (Frag: blk | start, len | chk | type, ok 0, pad 0); the stored CRC is kept
+// as the check word J (see Frag), ic = initc[len]
+__device__ __forceinline__ void put_frag_ic(Frag* __restrict__ frags, uint64_t g, uint64_t frag_cap, uint32_t b,
+                                            uint32_t start_len, uint32_t crc, uint32_t type, uint32_t ic) {
+  if (g >= frag_cap) return;
+  *reinterpret_cast<uint4*>(frags + g) = make_uint4(b, start_len, ~rotl32(crc - 0xa282ead8u, 15) ^ ic, type & 0xffu);
+}
 __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, uint64_t frag_cap, uint32_t b,
                                          uint32_t start, uint32_t len, uint32_t crc, uint32_t type,
                                          const uint32_t* __restrict__ initc) {
-  if (g >= frag_cap) return;
-  Frag f;
-  f.blk = b;
-  f.start = (uint16_t)start;
-  f.len = (uint16_t)len;
-  f.chk = ~rotl32(crc - 0xa282ead8u, 15) ^ initc[len];
-  f.type = (uint8_t)type;
-  f.ok = 0;
-  f.pad = 0;
-  frags[g] = f;
+  put_frag_ic(frags, g, frag_cap, b, start | (len << 16), crc, type, initc[len]);
 }
 
 // Block summary for the record state machine (wal_iterator.go:69-96), written by k_chase from the headers alone:
@@ -365,11 +362,23 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     bsum[b] = make_uint2(tacc | (tnz << 16), tst | (ne ? kSumHasE : 0u));
     if (badk != 0xffffffffu)  // the first unknown-type fragment of the segment (reset by the previous finalize)
       atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_TYPE]), (unsigned long long)(g0 + badk));
+    // the held headers' entries, kWb at a time: their initc[len] loads are issued together (one at a time, each
+    // entry waited one L2 round trip for its load: config C k_chase's table writes took ~17 us of its ~70)
     const uint32_t nh = n < (uint32_t)kHold ? n : (uint32_t)kHold;
-    for (uint32_t k = 0; k < nh; ++k) {
-      const uint32_t sl = s_hold[k][1][lane];
-      put_frag(frags, g0 + k, frag_cap, (uint32_t)b, sl & 0xffffu, sl >> 16, s_hold[k][0][lane], s_type[k][lane],
-               initc);
+    constexpr uint32_t kWb = 16;
+    static_assert(kHold % kWb == 0, "held-header batches stay inside s_hold");
+    for (uint32_t k0 = 0; k0 < nh; k0 += kWb) {
+      uint32_t sl[kWb], ic[kWb];
+#pragma unroll
+      for (uint32_t q = 0; q < kWb; ++q) {
+        sl[q] = s_hold[k0 + q][1][lane];
+        ic[q] = initc[k0 + q < nh ? sl[q] >> 16 : 0u];
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kWb; ++q)
+        if (k0 + q < nh)
+          put_frag_ic(frags, g0 + k0 + q, frag_cap, (uint32_t)b, sl[q], s_hold[k0 + q][0][lane], s_type[k0 + q][lane],
+                      ic[q]);
     }
     if (n > (uint32_t)kHold)  // the tail of a block with more headers than held, chased again from the first of them
       chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {

@@ -367,7 +367,7 @@ int main(int argc, char** argv) {
         ++s.epoch;
       }, reps, st);
     };
-    printf("k_chase alone %.4f  no sum %.4f  no writes %.4f  chase only %.4f ms  hold 64: %.4f ms\n", crun(k_chase<0>),
+    printf("k_chase alone %.4f  no sum %.4f  no writes %.4f  chase only %.4f ms  hold 16: %.4f ms\n", crun(k_chase<0>),
            crun(k_chase<1>), crun(k_chase<2>), crun(k_chase<3>), crun(k_chase<256>));
     CK(hipMemset(&s.misc[7], 0, 24));
     crun(k_chase<16>);
