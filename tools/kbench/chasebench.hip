@@ -25,6 +25,27 @@ __global__ __launch_bounds__(64) void k_hops(const uint8_t* __restrict__ buf, ui
   out[b] = acc;
 }
 
+// a mixed load like config C's chase: every lane hops `base` times, lane 0 of every `every`-th workgroup `lng` times
+// (every = 0: only workgroup 0's lane 0 runs, alone on the device: the unloaded round trip)
+__global__ __launch_bounds__(64) void k_mixed(const uint8_t* __restrict__ buf, uint32_t base, uint32_t lng,
+                                              uint32_t every, uint32_t* __restrict__ out) {
+  const uint64_t b = blockIdx.x * 64ull + threadIdx.x;
+  uint32_t hops = base;
+  if (every == 0) hops = (b == 0) ? lng : 0;
+  else if (threadIdx.x == 0 && blockIdx.x % every == 0) hops = lng;
+  uint64_t off = b * 32768 + 40;
+  uint32_t acc = 0;
+#pragma unroll 1
+  for (uint32_t h = 0; h < hops; ++h) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(buf + (off & ~3ull));
+    const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+    acc ^= w0 ^ w2;
+    off += 7 + (w1 & 0x3ffu);
+    if (off + 12 > (b + 1) * 32768) off = b * 32768 + 40;
+  }
+  out[b] = acc;
+}
+
 int main() {
   const uint64_t n = 1ull << 30;
   uint8_t* d;
@@ -54,5 +75,21 @@ int main() {
   printf("hops 4: block-start %.1f us  random %.1f us\n", t(k_hops<4>, 0), t(k_hops<4>, 1));
   printf("hops 8: block-start %.1f us  random %.1f us\n", t(k_hops<8>, 0), t(k_hops<8>, 1));
   printf("hops 16: block-start %.1f us  random %.1f us\n", t(k_hops<16>, 0), t(k_hops<16>, 1));
+  auto tm = [&](uint32_t base, uint32_t lng, uint32_t every) {
+    float best = 1e9;
+    for (int r = 0; r < 10; ++r) {
+      CK(hipEventRecord(a));
+      k_mixed<<<grid, 64>>>(d, base, lng, every, out);
+      CK(hipEventRecord(e));
+      CK(hipEventSynchronize(e));
+      float ms; CK(hipEventElapsedTime(&ms, a, e));
+      if (ms < best) best = ms;
+    }
+    return best * 1e3;
+  };
+  printf("one lane alone: 1 hop %.1f us, 29 hops %.1f us\n", tm(0, 1, 0), tm(0, 29, 0));
+  printf("all lanes 5 hops %.1f us; + lane 0 of every 8th workgroup 29 hops %.1f us; of every workgroup %.1f us\n",
+         tm(5, 5, 1), tm(5, 29, 8), tm(5, 29, 1));
+  printf("all lanes 2 hops + every 8th workgroup's lane 0 29 hops %.1f us\n", tm(2, 29, 8));
   return 0;
 }
