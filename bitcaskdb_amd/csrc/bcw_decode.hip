@@ -147,7 +147,7 @@ struct Spin {
   }
 };
 
-constexpr int kSpec = 8;
+constexpr int kSpec = 1;  // headers read per round (speculative stride reads: measured slower)
 constexpr int kChaseHold = 64;
 constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
 constexpr int kDirect = BCW_CHASE_DIRECT_MAX;  // k_chase workgroups up to which each sums all predecessors' aggregates

@@ -86,6 +86,37 @@ __global__ __launch_bounds__(WAVES * 64) void k_spat(const uint8_t* __restrict__
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+// the chase loop alone (no ticket, no LDS hold, no sum, no writes): V 0 chase_block with a count-only visit,
+// V 1 a plain one-header-per-round chain
+template <int V>
+__global__ __launch_bounds__(64) void k_chase_probe(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
+                                                    uint64_t nblocks, uint32_t* __restrict__ out) {
+  const uint64_t b = blockIdx.x * 64ull + threadIdx.x;
+  uint32_t bufsize = 0;
+  uint64_t boff = 0;
+  if (b < nblocks) {
+    boff = (uint64_t)start_off + b * kBlock;
+    bufsize = (uint32_t)((seg_len - boff) < kBlock ? (seg_len - boff) : kBlock);
+  }
+  uint32_t acc = 0, n = 0;
+  if (V == 0) {
+    n = chase_block(seg, seg_len, boff, bufsize,
+                    [&](uint32_t, uint32_t, uint32_t len, uint32_t crc, uint32_t ty) { acc ^= crc + len + ty; });
+  } else {
+    uint32_t h = 0;
+    while (h + kHdr <= bufsize) {
+      uint32_t cr, ln, ty;
+      read_header(seg, seg_len, boff + h, cr, ln, ty);
+      const uint32_t st = h + kHdr;
+      if (ln > bufsize - st) ln = bufsize - st;
+      acc ^= cr + ln + ty;
+      ++n;
+      h = st + ln;
+    }
+  }
+  if (b < nblocks) out[b] = acc + n;
+}
+
 template <typename F>
 static float timeit(F f, int reps, hipStream_t st) {
   hipEvent_t a, b;
@@ -369,6 +400,14 @@ int main(int argc, char** argv) {
     };
     printf("k_chase alone %.4f  no sum %.4f  no writes %.4f  chase only %.4f ms  hold 16: %.4f ms\n", crun(k_chase<0>),
            crun(k_chase<1>), crun(k_chase<2>), crun(k_chase<3>), crun(k_chase<256>));
+    {
+      uint32_t* pout;
+      CK(hipMalloc(&pout, (nblocks + 64) * 4));
+      const uint32_t pg = (uint32_t)((nblocks + 63) / 64);
+      const float p0 = timeit([&] { k_chase_probe<0><<<pg, 64, 0, st>>>(d, n, 40, nblocks, pout); }, reps, st);
+      const float p1 = timeit([&] { k_chase_probe<1><<<pg, 64, 0, st>>>(d, n, 40, nblocks, pout); }, reps, st);
+      printf("chase probe: chase_block with a count-only visit %.4f ms, plain one-header chain %.4f ms\n", p0, p1);
+    }
     CK(hipMemset(&s.misc[7], 0, 24));
     crun(k_chase<16>);
     uint64_t m3[3];
