@@ -541,7 +541,8 @@ struct EmitArgs {
   uint64_t* misc;
   uint32_t* equeue;  // [8 x kEqStride] per-XCD emission work-queue heads (reset by k_chase)
   uint32_t kb_flags; // tools/kbench only (0 in the product): 1 = skip the emission at run time
-  uint64_t* kb_stamps;  // tools/kbench only (null in the product): per wave {CRC done, emission done, items}
+  uint64_t* kb_stamps;  // tools/kbench only (null in the product): 8 words per wave {CRC done, emission done, items,
+                        // fragments, entry (real time), entry (shader cycles), emission done (shader cycles), 0}
 };
 
 
@@ -1177,6 +1178,11 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint32_t lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < (uint32_t)kCrcWaves) s_rem[tid] = 0;
+  if (ea.kb_stamps && lane == 0) {  // (kbench: the in-kernel clock = shader cycles / real time between entry and end)
+    uint64_t* q = ea.kb_stamps + 8 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
+    q[4] = wall_clock64();
+    q[5] = __builtin_amdgcn_s_memtime();
+  }
   if (tid == 0) {
     s_wdone = 0;
     s_eq = 0;
@@ -1296,8 +1302,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     q[0] = t_entry; q[1] = t_tables; q[2] = t_crc; q[3] = nfr;
   }
   if (A.kb_stamps && lane == 0) {
-    uint64_t* q = A.kb_stamps + 4 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
+    uint64_t* q = A.kb_stamps + 8 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
     q[0] = t_crc; q[1] = wall_clock64(); q[2] = n_items; q[3] = nfr;
+    q[6] = __builtin_amdgcn_s_memtime();
   }
   // ---- completion: each wave's stores and atomics are done (vmcnt(0)) before it counts itself done in LDS;
   // the last wave of a workgroup adds the workgroup to the agent-scope counter, and the last workgroup's

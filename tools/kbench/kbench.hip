@@ -1,4 +1,5 @@
 #include <unistd.h>
+#include <time.h>
 // k_crc ablation harness (not product code): one TU with the codec sources, times the full decode
 // pipeline and k_crc variants on a synthetic 1 GiB config-B segment.
 #include "../../bitcaskdb_amd/csrc/bcw_api.cpp"
@@ -23,6 +24,24 @@ __global__ __launch_bounds__(256) void k_stream(const uint4* __restrict__ p, uin
     acc ^= v.x ^ v.y ^ v.z ^ v.w;
   }
   if (acc == 0x12345678u) out[0] = acc;
+}
+
+// the same with per-workgroup clock stamps (8 words per workgroup, the k_crc kb_stamps layout: [1] end real time,
+// [4] entry real time, [5] entry shader cycles, [6] end shader cycles)
+__global__ __launch_bounds__(256) void k_stream_clk(const uint4* __restrict__ p, uint64_t n, uint32_t* out,
+                                                    uint64_t* __restrict__ st) {
+  uint64_t t0 = 0, c0 = 0;
+  if (threadIdx.x == 0) { t0 = wall_clock64(); c0 = __builtin_amdgcn_s_memtime(); }
+  uint32_t acc = 0;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull) {
+    const uint4 v = p[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+  if (threadIdx.x == 0) {
+    uint64_t* q = st + 8 * (uint64_t)blockIdx.x;
+    q[1] = wall_clock64(); q[4] = t0; q[5] = c0; q[6] = __builtin_amdgcn_s_memtime();
+  }
 }
 
 // access-pattern probe: each wave reads consecutive 8 KiB pieces = 64 windows x 8 pieces of 16 B;
@@ -196,11 +215,12 @@ int main(int argc, char** argv) {
   EmitArgs ea_off = ea;
   ea_off.kb_flags = 1u;  // the product kernel with its emission skipped at run time
   EmitArgs ea_st = ea;   // ... with per-wave stamps of its CRC end, emission end and items
-  CK(hipMalloc(&ea_st.kb_stamps, 4 * 8 * (size_t)ctx->num_cus * kCrcWaves));
+  CK(hipMalloc(&ea_st.kb_stamps, 8 * 8 * (size_t)ctx->num_cus * kCrcWaves));
   auto stamp_report = [&]() {
     const int nw = ctx->num_cus * kCrcWaves;
-    std::vector<uint64_t> q(4 * (size_t)nw);
-    CK(hipMemcpy(q.data(), ea_st.kb_stamps, q.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> q8(8 * (size_t)nw), q(4 * (size_t)nw);
+    CK(hipMemcpy(q8.data(), ea_st.kb_stamps, q8.size() * 8, hipMemcpyDeviceToHost));
+    for (int w = 0; w < nw; ++w) for (int k = 0; k < 4; ++k) q[4 * w + k] = q8[8 * w + k];
     uint64_t t0 = ~0ull;
     for (int w = 0; w < nw; ++w) t0 = std::min(t0, q[4 * w]);
     std::vector<double> ce(nw), ee(nw);
@@ -216,10 +236,39 @@ int main(int argc, char** argv) {
     int last = 0; for (int w = 0; w < nw; ++w) if (ee[w] > ee[last]) last = w;
     printf("  last wave to finish: w%d CRC end %.1f emission end %.1f items %lu\n", last, ce[last], ee[last], it[last]);
   };
-  auto run = [&](auto kern, int grid, const EmitArgs& a) {
-    return timeit([&] { hipMemsetAsync(s.equeue, 0, 1024, st);  // the emission queues (k_chase resets them)
+  // KB_CLOCK: every timed launch also writes per-wave stamps; last_mhz = the last launch's in-kernel clock (median
+  // over waves of shader cycles / real time), so that a variant's cycles = ms x MHz
+  const bool kb_clock = getenv("KB_CLOCK") != nullptr;
+  uint64_t* clk_st = nullptr;
+  const size_t clk_per = 8 * (size_t)ctx->num_cus * kCrcWaves;
+  if (kb_clock) CK(hipMalloc(&clk_st, clk_per * 8));
+  double last_mhz = 0;
+  auto clock_of = [&](const uint64_t* dq, int nw) {
+    std::vector<uint64_t> q(8 * (size_t)nw);
+    CK(hipMemcpy(q.data(), dq, q.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> f;
+    for (int w = 0; w < nw; ++w) {
+      const uint64_t* e = q.data() + 8 * w;
+      if (e[1] > e[4]) f.push_back((double)(e[6] - e[5]) / (double)(e[1] - e[4]) * 100.0);
+    }
+    std::sort(f.begin(), f.end());
+    return f.empty() ? 0.0 : f[f.size() / 2];
+  };
+  int run_reps = reps;            // 0: run() launches once, untimed (seqk)
+  uint64_t* seq_stamps = nullptr;  // seqk: this launch's stamp slice
+  auto run = [&](auto kern, int grid, const EmitArgs& a0) {
+    EmitArgs a = a0;
+    if (kb_clock && !a.kb_stamps) a.kb_stamps = seq_stamps ? seq_stamps : clk_st;
+    if (run_reps == 0) {
+      hipMemsetAsync(s.equeue, 0, 1024, st);
+      kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, (const uint4*)s.frags, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid);
+      return 0.0f;
+    }
+    const float ms = timeit([&] { hipMemsetAsync(s.equeue, 0, 1024, st);  // the emission queues (k_chase resets them)
                         kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, (const uint4*)s.frags, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid); },
                   reps, st);
+    if (kb_clock && a.kb_stamps == clk_st) last_mhz = clock_of(clk_st, grid * kCrcWaves);
+    return ms;
   };
   const int cus = ctx->num_cus;
   auto runv = [&](int v) -> float {
@@ -262,6 +311,67 @@ int main(int argc, char** argv) {
       default: return run(k_crc<0>, cus, ea);
     }
   };
+  if (argc > 5 && std::string(argv[3]) == "seqk") {  // N back-to-back launches of one kernel, per-launch times
+    // v: -1 plain HBM stream (k_stream), -2 the decode pipeline, otherwise the k_crc variant v (runv's list)
+    const int nrep = atoi(argv[4]), v = atoi(argv[5]);
+    uint32_t* dout;
+    CK(hipMalloc(&dout, 4));
+    std::vector<hipEvent_t> ev(2 * nrep);
+    for (auto& e : ev) CK(hipEventCreate(&e));
+    const uint64_t nb = (n - 40 + kBlock - 1) / kBlock;
+    CK(hipStreamSynchronize(st));
+    // KB_CLOCK (k_crc variants only): every launch writes per-wave stamps into its own slice; the in-kernel clock of a
+    // launch is the median over waves of shader cycles / real time between k_crc's entry and the wave's end
+    const bool clk = getenv("KB_CLOCK") != nullptr && v != -2;
+    const size_t per = 8 * (size_t)cus * kCrcWaves;  // (>= the stream's 16 x cus workgroups)
+    uint64_t* dst = nullptr;
+    if (clk) CK(hipMalloc(&dst, per * 8 * (size_t)nrep));
+    if (getenv("KB_IDLE_MS")) usleep(1000 * atoi(getenv("KB_IDLE_MS")));  // start from an idle chip
+    timespec tm0, tb0;
+    clock_gettime(CLOCK_MONOTONIC, &tm0);
+    clock_gettime(CLOCK_BOOTTIME, &tb0);
+    printf("mark seqk_start mono_ns %lld boot_ns %lld\n", tm0.tv_sec * 1000000000ll + tm0.tv_nsec,
+           tb0.tv_sec * 1000000000ll + tb0.tv_nsec);
+    for (int i = 0; i < nrep; ++i) {
+      CK(hipEventRecord(ev[2 * i], st));
+      if (v == -1 || (v == -3 && (i & 1))) {
+        if (clk) k_stream_clk<<<cus * 16, 256, 0, st>>>((const uint4*)d, n / 16, dout, dst + per * i);
+        else k_stream<<<cus * 16, 256, 0, st>>>((const uint4*)d, n / 16, dout);
+      } else if (v == -2) {
+        CK(launch_decode(d, p, t, dres, ctx->tabs, s, nb, 1, st, cus, nullptr));
+      } else {
+        run_reps = 0;
+        seq_stamps = clk ? dst + per * i : nullptr;
+        runv(v);
+        run_reps = reps;
+        seq_stamps = nullptr;
+      }
+      CK(hipEventRecord(ev[2 * i + 1], st));
+    }
+    CK(hipStreamSynchronize(st));
+    if (clk) {
+      std::vector<uint64_t> q(per * nrep);
+      CK(hipMemcpy(q.data(), dst, q.size() * 8, hipMemcpyDeviceToHost));
+      printf("seqk %d clock MHz:", v);
+      for (int i = 0; i < nrep; ++i) {
+        std::vector<double> f;
+        for (int w = 0; w < cus * 16; ++w) {  // (k_crc: waves; the stream: workgroups)
+          const uint64_t* e = q.data() + per * i + 8 * w;
+          if (e[1] > e[4]) f.push_back((double)(e[6] - e[5]) / (double)(e[1] - e[4]) * 100.0);
+        }
+        std::sort(f.begin(), f.end());
+        printf(" %.0f", f.empty() ? 0.0 : f[f.size() / 2]);
+      }
+      printf("\n");
+    }
+    printf("seqk %d us:", v);
+    for (int i = 0; i < nrep; ++i) {
+      float ms; CK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+      printf(" %.0f", ms * 1e3);
+    }
+    printf("\n");
+    return 0;
+  }
   if (argc > 4 && std::string(argv[3]) == "seq") {  // N back-to-back pipelines (k_chase + k_crc), per-launch times
     const int nrep = atoi(argv[4]);
     const int gap_us = argc > 5 ? atoi(argv[5]) : 0;  // host sleep between launches (0: queued back to back)
@@ -291,11 +401,21 @@ int main(int argc, char** argv) {
   if (argc > 4 && std::string(argv[3]) == "cmp") {  // k_crc variants interleaved in one process (same buffers)
     const int nv = argc - 4;
     std::vector<std::vector<float>> ts(nv);
+    std::vector<std::vector<double>> mc(nv), mh(nv);
     for (int r = 0; r < 7; ++r)
-      for (int i = 0; i < nv; ++i) ts[i].push_back(runv(atoi(argv[4 + i])));
+      for (int i = 0; i < nv; ++i) {
+        const float ms = runv(atoi(argv[4 + i]));
+        ts[i].push_back(ms);
+        mh[i].push_back(last_mhz);
+        mc[i].push_back(ms * last_mhz * 1e-3);  // Mcycles
+      }
     for (int i = 0; i < nv; ++i) {
       std::sort(ts[i].begin(), ts[i].end());
-      printf("k_crc<%s>: min %.4f  median %.4f  max %.4f ms\n", argv[4 + i], ts[i][0], ts[i][3], ts[i][6]);
+      std::sort(mc[i].begin(), mc[i].end());
+      std::sort(mh[i].begin(), mh[i].end());
+      printf("k_crc<%s>: min %.4f  median %.4f  max %.4f ms", argv[4 + i], ts[i][0], ts[i][3], ts[i][6]);
+      if (kb_clock) printf("  | clock median %.0f MHz, Mcycles min %.4f median %.4f", mh[i][3], mc[i][0], mc[i][3]);
+      printf("\n");
     }
     return 0;
   }

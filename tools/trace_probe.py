@@ -46,11 +46,18 @@ ctx.set_stream(stream.cuda_stream)
 torch.cuda.synchronize()
 
 
+def mark(tag):  # host clocks for aligning the kernel trace with tools/power_trace.py's samples
+    print(f"mark {tag} mono_ns {time.clock_gettime_ns(time.CLOCK_MONOTONIC)} "
+          f"boot_ns {time.clock_gettime_ns(time.CLOCK_BOOTTIME)}", flush=True)
+
+
 def run(k):
+    mark("run_start")
     for _ in range(k):
         assert L.lib.bcw_decode_segment_async(ctx.handle, C.c_void_p(seg_ptr), C.byref(params), C.byref(table),
                                               C.c_void_p(d_res.data_ptr())) == 0
     torch.cuda.synchronize()
+    mark("run_end")
 
 
 run(n_rep)
