@@ -119,13 +119,7 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 //
 // The chase is the iterator's header loop (wal_iterator.go:45-77: the block's buffer is
 // min(32768, Size - fileOff) bytes, a header is parsed while bufOff + 7 <= bufSize, the data length is
-// clamped to the buffer), a dependent chain of header reads. To shorten it, once two consecutive Full
-// fragments of the block had the same length (a run of equal-size records, as in every 4 KiB-value
-// block), a round issues kSpec header loads at once at the positions that stride predicts and consumes
-// them while each lies exactly where the chain arrives; the round ends at the first mismatch and the
-// next one starts from the true position. Without that evidence a round reads one header. (Speculating
-// right after the first Full fragment, until a prediction fails, measured slower: config B k_chase
-// 27.4 -> 28.2 us, config C 83 -> 91 us.)
+// clamped to the buffer), a dependent chain of header reads (chase_block).
 // A bounded wait (k_chase's predecessor waits): every spin gives up after 200 ms (a correct wait lasts microseconds)
 // or once another wave has given up, records its site in misc[M_ABORT] and lets the kernel run to its end; the decode
 // then reports BCW_ERR_INTERNAL instead of hanging the device. k_crc skips its CRC pass and emission over the
@@ -147,43 +141,25 @@ struct Spin {
   }
 };
 
-constexpr int kSpec = 1;  // headers read per round (speculative stride reads: measured slower)
 constexpr int kChaseHold = 64;
 constexpr uint64_t kLbAgg = 1, kLbInc = 2, kLbMask = (1ull << 38) - 1;
 constexpr int kDirect = BCW_CHASE_DIRECT_MAX;  // k_chase workgroups up to which each sums all predecessors' aggregates
 
-// visit(k, start, len, crc, type) for every header of the block; returns the fragment count
+// visit(k, start, len, crc, type) for every header of the block from header n at block offset h on; returns the
+// fragment count. One header per round: speculative stride reads (several predicted headers per round once two
+// consecutive Full fragments had equal lengths) cost more than they saved (config C k_chase 60 -> 29 us without
+// them, round 4).
 template <typename V>
 __device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg, uint64_t seg_len, uint64_t boff,
                                                 uint32_t bufsize, V&& visit, uint32_t h = 0, uint32_t n = 0) {
-  uint32_t s = 0;      // predicted distance to the next header (0: read one header)
-  uint32_t lfull = 0;  // length of the last Full fragment (+1; 0: none)
   while (h + kHdr <= bufsize) {
-    uint32_t cr[kSpec], ln[kSpec], ty[kSpec];
-    read_header(seg, seg_len, boff + h, cr[0], ln[0], ty[0]);
-#pragma unroll
-    for (int j = 1; j < kSpec; ++j) {
-      const uint32_t p = h + (uint32_t)j * s;
-      cr[j] = ln[j] = ty[j] = 0;
-      if (s != 0 && p + kHdr <= bufsize) read_header(seg, seg_len, boff + p, cr[j], ln[j], ty[j]);
-    }
-    const uint32_t h0 = h, s0 = s;
-#pragma unroll
-    for (int j = 0; j < kSpec; ++j) {
-      if (j > 0 && (s0 == 0 || h != h0 + (uint32_t)j * s0 || h + kHdr > bufsize)) break;
-      const uint32_t start = h + kHdr;
-      uint32_t len = ln[j];
-      if (len > bufsize - start) len = bufsize - start;
-      visit(n, start, len, cr[j], ty[j]);
-      ++n;
-      h = start + len;
-      if (ty[j] == BCW_RECORD_FULL) {
-        s = (lfull == len + 1) ? kHdr + len : 0;
-        lfull = len + 1;
-      } else {
-        s = 0;
-      }
-    }
+    uint32_t crc, len, type;
+    read_header(seg, seg_len, boff + h, crc, len, type);
+    const uint32_t start = h + kHdr;
+    if (len > bufsize - start) len = bufsize - start;  // wal_iterator.go:75
+    visit(n, start, len, crc, type);
+    ++n;
+    h = start + len;
   }
   return n;
 }
@@ -595,7 +571,7 @@ __device__ __forceinline__ EmitState emit_state(const EmitArgs& A, uint64_t b0, 
 // one lane each.
 // hook(): called once, right after the first chunk's fragment descriptors are requested (the caller issues the
 // next work item's loads there, so they fly beside this item's).
-template <int ABL = 0, typename Hook>  // kbench ablations: 4096 no parse, 8192 no parse and no record-prefix loads
+template <typename Hook>
 __device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& es, uint64_t f0, uint64_t f1,
                                             uint32_t lane, Hook&& hook) {
   if (f0 >= f1) {
@@ -685,12 +661,7 @@ __device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& 
       uint64_t want = size < 64u ? size : 64u;
       if (want > fs.len) want = fs.len;
       rd.nhead = (uint32_t)want;
-      if (ABL & 8192) {
-#pragma unroll
-        for (int k = 0; k < kHeadWords; ++k) rd.h[k] = 0;
-      } else {
-        load_words(A.seg, A.seg_len, a0, rd.h);
-      }
+      load_words(A.seg, A.seg_len, a0, rd.h);
       rd.tstart = ~0ull;
       if (hint) {  // the last bytes: HintRecord.Decode reads fid, offset and size after the key
         uint64_t nt = size < 32u ? size : 32u;
@@ -705,13 +676,7 @@ __device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& 
       rd.f_first = src; rd.f_last = (uint32_t)g;
       uint8_t status, hdr, flags, etag_off;
       uint64_t key_len, val_len, meta_len, expire, aux0, aux1;
-      if (ABL & (4096 | 8192)) {
-        status = (uint8_t)(rd.h[0] == 0x12345u);
-        hdr = flags = etag_off = 0;
-        key_len = val_len = meta_len = expire = aux0 = aux1 = rd.h[1];
-      } else {
-        parse_record(A.p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
-      }
+      parse_record(A.p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
       const bcw_record_table& tab = A.tab;
       if (r < tab.capacity) {
         tab.foff[r] = foff;
@@ -949,195 +914,169 @@ __device__ __forceinline__ uint32_t apply_op_b(const uint32_t* __restrict__ t, u
 }
 
 // Verify fragments [f0, f0 + nfr) of the fragment table (one wave). lds: the kS2Image tables; frd: the fragment
-// table again, read-only: the descriptors are wave-uniform, read by scalar loads (s_load, counted in lgkmcnt). The
-// verdicts collect in a 64-bit mask and reach the table with plain stores every 64 fragments. No path of the chunk
-// loop waits on vmcnt except for its own chunk loads (a vector load with a wait inside the loop makes the compiler
-// merge the paths' counts pessimistically: it then drained nearly every chunk load in flight, vmcnt(1)).
-// Positions are 32-bit, relative to the wave's first chunk (a wave's blocks span far less than 1 GiB).
-// SV: kbench ablations (0 in the product): 1 no chains (words folded by xor), 2 no loads, 4 every chunk takes the
-// fast path (verdicts meaningless). PB: issue-priority balancing (below).
-template <int D, int SV = 0, bool PB = true, int SX = 0>  // SX (kbench): 1 no close, 2 no split op, 4 no masks
+// table again, read-only: the descriptors are wave-uniform, read by scalar loads (s_load, counted in lgkmcnt), one
+// fragment ahead. The verdicts collect in a 64-bit mask and reach the dense verdict array (fok) every 64 fragments.
+//
+// Positions are 32-bit and relative to the wave's first chunk (pos = (blk - blk0) * 32768 + start + adj: a wave's
+// blocks span far fewer than 2^16 blocks). The loop carries little uniform state -- the current and the next fragment
+// (gs, ge, J), the raw descriptor after them, the fragment index, the verdict mask and `ev`, the next chunk that needs
+// more than the fast chain -- so that the unrolled ring keeps it in SGPRs without spills: a chunk c != ev lies inside
+// the open fragment's data (one compare, then the chain), and only chunk ev runs the fragment-end loop. (Round 4's
+// loop kept per-fragment fast-range bounds, a stale-table clamp on every position and ablation switches; it spilled 57
+// SGPRs and its fragment end cost ~160 VALU + ~150 SALU instructions, SQ counters in profiles/r05_clock.)
+// FASTONLY (tools/kbench only): every chunk takes the fast chain (verdicts meaningless).
+template <bool FASTONLY = false>
 __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
                                               uint8_t* __restrict__ fok, const uint4* __restrict__ frd, uint64_t f0,
                                               uint32_t nfr, const uint32_t* __restrict__ lds, uint32_t lane,
                                               uint64_t* __restrict__ misc, uint32_t* __restrict__ s_rem,
                                               uint32_t wslot, const uint8_t* __restrict__ dummy) {
+  constexpr int D = 8;  // chunks in flight per wave (kbench, round 4: 12 within noise of 8, 4 and 6 slower)
   if (nfr == 0) return;
   const uint8_t* tb = reinterpret_cast<const uint8_t*>(lds);
   const uint32_t* s_lop = lds + kS2Slice;
   const uint32_t* s_kop = s_lop + kS2Lop;
   const SliceLane2 sl = slice_lane2(lane);
   const uint4* fd = frd + f0;
-  // the wave's chunks: [c_first, c_end) (absolute chunk indices); positions below are relative to c_first's start
-  uint64_t c_first, c_end;
-  {
-    const uint4 v0 = fd[0], v1 = fd[nfr - 1u];
-    c_first = ((uint64_t)start_off + (uint64_t)v0.x * kBlock + (v0.y & 0xffffu)) / kSChunk;
-    const uint64_t ge_last = (uint64_t)start_off + (uint64_t)v1.x * kBlock + (v1.y & 0xffffu) + (v1.y >> 16);
-    c_end = (ge_last + 4u + kSChunk - 1u) / kSChunk;
-    if (c_end > c_safe_bound(seg_len)) c_end = c_safe_bound(seg_len);  // (a stale table after a given-up wait)
-    if (c_end < c_first) c_end = c_first;
-    if (c_end - c_first > ((1ull << 30) / kSChunk)) c_end = c_first;  // (ditto: never a real wave's range)
-  }
-  const int64_t wbase = (int64_t)(c_first * kSChunk);
+  const uint4 v0 = fd[0], v1 = fd[nfr - 1u];
+  // the wave's chunks: [c_first, c_first + nch), absolute chunk indices
+  const uint64_t c_first = ((uint64_t)start_off + (uint64_t)v0.x * kBlock + (v0.y & 0xffffu)) / kSChunk;
+  const uint64_t ge_last = (uint64_t)start_off + (uint64_t)v1.x * kBlock + (v1.y & 0xffffu) + (v1.y >> 16);
+  uint64_t c_end = (ge_last + 4u + kSChunk - 1u) / kSChunk;
+  if (c_end > c_safe_bound(seg_len)) c_end = c_safe_bound(seg_len);  // (a table bug: reported below, never silent)
+  if (v1.x - v0.x >= (1u << 16) || c_end < c_first) c_end = c_first;  // (ditto: no real wave spans that far)
   const uint32_t nch = (uint32_t)(c_end - c_first);
+  const uint32_t blk0 = v0.x;
+  const int32_t adj = (int32_t)((int64_t)start_off + (int64_t)blk0 * kBlock - (int64_t)(c_first * kSChunk));
   struct G32 { int32_t gs, ge; uint32_t J; };  // wave-relative data range, check word
   constexpr int32_t kFar = 0x40000000;
-  // (readfirstlane: the fragment state is wave-uniform; without it the compiler kept parts of it in VGPRs and moved
-  // them back and forth at every fragment end)
-  auto uni = [](int32_t x) -> int32_t { return __builtin_amdgcn_readfirstlane(x); };
-  auto geo = [&](uint4 v, bool valid) -> G32 {
-    G32 g{kFar, kFar, 0u};
-    if (valid) {
-      g.J = v.z;
-      const int64_t gs = (int64_t)start_off + (int64_t)v.x * kBlock + (v.y & 0xffffu) - wbase;
-      g.gs = gs < 0 ? -64 : (gs > kFar ? kFar : (int32_t)gs);
-      g.ge = g.gs + (int32_t)(v.y >> 16);
-    }
-    g.gs = uni(g.gs);
-    g.ge = uni(g.ge);
-    g.J = (uint32_t)uni((int32_t)g.J);
-    return g;
+  auto geo = [&](uint4 v) -> G32 {
+    const int32_t gs = (int32_t)((v.x - blk0) << 15) + (int32_t)(v.y & 0xffffu) + adj;
+    return G32{gs, gs + (int32_t)(v.y >> 16), v.z};
   };
-  uint32_t i = 0;  // the current fragment (wave-relative): open (H holds its state) or not begun (H = 0)
-  G32 fc = geo(fd[0], true), fn = geo(fd[nfr > 1u ? 1u : 0u], nfr > 1u);
-  uint4 fnn = fd[nfr > 2u ? 2u : 0u];  // fragment i + 2's descriptor, loaded one advance ahead
-  // chunks [fs_lo, fs_lo + fs_n) lie inside the current fragment's data
-  uint32_t fs_lo = 0, fs_n = 0;
-  auto set_fast = [&]() {
-    const int32_t lo = (fc.gs + kSChunk - 1) / kSChunk, hi = fc.ge / kSChunk;
-    fs_lo = (uint32_t)uni(lo);
-    fs_n = (uint32_t)uni(hi > lo ? hi - lo : 0);
-  };
-  set_fast();
+  uint32_t i = 0;  // the current fragment (wave-relative)
+  G32 fc = geo(v0);
+  // fragment i + 1's raw descriptor: its scalar load is issued when fragment i becomes current and first used at the
+  // next chunk ev, so the fast chunks in between hide its latency (a decoded copy carried instead made the compiler
+  // wait for the load at once)
+  uint4 dn = fd[nfr > 1u ? 1u : 0u];
+  uint32_t ev = 0;  // the next chunk that is not inside the open fragment's data (fc begins in chunk 0)
   uint32_t H = 0;
   uint64_t okm = 0;            // verdicts of fragments (i & ~63) + j, bit j
   uint32_t bad = 0xffffffffu;  // first failing fragment (wave-relative)
   auto flush = [&](uint32_t from, uint32_t n) {  // verdicts of fragments [from, from + n) (n <= 64)
     if (lane < n) fok[f0 + from + lane] = (uint8_t)((okm >> lane) & 1u);
   };
-  auto advance = [&]() {
+  // the closing fragment's zero test over the masked chunk words x (its data and J end at pb + 4, chunk-relative),
+  // then the next fragment's state, then the next fragment
+  auto close = [&](const uint32_t (&x)[kSPW], int32_t pb) {
+    const uint32_t e = (uint32_t)(pb + 4);  // the closing fragment's bytes end here (1 <= e <= kSChunk)
+    // lanes < Lf: all theirs; lane Lf: split at word K (K == kSPW: all its piece; K == 0: none of it)
+    const uint32_t Lf = e / kSPiece, K = ((e % kSPiece) + 3u) >> 2;
+    uint32_t cap = 0;
+    const uint32_t s8 = chain_piece2<true>(tb, sl, H, x, K, &cap);
+    const uint32_t Lfull = K == (uint32_t)kSPW ? Lf + 1u : Lf;
+    const uint32_t Lsplit = (K != 0u && K != (uint32_t)kSPW) ? Lf : 64u;
+    const bool full = lane < Lfull, split = lane == Lsplit;
+    // split lane: its captured state shifted by A_{8(4(4-K)+1008)}; lanes after it: the carried H shifted by
+    // A_{8*1024} (table 0); then each lane's share G_l(A_l) = A_{8*16*(63-l)}(A_l), XOR-reduced over the wave
+    const uint32_t A = full ? s8 : apply_op_b(s_kop + (split ? K : 0u) * 1024u, split ? cap : H);
+    const uint32_t T = wave_scan_z(apply_fwd(s_lop, lane, A), [](uint32_t a, uint32_t b) { return a ^ b; });
+    const uint32_t ok = __builtin_amdgcn_readlane(T, 63) == 0u ? 1u : 0u;
+    okm |= (uint64_t)ok << (i & 63u);
+    if (!ok && bad == 0xffffffffu) bad = i;
+    H = s8 ^ A;
     ++i;
     if ((i & 63u) == 0u) {
       flush(i - 64u, 64u);
       okm = 0;
     }
-    fc = fn;
-    fn = geo(fnn, i + 1u < nfr);
-    fnn = fd[i + 2u < nfr ? i + 2u : 0u];
-    set_fast();
   };
-  // the closing fragment's zero test over the masked chunk words x (its data and J end at pb + 4, chunk-relative),
-  // then the next fragment's state
-  auto close = [&](const uint32_t (&x)[kSPW], int32_t pb) {
-    const uint32_t e = (uint32_t)(pb + 4);  // the closing fragment's bytes end here (1 <= e <= kSChunk)
-    // lanes < Lf: all theirs; lane Lf: split at word K
-    const uint32_t Lf = e / kSPiece, K = ((e % kSPiece) + 3u) >> 2;
-    uint32_t cap = 0;
-    const uint32_t s8 = chain_piece2<true>(tb, sl, H, x, K, &cap);
-    // K == kSPW: lane Lf's part ends with its piece (A = s8, as for the lanes before it)
-    const bool full = lane < Lf || (lane == Lf && K == (uint32_t)kSPW);
-    const bool split = lane == Lf && K != 0u;  // (K == 0: the lanes from Lf on hold none of its bytes)
-    const uint32_t A = full ? s8 : ((SX & 2) ? (split ? cap : H) : apply_op_b(s_kop + (split ? K : 0u) * 1024u, split ? cap : H));
-    const uint32_t T = (SX & 1) ? A : wave_scan_z(apply_fwd(s_lop, lane, A), [](uint32_t a, uint32_t b) { return a ^ b; });
-    const bool ok = __builtin_amdgcn_readlane(T, 63) == 0u;
-    okm |= (uint64_t)(ok ? 1u : 0u) << (i & 63u);
-    okm = (uint64_t)(uint32_t)uni((int32_t)(uint32_t)okm) | ((uint64_t)(uint32_t)uni((int32_t)(okm >> 32)) << 32);
-    if (!ok && bad == 0xffffffffu) bad = i;
-    bad = (uint32_t)uni((int32_t)bad);
-    H = s8 ^ A;
-    advance();
-  };
-  auto process = [&](uint32_t c, const uint32_t (&w)[kSPW]) {  // c: wave-relative chunk
-    if ((SV & 4) || c - fs_lo < fs_n) {  // inside the current fragment's data
-      if (SV & 1) H ^= w[0] ^ w[1] ^ w[2] ^ w[3];
-      else H = chain_piece2<false>(tb, sl, H, w);
-      return;
-    }
+  // chunk c == ev: the fragment ends (and beginnings) inside it, one close per end; then the next `ev`
+  auto slow = [&](uint32_t c, const uint32_t (&w)[kSPW]) {
     const int32_t C0 = (int32_t)(c * kSChunk), C1 = C0 + kSChunk;
-    // the usual fragment end, straight-line: the closing fragment began before the chunk, a header follows its data
-    // and the next fragment's data runs on to the chunk's end (config B: nearly every end)
-    if (!(SX & 4) && fc.gs <= C0 && fc.ge + 4 <= C1 && fn.gs - fc.ge == (int32_t)kHdr && fn.gs < C1 && fn.ge >= C1) {
-      uint32_t x[kSPW];
-      mask_gap(x, w, fc.ge - C0, fc.J, lane, lds);
-      close(x, fc.ge - C0);
-      return;
-    }
     auto rel = [&](int32_t p) -> int32_t { return min(max(p - C0, -64), 4096); };
+    G32 fn = i + 1u < nfr ? geo(dn) : G32{kFar, kFar, 0u};
     for (;;) {
-      if (fc.gs >= C1) return;  // (also once every fragment is done: fc.gs = kFar)
+      if (fc.gs >= C1) break;  // not begun here (also once every fragment is done: fc.gs = kFar)
       const bool closes = fc.ge + 4 <= C1;
       // the next fragment shares the chain when its data runs to the chunk's end (bytes [gs, C1) all data, no J)
       const bool next_in = closes && fn.gs < C1 && fn.ge >= C1;
       uint32_t x[kSPW];
       const int32_t pa = rel(fc.gs), pb = rel(fc.ge);
-      if (SX & 4) {
-#pragma unroll
-        for (int q = 0; q < kSPW; ++q) x[q] = w[q];
-      } else if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr)  // a header between two data runs
+      if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr)  // the usual end: a header between two data runs
         mask_gap(x, w, pb, fc.J, lane, lds);
       else
         mask_chunk(x, w, pa, pb, next_in ? rel(fn.gs) : 4096, fc.J, lane, lds);
-      if (!closes) {
+      if (!closes) {  // the data (or J) runs on into the next chunk
         H = chain_piece2<false>(tb, sl, H, x);
-        return;
+        break;
       }
       close(x, pb);
-      if (next_in) return;
+      fc = fn;
+      dn = fd[i + 1u < nfr ? i + 1u : 0u];
+      if (next_in) break;
+      fn = i + 1u < nfr ? geo(dn) : G32{kFar, kFar, 0u};
     }
+    // open: fc's bytes so far are in H; its data ends in chunk fc.ge / kSChunk (its J may straddle into the next)
+    const uint32_t nx = c + 1u;
+    ev = fc.gs < C1 ? max((uint32_t)fc.ge / (uint32_t)kSChunk, nx) : nx;
+  };
+  auto step = [&](uint32_t c, const uint32_t (&w)[kSPW]) {
+    if (FASTONLY || c != ev) H = chain_piece2<false>(tb, sl, H, w);
+    else slow(c, w);
   };
   const uint64_t c_safe = seg_len / kSChunk;  // chunks [0, c_safe) lie inside the segment
   const uint32_t nl = c_safe > c_first ? (uint32_t)min(c_safe - c_first, (uint64_t)nch) : 0u;  // pipelined chunks
   if (nl > 0u) {
-    const uint8_t* sbase = seg + c_first * kSChunk + lane * kSPiece;
-    // the loads issued past the last chunk read 1 KiB of the table image instead, which every workgroup has just
-    // read (an L2 hit): reloading the wave's own first chunk cost 8 KiB of HBM reads per wave (32 MB per launch)
-    const uint8_t* dbase = dummy + lane * kSPiece;
+    const uint8_t* wseg = seg + c_first * kSChunk;
+    const uint32_t lane16 = lane * kSPiece;
     uint32_t buf[D][kSPW];
-    auto issue = [&](uint32_t c, uint32_t (&w)[kSPW]) {  // unconditional (no branch around a load)
-      if (SV & 2) {
-#pragma unroll
-        for (int k = 0; k < kSPW; ++k) w[k] = c * 2654435761u + lane * 40503u + k;
-        return;
-      }
-      // non-temporal: the segment is read once (kbench spat: 185 -> 160 us for the whole segment)
+    // unconditional (no branch around a load); the loads issued past the last chunk read 1 KiB of the table image
+    // instead, which every workgroup has just read (an L2 hit)
+    auto issue = [&](uint32_t c, uint32_t (&w)[kSPW]) {
+      const uint8_t* p = c < nl ? wseg + (size_t)c * kSChunk : dummy;  // uniform: the lane offset is the VGPR part
       typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-      const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(c < nl ? sbase + (size_t)c * kSChunk : dbase));
+      // non-temporal: the segment is read once (kbench spat: 185 -> 160 us for the whole segment)
+      const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p + lane16));
       w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
     };
 #pragma unroll
     for (int k = 0; k < D; ++k) issue((uint32_t)k, buf[k]);
     for (uint32_t c = 0; c < nl; c += D) {
-      if (PB) {
-        // issue-priority balancing: a SIMD's issue arbiter serves its oldest wave first, so with equal shares the four
-        // waves of a SIMD finished up to 50 us apart and the last of them streamed alone. Each wave publishes its
-        // chunks left (s_rem[simd][age]) and runs at priority 2 while it has (nearly) the most left on its SIMD.
-        const uint32_t left = nl - c;
-        if (lane == 0) s_rem[wslot] = left;
-        const uint4 r = *reinterpret_cast<const uint4*>(s_rem + (wslot & ~3u));
-        const uint32_t mx = max(max(r.x, r.y), max(r.z, r.w));
-        if (left + (uint32_t)D >= mx) __builtin_amdgcn_s_setprio(2);
-        else __builtin_amdgcn_s_setprio(0);
-      }
+      // issue-priority balancing: a SIMD's issue arbiter serves its oldest wave first, so with equal shares the four
+      // waves of a SIMD finished up to 50 us apart and the last of them streamed alone. Each wave publishes its
+      // chunks left (s_rem[simd][age]) and runs at priority 2 while it has (nearly) the most left on its SIMD.
+      const uint32_t left = nl - c;
+      if (lane == 0) s_rem[wslot] = left;
+      const uint4 r = *reinterpret_cast<const uint4*>(s_rem + (wslot & ~3u));
+      const uint32_t mx = max(max(r.x, r.y), max(r.z, r.w));
+      if (left + (uint32_t)D >= mx) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         // chunk c + k, then its registers take chunk c + k + D (no copy: a copy would make the loop carry two sets
         // and wait for every load at the back-edge)
-        if (c + k < nl) process(c + k, buf[k]);
+        if (c + k < nl) step(c + k, buf[k]);
         issue(c + k + D, buf[k]);
       }
     }
   }
   for (uint32_t c = nl; c < nch; ++c) {  // chunks touching the segment's end
     uint32_t w[kSPW];
-    const uint4 A = load16_safe(seg, seg_len, wbase + (int64_t)c * kSChunk + lane * kSPiece);
+    const uint4 A = load16_safe(seg, seg_len, (int64_t)((c_first + c) * kSChunk) + lane * kSPiece);
     w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
-    process(c, w);
+    step(c, w);
   }
-  flush(i & ~63u, i & 63u);  // (i == nfr: every fragment closed)
-  if ((SV & 7) && H == 0x9e3779b9u) misc[7] = H;  // (kbench ablations: keep the chains alive)
-  if (bad != 0xffffffffu && lane == 0)
-    atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_CRC]), (unsigned long long)(f0 + bad));
+  flush(i & ~63u, i & 63u);
+  if (FASTONLY && H == 0x9e3779b9u) misc[7] = H;  // (kbench: keep the chains alive)
+  if (lane == 0) {
+    if (bad != 0xffffffffu)
+      atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_CRC]), (unsigned long long)(f0 + bad));
+    // every fragment of the wave is closed by its chunks; one that is not means the fragment table and the chunk range
+    // disagree (a bug): report the decode as failed (BCW_ERR_INTERNAL) instead of passing the fragment unverified
+    if (!FASTONLY && i < nfr) atomicMax(reinterpret_cast<unsigned long long*>(&misc[M_ABORT]), 20ull);
+  }
 }
 
 // The arguments of k_crc's record emission and completion, parked in LDS during the CRC pass: kept in SGPRs they
@@ -1153,9 +1092,8 @@ struct CrcTail {
 // k_crc: one 1024-thread workgroup per CU. Each wave verifies the fragments of its share of the blocks (stream_verify),
 // then takes record-emission items of its workgroup's blocks (emit_chunks); the last wave of the last workgroup
 // writes the segment result (finalize).
-// ABL: kbench ablations (0 in the product): 8 no emission, 512 per-wave stamps {entry, tables, CRC done, fragments}
-// into the expire column, 32768 no CRC pass (the emission alone); bits 21-23: stream_verify's SV; bits 24-27: its
-// chunk prefetch depth D (0: 8)
+// ABL: tools/kbench ablations (0 in the product): 8 no emission, 32768 no CRC pass (the emission alone), 8388608 every
+// chunk on the fast chain (stream_verify<true>)
 template <int ABL = 0>
 __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                      uint32_t start_off, uint64_t nblocks,
@@ -1173,7 +1111,6 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   __shared__ uint32_t s_wdone;  // waves of this workgroup done
   __shared__ uint32_t s_eq;     // the workgroup's emission items taken
   __shared__ __attribute__((aligned(16))) uint32_t s_rem[kCrcWaves];  // chunks left per wave [simd][age] (stream_verify)
-  const uint64_t t_entry = (ABL & 512) ? wall_clock64() : 0;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1190,15 +1127,10 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   }
   const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
   const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
-  // the CRC stream runs on the first SW waves of the workgroup; the last kCrcWaves - SW (the youngest wave of each
-  // SIMD, the one its issue arbiter serves last) take record-emission items from the start, so the latency-bound
-  // emission overlaps the stream instead of following it (ABL bits 28-30, kbench: v != 0 -> v - 1 emission waves)
-  constexpr int EW = ((ABL >> 28) & 7) ? ((ABL >> 28) & 7) - 1 : kCrcEmitWaves;
-  constexpr int SW = kCrcWaves - EW;
-  const bool streams = wave < (uint32_t)SW;
-  const uint64_t nsw = (uint64_t)gridDim.x * SW, gsw = (uint64_t)blockIdx.x * SW + (streams ? wave : 0u);
+  // every wave streams the fragments of its 1 / (16 x CUs) share of the blocks (dedicated emission waves measured
+  // slower)
   const uint64_t cn = cb1 - cb0;
-  const uint64_t b0 = cb0 + cn * gsw / nsw, b1 = streams ? cb0 + cn * (gsw + 1) / nsw : b0;
+  const uint64_t b0 = cb0 + cn * gw / nw, b1 = cb0 + cn * (gw + 1) / nw;
   const uint64_t f0 = fbase[b0];
   uint64_t f1 = fbase[b1];
   if (f1 > frag_cap) f1 = frag_cap;
@@ -1223,7 +1155,6 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   }
   __syncthreads();
   if (blockIdx.x == 0 && tid == 0) misc[M_T_CRC0] = wall_clock64();
-  const uint64_t t_tables = (ABL & 512) ? wall_clock64() : 0;
   const uint32_t nfr = f1 > f0 ? (uint32_t)(f1 - f0) : 0u;
   // ---- record emission: the workgroup's work items (those starting in its blocks), taken from an LDS counter by
   // its waves as they finish their CRC streams (ItemMeta). The next item is taken and its block data requested while
@@ -1270,7 +1201,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       const uint64_t mf1 = m.f1 < fcap ? m.f1 : fcap;
       uint64_t nx = ~0ull;
       ItemMeta mn = m;
-      emit_chunks<ABL & (4096 | 8192)>(A, es, m.f0, mf1, lane, [&]() {
+      emit_chunks(A, es, m.f0, mf1, lane, [&]() {
         if (taken < max_items) {
           nx = deq();
           mn = item_meta(A, nx, bpw, cb0t, cb1t, lane);
@@ -1282,11 +1213,11 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     n_items += taken;
   };
   if (!(ABL & 32768))
-    stream_verify<(ABL >> 24) & 15 ? (ABL >> 24) & 15 : 8, (ABL >> 21) & 7, !(ABL & 1048576), (ABL >> 16) & 15>(
-        seg, seg_len, start_off, fok, frags_ro, f0, nfr, lds, lane, misc, s_rem, (wave & 3u) * 4u + (wave >> 2),
-        reinterpret_cast<const uint8_t*>(tabs.lds_image2));
+    stream_verify<(ABL & 8388608) != 0>(seg, seg_len, start_off, fok, frags_ro, f0, nfr, lds, lane, misc, s_rem,
+                                        (wave & 3u) * 4u + (wave >> 2),
+                                        reinterpret_cast<const uint8_t*>(tabs.lds_image2));
   __builtin_amdgcn_s_setprio(0);
-  const uint64_t t_crc = (ABL & 512) || ea.kb_stamps ? wall_clock64() : 0;
+  const uint64_t t_crc = ea.kb_stamps ? wall_clock64() : 0;
   emit_items(~0ull);
   asm volatile("" ::: "memory");  // (reload the tail arguments from LDS, see CrcTail)
   CrcTail T;
@@ -1297,10 +1228,6 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     for (int k = 0; k < (int)(sizeof(CrcTail) / 4); ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
   }
   const EmitArgs& A = T.ea;
-  if ((ABL & 512) && lane == 0) {
-    uint64_t* q = A.tab.expire + 4 * gw;  // kbench only (the table is overwritten by the emission unless ABL & 8)
-    q[0] = t_entry; q[1] = t_tables; q[2] = t_crc; q[3] = nfr;
-  }
   if (A.kb_stamps && lane == 0) {
     uint64_t* q = A.kb_stamps + 8 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
     q[0] = t_crc; q[1] = wall_clock64(); q[2] = n_items; q[3] = nfr;

@@ -70,7 +70,6 @@ constexpr int kS2Image = kS2Gap + 4 * kS2GapN + 4;  // (+ pad to 16 B)
 #endif
 constexpr int kCrcWaves = BCW_CRC_WAVES;  // waves per k_crc workgroup (one workgroup per CU)
 constexpr int kCrcThreads = kCrcWaves * 64;
-constexpr int kCrcEmitWaves = 0;  // of them, the waves that start with record emission (bcw_decode.hip k_crc)
 
 struct Scratch {
   uint64_t nblocks_cap = 0;

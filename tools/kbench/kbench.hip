@@ -273,41 +273,12 @@ int main(int argc, char** argv) {
   const int cus = ctx->num_cus;
   auto runv = [&](int v) -> float {
     switch (v) {
-      case 2097152: return run(k_crc<2097152>, cus, ea);  // stream: no chains
-      case 4194304: return run(k_crc<4194304>, cus, ea);  // stream: no loads
-      case 8388608: return run(k_crc<8388608>, cus, ea);  // stream: fast path only
-      case 10485760: return run(k_crc<10485760>, cus, ea);  // stream: fast path only, no chains
       case 8: return run(k_crc<8>, cus, ea);              // no emission
-      case 8388616: return run(k_crc<8388616>, cus, ea);  // fast path only, no emission
-      case 10485768: return run(k_crc<10485768>, cus, ea);  // fast path only, no chains, no emission
-      case 10486280: return run(k_crc<10486280>, cus, ea);  // the same with per-wave stamps
-      case 33554432: return run(k_crc<33554432>, cus, ea);  // D = 2
-      case 100663296: return run(k_crc<100663296>, cus, ea);  // D = 6
-      case 67108864: return run(k_crc<67108864>, cus, ea);  // D = 4
-      case 201326592: return run(k_crc<201326592>, cus, ea);  // D = 12
-      case 134217728: return run(k_crc<134217728>, cus, ea);  // D = 8
+      case 8388608: return run(k_crc<8388608>, cus, ea);  // every chunk on the fast chain
+      case 8388616: return run(k_crc<8388616>, cus, ea);  // the same without emission
+      case 32768: return run(k_crc<32768>, cus, ea);      // emission only (no CRC pass)
       case 99: return run(k_crc<0>, cus, ea_off);
-      case 32768: return run(k_crc<32768>, cus, ea);
-      case 40960: return run(k_crc<32768 | 8192>, cus, ea);
-      case 32776: return run(k_crc<32768 | 8>, cus, ea);
-      case 36864: return run(k_crc<32768 | 4096>, cus, ea);
       case 98: { const float r = run(k_crc<0>, cus, ea_st); stamp_report(); return r; }
-      case 97: { const float r = run(k_crc<10485760>, cus, ea_st); stamp_report(); return r; }  // fast, no chain
-      case 520: return run(k_crc<520>, cus, ea);
-      case 65544: return run(k_crc<65544>, cus, ea);    // no emission, no close
-      case 131080: return run(k_crc<131080>, cus, ea);  // no emission, no split op
-      case 262152: return run(k_crc<262152>, cus, ea);  // no emission, no masks
-      case 458760: return run(k_crc<458760>, cus, ea);  // no emission, none of the three
-      case 1048576: return run(k_crc<1048576>, cus, ea);  // no priority balancing
-      case 1048584: return run(k_crc<1048584>, cus, ea);  // no priority balancing, no emission
-      case 1049096: return run(k_crc<1049096>, cus, ea);  // the same with per-wave stamps
-      case 268435456: return run(k_crc<268435456>, cus, ea);    // no emission-first waves
-      case 536870912: return run(k_crc<536870912>, cus, ea);    // 1
-      case 805306368: return run(k_crc<805306368>, cus, ea);    // 2
-      case 1342177280: return run(k_crc<1342177280>, cus, ea);  // 4
-      case 1879048192: return run(k_crc<1879048192>, cus, ea);  // 6
-      case 4096: return run(k_crc<4096>, cus, ea);
-      case 8192: return run(k_crc<8192>, cus, ea);
       default: return run(k_crc<0>, cus, ea);
     }
   };
@@ -445,55 +416,12 @@ int main(int argc, char** argv) {
     }
     CK(hipStreamSynchronize(st));
     printf("k_crc<%d> x%d done, %.4f ms\n", v, k, tm);
-    if (v == 520 || v == 1544 || v == 10486280 || v == 1049096) {  // per-wave stamps of the last launch: start / tables / loop end, by XCD (blockIdx % 8)
-      const int nw = cus * kCrcWaves;
-      std::vector<uint64_t> q(4 * (size_t)nw);
-      CK(hipMemcpy(q.data(), t.expire, q.size() * 8, hipMemcpyDeviceToHost));
-      uint64_t t0 = ~0ull, tmax = 0;
-      for (int w = 0; w < nw; ++w) { t0 = std::min(t0, q[4 * w]); tmax = std::max(tmax, q[4 * w + 2]); }
-      std::vector<double> ends(nw);
-      double xs[8] = {0}, xe[8] = {0}, xm[8] = {0}; int xn[8] = {0};
-      for (int w = 0; w < nw; ++w) {
-        const int x = (w / kCrcWaves) % 8;
-        const double st = (q[4 * w] - t0) / 100.0, en = (q[4 * w + 2] - t0) / 100.0;
-        ends[w] = en; xs[x] += st; xe[x] += en; xm[x] = std::max(xm[x], en); ++xn[x];
-      }
-      std::vector<double> so = ends; std::sort(so.begin(), so.end());
-      printf("wave loop end (us from first entry): min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f\n", so[0], so[nw / 10],
-             so[nw / 2], so[nw * 9 / 10], so[nw - 1]);
-      for (int x = 0; x < 8; ++x)
-        printf("  xcd %d: mean start %.1f  mean end %.1f  max end %.1f us\n", x, xs[x] / xn[x], xe[x] / xn[x], xm[x]);
-      double ss[kCrcWaves] = {0};
-      for (int w = 0; w < nw; ++w) ss[w % kCrcWaves] += ends[w];
-      printf("  mean end by wave slot:");
-      for (int k = 0; k < kCrcWaves; ++k) printf(" %.1f", ss[k] / (nw / kCrcWaves));
-      printf("\n");
-      std::vector<double> cuend(cus), cuspread(cus);
-      for (int c = 0; c < cus; ++c) {
-        double mx = 0, mn = 1e30, sm = 0;
-        for (int k = 0; k < kCrcWaves; ++k) { const double e = ends[c * kCrcWaves + k]; mx = std::max(mx, e); mn = std::min(mn, e); sm += e; }
-        cuend[c] = sm / kCrcWaves; cuspread[c] = mx - mn;
-      }
-      std::sort(cuend.begin(), cuend.end()); std::sort(cuspread.begin(), cuspread.end());
-      printf("  per-WG mean end: min %.1f p50 %.1f max %.1f | per-WG spread (max-min): p10 %.1f p50 %.1f p90 %.1f\n",
-             cuend[0], cuend[cus / 2], cuend[cus - 1], cuspread[cus / 10], cuspread[cus / 2], cuspread[cus * 9 / 10]);
-      {  // slowest waves: their fragment counts
-        std::vector<std::pair<double, int>> ew(nw);
-        for (int w = 0; w < nw; ++w) ew[w] = {ends[w], w};
-        std::sort(ew.begin(), ew.end());
-        printf("  fastest/slowest waves (end us, frags):");
-        for (int k : {0, 1, 2, nw - 3, nw - 2, nw - 1}) printf(" [w%d %.1f %lu]", ew[k].second, ew[k].first, q[4 * ew[k].second + 3]);
-        printf("\n");
-      }
-      double tl = 0; for (int w = 0; w < nw; ++w) tl += (q[4 * w + 1] - q[4 * w]) / 100.0;
-      printf("  mean table-load time %.2f us\n", tl / nw);
-    }
     return 0;
   }
-  const float a0 = run(k_crc<0>, cus, ea), a1 = run(k_crc<2097152>, cus, ea), a2 = run(k_crc<4194304>, cus, ea),
-              a8 = run(k_crc<8>, cus, ea), a9 = run(k_crc<32768>, cus, ea);
+  const float a0 = run(k_crc<0>, cus, ea), a1 = run(k_crc<8388616>, cus, ea), a8 = run(k_crc<8>, cus, ea),
+              a9 = run(k_crc<32768>, cus, ea);
   printf("k_crc full      %.4f ms  %.1f GB/s\n", a0, n / (a0 * 1e-3) / 1e9);
-  printf("k_crc no fast-path chain %.4f  no loads %.4f  no emission %.4f  emission only %.4f ms\n", a1, a2, a8, a9);
+  printf("k_crc fast chain only (no emission) %.4f  no emission %.4f  emission only %.4f ms\n", a1, a8, a9);
   const float as = timeit([&] {
     hipMemsetAsync(&s.misc[M_DONE_CRC], 0, 8, st);  // the last workgroup finalizes
     hipMemsetAsync(s.equeue, 0, 1024, st);
