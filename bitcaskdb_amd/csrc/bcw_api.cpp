@@ -24,11 +24,6 @@ static void byte_table(uint32_t* t0) {
   }
 }
 
-void build_slice_tables(uint32_t* t) {
-  byte_table(t);
-  for (int b = 0; b < 256; ++b) t[256 + b] = (t[b] >> 8) ^ t[t[b] & 0xffu];
-}
-
 static inline uint32_t zero_step(const uint32_t* t0, uint32_t s) { return (s >> 8) ^ t0[s & 0xffu]; }
 
 // images of the 32 basis vectors under "advance over n zero bytes"
@@ -44,30 +39,6 @@ static inline uint32_t apply_basis(const uint32_t* img, uint32_t x) {
   for (int i = 0; x; ++i, x >>= 1)
     if (x & 1u) r ^= img[i];
   return r;
-}
-
-// fwd[l][i][n] = F_l(n << 4i), F_l = A_{8*128*(63-l)};  carry[i][n] = A_{8*8192}(n << 4i);
-// half[i][n] = A_{8*64}(n << 4i)
-void build_lane_tables(uint32_t* fwd, uint32_t* carry, uint32_t* half) {
-  uint32_t t0[256];
-  byte_table(t0);
-  uint32_t step128[32];
-  shift_basis(t0, kWin, step128);
-  uint32_t m[32];
-  for (int i = 0; i < 32; ++i) m[i] = 1u << i;  // identity for lane 63
-  for (int l = 63; l >= 0; --l) {
-    for (int i = 0; i < 8; ++i)
-      for (uint32_t n = 0; n < 16; ++n) fwd[(l * 8 + i) * 16 + n] = apply_basis(m, n << (4 * i));
-    for (int i = 0; i < 32; ++i) m[i] = apply_basis(step128, m[i]);
-  }
-  uint32_t c8k[32];
-  shift_basis(t0, 8192, c8k);
-  for (int i = 0; i < 8; ++i)
-    for (uint32_t n = 0; n < 16; ++n) carry[i * 16 + n] = apply_basis(c8k, n << (4 * i));
-  uint32_t h64[32];
-  shift_basis(t0, 64, h64);
-  for (int i = 0; i < 8; ++i)
-    for (uint32_t n = 0; n < 16; ++n) half[i * 16 + n] = apply_basis(h64, n << (4 * i));
 }
 
 // basis images of the inverse of a (bijective) GF(2)-linear map given by its basis images
@@ -268,9 +239,7 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
     c->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return BCW_E_HIP; }
   c->cur = c->own;
-  std::vector<uint32_t> slice(512), fwd(64 * 128), carry(128), half(128), initc(kBlock + 1);
-  build_slice_tables(slice.data());
-  build_lane_tables(fwd.data(), carry.data(), half.data());
+  std::vector<uint32_t> initc(kBlock + 1);
   build_initc(initc.data());
   std::vector<uint32_t> enc_ops(kEncOpsWords);
   build_enc_ops(enc_ops.data());
@@ -285,21 +254,6 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
       memcpy(img, sq, sizeof img);
     }
   }
-  std::vector<uint32_t> image(kLdsImage);
-  {  // slice-by-4 rows (see crc_window): row e = {T3[e] x16, T2[e] x16, T1[e] x16, T0[e] x16}
-    uint32_t tk[4][256];
-    byte_table(tk[0]);
-    for (int k = 1; k < 4; ++k)
-      for (int e = 0; e < 256; ++e) tk[k][e] = (tk[k - 1][e] >> 8) ^ tk[0][tk[k - 1][e] & 0xffu];
-    for (int e = 0; e < 256; ++e)
-      for (int t = 0; t < 4; ++t)
-        for (int r = 0; r < 16; ++r) image[e * 64 + t * 16 + r] = tk[3 - t][e];
-  }
-  for (int i = 0; i < kLdsFwd; ++i) image[kLdsSlice + i] = fwd[(i & 63) * 128 + (i >> 6)];
-  for (int i = 0; i < 128; ++i) {
-    image[kLdsSlice + kLdsFwd + i] = carry[i];
-    image[kLdsSlice + kLdsFwd + 128 + i] = half[i];
-  }
   std::vector<uint32_t> image2(kS2Image);
   {  // stream verify (bcw_internal.h kS2*): slice rows with the shifted tables, lane operators, split operators
     uint32_t tk[4][256], t0[256], img[32], nib[128], step[32], m[32];
@@ -312,21 +266,21 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
     for (int e = 0; e < 256; ++e)
       for (int s = 0; s < 4; ++s)
         for (int cp = 0; cp < 8; ++cp) {
-          image2[e * 64 + s * 8 + cp] = tk[3 - s][e];
-          image2[e * 64 + 32 + s * 8 + cp] = apply_basis(sh, tk[3 - s][e]);
+          image2[kS2SliceOff + e * 64 + s * 8 + cp] = tk[3 - s][e];
+          image2[kS2SliceOff + e * 64 + 32 + s * 8 + cp] = apply_basis(sh, tk[3 - s][e]);
         }
     shift_basis(t0, kSPiece, step);
     for (int i = 0; i < 32; ++i) m[i] = 1u << i;  // identity for lane 63
     for (int l = 63; l >= 0; --l) {
       nibble_image(m, nib);
-      for (int k = 0; k < 128; ++k) image2[kS2Slice + k * 64 + l] = nib[k];
+      for (int k = 0; k < 128; ++k) image2[kS2LopOff + k * 64 + l] = nib[k];
       for (int i = 0; i < 32; ++i) m[i] = apply_basis(step, m[i]);
     }
     for (int k = 0; k < kSPW; ++k) {  // split operators as byte tables: [k][t][e] = A(e << 8t)
       shift_basis(t0, 4u * (kSPW - k) + (kSChunk - kSPiece), img);
       for (int t = 0; t < 4; ++t)
         for (uint32_t e = 0; e < 256; ++e)
-          image2[kS2Slice + kS2Lop + (k * 4 + t) * 256 + e] = apply_basis(img, e << (8 * t));
+          image2[kS2KopOff + (k * 4 + t) * 256 + e] = apply_basis(img, e << (8 * t));
     }
     auto put_bytes = [&](int at, const uint8_t (&b)[16]) {
       for (int w = 0; w < 4; ++w)
@@ -357,23 +311,13 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
   }
   bool ok = hipMalloc(&c->tabs.lds_image2, image2.size() * 4) == hipSuccess &&
             hipMemcpy(c->tabs.lds_image2, image2.data(), image2.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
-  ok = ok && hipMalloc(&c->tabs.slice, slice.size() * 4) == hipSuccess &&
-            hipMalloc(&c->tabs.fwd, fwd.size() * 4) == hipSuccess &&
-            hipMalloc(&c->tabs.carry, carry.size() * 4) == hipSuccess &&
-            hipMalloc(&c->tabs.half, half.size() * 4) == hipSuccess &&
-            hipMalloc(&c->tabs.initc, initc.size() * 4) == hipSuccess &&
-            hipMalloc(&c->tabs.lds_image, image.size() * 4) == hipSuccess &&
+  ok = ok && hipMalloc(&c->tabs.initc, initc.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.enc_ops, enc_ops.size() * 4) == hipSuccess &&
             hipMalloc(&c->tabs.pow2, pow2.size() * 4) == hipSuccess &&
             hipMalloc(&c->d_eres, sizeof(bcw_encode_result)) == hipSuccess &&
             hipMalloc(&c->d_result, sizeof(bcw_decode_result)) == hipSuccess &&
             hipMalloc(&c->d_ires, sizeof(bcw_index_result)) == hipSuccess;
-  ok = ok && hipMemcpy(c->tabs.slice, slice.data(), slice.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemcpy(c->tabs.fwd, fwd.data(), fwd.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemcpy(c->tabs.carry, carry.data(), carry.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemcpy(c->tabs.half, half.data(), half.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemcpy(c->tabs.initc, initc.data(), initc.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-       hipMemcpy(c->tabs.lds_image, image.data(), image.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+  ok = ok && hipMemcpy(c->tabs.initc, initc.data(), initc.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.enc_ops, enc_ops.data(), enc_ops.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
        hipMemcpy(c->tabs.pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
   if (!ok) { bcw_ctx_destroy(c); return BCW_E_NOMEM; }
@@ -388,6 +332,7 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.lb);
   (void)hipFree(s.lbe);
   (void)hipFree(s.frags);
+  (void)hipFree(s.srec);
   (void)hipFree(s.fok);
   (void)hipFree(s.misc);
   (void)hipFree(s.equeue);
@@ -424,12 +369,7 @@ int bcw_ctx_destroy(bcw_ctx* c) {
   (void)hipFree(c->d_keep);
   (void)hipFree(c->d_eout);
   (void)hipFree(c->d_eres);
-  (void)hipFree(c->tabs.slice);
-  (void)hipFree(c->tabs.fwd);
-  (void)hipFree(c->tabs.carry);
-  (void)hipFree(c->tabs.half);
   (void)hipFree(c->tabs.initc);
-  (void)hipFree(c->tabs.lds_image);
   (void)hipFree(c->tabs.lds_image2);
   (void)hipFree(c->d_seg);
   (void)hipFree(c->d_tab_mem);
@@ -461,11 +401,13 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   const uint64_t nb = std::max(nblocks, s.nblocks_cap);
   const uint64_t fc = std::max(frag_cap, s.frag_cap);
   free_scratch(s);
-  // look-back words: one per 64-block k_chase workgroup
+  // look-back words: one per 64-block k_chase workgroup. The stream records have 4 entries of slack: k_crc's stream
+  // loads the record after a wave's current fragment unconditionally (bcw_decode.hip, stream_verify)
   const uint64_t nwg = std::max<uint64_t>(nb / 64 + 2, (uint64_t)c->num_cus + 2);
   bool ok = hipMalloc(&s.fbase, (nb + 1) * 4) == hipSuccess && hipMalloc(&s.rbase, (nb + 1) * 4) == hipSuccess &&
             hipMalloc(&s.bsum, (nb + 1) * sizeof(uint2)) == hipSuccess && hipMalloc(&s.lb, nwg * 8) == hipSuccess &&
             hipMalloc(&s.lbe, nwg * 8) == hipSuccess && hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
+            hipMalloc(&s.srec, (fc + 4) * sizeof(uint4)) == hipSuccess &&
             hipMalloc(&s.fok, fc) == hipSuccess &&
             hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess && hipMalloc(&s.equeue, 8 * 128) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }

@@ -164,17 +164,36 @@ __device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg,
   return n;
 }
 
-// the fragment table entry, one 16 B store (Frag: blk | start, len | chk | type, ok 0, pad 0); the stored CRC is kept
-// as the check word J (see Frag), ic = initc[len]
-__device__ __forceinline__ void put_frag_ic(Frag* __restrict__ frags, uint64_t g, uint64_t frag_cap, uint32_t b,
-                                            uint32_t start_len, uint32_t crc, uint32_t type, uint32_t ic) {
+// The fragment table entry, one 16 B store (Frag: blk | start, len | chk | type, ok 0, pad 0; the stored CRC is kept as
+// the check word J, see Frag; ic = initc[len]), and the fragment's stream record (k_crc's stream verify reads only
+// these): x = end chunk ce = ge / 1024, y = begin chunk cb = gs / 1024 (absolute 1 KiB chunks of the segment; gs, ge
+// the data's absolute byte range), z = J, w = pb | pa << 10 | kRecUsual | kRecAdj with pb = ge % 1024, pa = gs % 1024.
+// kRecAdj: the next fragment's data starts at ge + 7 (a header follows at once: the next header of the block, or the
+// next block's first when the data ends exactly at this full block's end). kRecUsual: kRecAdj, the fragment began in an
+// earlier chunk and pb <= 1016 (its J and the next fragment's start lie in chunk ce) -- chunk ce then needs one
+// gap mask and one close, provided the next fragment's data runs past it (k_crc checks that on the next record).
+// Bits 22-28: Lfull, the lanes [0, Lfull) whose 16 B piece of chunk ce holds only the fragment's bytes (and J); bits
+// 29-31: K, the fragment's J ends in word K of lane Lfull's piece (0 or 4: no lane is split), as stream_verify's
+// close derives them from pb.
+constexpr uint32_t kRecUsual = 1u << 20, kRecAdj = 1u << 21;
+__device__ __forceinline__ void put_frag_ic(Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t g,
+                                            uint64_t frag_cap, uint32_t b, uint64_t boff, uint32_t start_len,
+                                            uint32_t crc, uint32_t type, uint32_t ic, bool adj) {
   if (g >= frag_cap) return;
-  *reinterpret_cast<uint4*>(frags + g) = make_uint4(b, start_len, ~rotl32(crc - 0xa282ead8u, 15) ^ ic, type & 0xffu);
+  const uint32_t J = ~rotl32(crc - 0xa282ead8u, 15) ^ ic;
+  *reinterpret_cast<uint4*>(frags + g) = make_uint4(b, start_len, J, type & 0xffu);
+  const uint64_t gs = boff + (start_len & 0xffffu), ge = gs + (start_len >> 16);
+  const uint32_t cb = (uint32_t)(gs / kSChunk), ce = (uint32_t)(ge / kSChunk);
+  const uint32_t pa = (uint32_t)(gs % kSChunk), pb = (uint32_t)(ge % kSChunk);
+  const bool usual = adj && cb < ce && pb <= (uint32_t)kSChunk - 8u;
+  const uint32_t e = pb + 4u, K = ((e % kSPiece) + 3u) >> 2, Lfull = e / kSPiece + (K == (uint32_t)kSPW ? 1u : 0u);
+  srec[g] = make_uint4(ce, cb, J, pb | pa << 10 | (usual ? kRecUsual : 0u) | (adj ? kRecAdj : 0u) | Lfull << 22 |
+                                      (K & 3u) << 29);
 }
-__device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint64_t g, uint64_t frag_cap, uint32_t b,
-                                         uint32_t start, uint32_t len, uint32_t crc, uint32_t type,
-                                         const uint32_t* __restrict__ initc) {
-  put_frag_ic(frags, g, frag_cap, b, start | (len << 16), crc, type, initc[len]);
+__device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t g,
+                                         uint64_t frag_cap, uint32_t b, uint64_t boff, uint32_t start, uint32_t len,
+                                         uint32_t crc, uint32_t type, const uint32_t* __restrict__ initc, bool adj) {
+  put_frag_ic(frags, srec, g, frag_cap, b, boff, start | (len << 16), crc, type, initc[len], adj);
 }
 
 // Block summary for the record state machine (wal_iterator.go:69-96), written by k_chase from the headers alone:
@@ -192,7 +211,8 @@ template <int ABL = 0>
 __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
                                               uint64_t nblocks, uint32_t* __restrict__ fbase,
                                               uint32_t* __restrict__ rbase, uint2* __restrict__ bsum,
-                                              Frag* __restrict__ frags, uint64_t frag_cap, uint64_t* __restrict__ lb,
+                                              Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t frag_cap,
+                                              uint64_t* __restrict__ lb,
                                               uint64_t* __restrict__ lbe, uint64_t* __restrict__ misc,
                                               uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc,
                                               uint32_t direct_max, uint32_t* __restrict__ equeue,
@@ -339,7 +359,11 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     if (badk != 0xffffffffu)  // the first unknown-type fragment of the segment (reset by the previous finalize)
       atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_TYPE]), (unsigned long long)(g0 + badk));
     // the held headers' entries, kWb at a time: their initc[len] loads are issued together (one at a time, each
-    // entry waited one L2 round trip for its load: config C k_chase's table writes took ~17 us of its ~70)
+    // entry waited one L2 round trip for its load: config C k_chase's table writes took ~17 us of its ~70). The
+    // block's last fragment is adjacent to the next block's first when it ends exactly at this full block's end and
+    // the next block holds a header.
+    const bool next_hdr = b + 1 < nblocks && seg_len - (boff + kBlock) >= kHdr;
+    auto adj = [&](uint32_t k, uint32_t sl_k) { return k + 1u < n || (next_hdr && (sl_k & 0xffffu) + (sl_k >> 16) == kBlock); };
     const uint32_t nh = n < (uint32_t)kHold ? n : (uint32_t)kHold;
     constexpr uint32_t kWb = 16;
     static_assert(kHold % kWb == 0, "held-header batches stay inside s_hold");
@@ -353,12 +377,13 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
 #pragma unroll
       for (uint32_t q = 0; q < kWb; ++q)
         if (k0 + q < nh)
-          put_frag_ic(frags, g0 + k0 + q, frag_cap, (uint32_t)b, sl[q], s_hold[k0 + q][0][lane], s_type[k0 + q][lane],
-                      ic[q]);
+          put_frag_ic(frags, srec, g0 + k0 + q, frag_cap, (uint32_t)b, boff, sl[q], s_hold[k0 + q][0][lane],
+                      s_type[k0 + q][lane], ic[q], adj(k0 + q, sl[q]));
     }
     if (n > (uint32_t)kHold)  // the tail of a block with more headers than held, chased again from the first of them
       chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
-        put_frag(frags, g0 + k, frag_cap, (uint32_t)b, start, len, crc, type, initc);
+        put_frag(frags, srec, g0 + k, frag_cap, (uint32_t)b, boff, start, len, crc, type, initc,
+                 adj(k, start | (len << 16)));
       }, hres, (uint32_t)kHold);
   }
   if (ABL & 16) {
@@ -387,12 +412,21 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   if (wg == 0 && lane < 8u) equeue[lane * kEqStride] = 0;  // k_crc's emission queues
 }
 
-// F_l(x): lane-replicated nibble images, lane l reads its own copy (bank = l % 32)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// F_l(x): lane-replicated nibble images, lane l reads its own copy (bank = l % 32). Byte offsets: nibble image i of
+// value v at i * 4096 + v * 256 + 4 l, so each address is one shift and one v_and_or_b32 (the lane's 4 l never
+// overlaps the 0xf00 field) and the image offset i * 4096 is the ds_read immediate (the operators lie first in LDS).
 __device__ __forceinline__ uint32_t apply_fwd(const uint32_t* __restrict__ fwd, uint32_t lane, uint32_t x) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r ^= fwd[((i * 16 + ((x >> (4 * i)) & 15u)) << 6) | lane];
-  return r;
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(fwd);
+  const uint32_t lane4 = 4u * lane;
+  auto at = [&](int i) -> uint32_t {
+    const uint32_t sh = 4 * i >= 8 ? (x >> (4 * i - 8)) : (x << (8 - 4 * i));
+    return *reinterpret_cast<const uint32_t*>(b + (((sh & 0xf00u) | lane4) + 4096u * (uint32_t)i));
+  };
+  const uint32_t r0 = at(0), r1 = at(1), r2 = at(2), r3 = at(3), r4 = at(4), r5 = at(5), r6 = at(6), r7 = at(7);
+  return xor3(xor3(r0, r1, r2), xor3(r3, r4, r5), r6) ^ r7;
 }
 // uniform operator (one 8x16 nibble table shared by all lanes: 16 distinct banks per lookup)
 __device__ __forceinline__ uint32_t apply_op(const uint32_t* __restrict__ c, uint32_t x) {
@@ -839,9 +873,6 @@ __device__ __forceinline__ SliceLane2 slice_lane2(uint32_t lane) {
   }
   return s;
 }
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
 // A_32(x) (or, SH, A_{8*1012}(x)) ^ next
 template <bool SH>
 __device__ __forceinline__ uint32_t slice4_step2(const uint8_t* __restrict__ tb, const SliceLane2& sl, uint32_t x,
@@ -913,133 +944,151 @@ __device__ __forceinline__ uint32_t apply_op_b(const uint32_t* __restrict__ t, u
   return xor3(a0, a1, a2) ^ a3;
 }
 
-// Verify fragments [f0, f0 + nfr) of the fragment table (one wave). lds: the kS2Image tables; frd: the fragment
-// table again, read-only: the descriptors are wave-uniform, read by scalar loads (s_load, counted in lgkmcnt), one
-// fragment ahead. The verdicts collect in a 64-bit mask and reach the dense verdict array (fok) every 64 fragments.
+// Verify fragments [f0, f0 + nfr) (one wave) from their stream records (k_chase, kRecUsual), read with scalar loads
+// (s_load, counted in lgkmcnt) one fragment ahead. lds: the kS2Image tables. The verdicts collect in a 64-bit mask
+// and reach the dense verdict array (fok) every 64 fragments.
 //
-// Positions are 32-bit and relative to the wave's first chunk (pos = (blk - blk0) * 32768 + start + adj: a wave's
-// blocks span far fewer than 2^16 blocks). The loop carries little uniform state -- the current and the next fragment
-// (gs, ge, J), the raw descriptor after them, the fragment index, the verdict mask and `ev`, the next chunk that needs
-// more than the fast chain -- so that the unrolled ring keeps it in SGPRs without spills: a chunk c != ev lies inside
-// the open fragment's data (one compare, then the chain), and only chunk ev runs the fragment-end loop. (Round 4's
-// loop kept per-fragment fast-range bounds, a stale-table clamp on every position and ablation switches; it spilled 57
-// SGPRs and its fragment end cost ~160 VALU + ~150 SALU instructions, SQ counters in profiles/r05_clock.)
+// Positions are 32-bit and relative to the wave's first chunk. The loop carries little uniform state -- the current
+// fragment's record, the next one's (raw: its load is first waited for at the next fragment end, so the fast chunks
+// in between hide its latency), the fragment index, the verdict mask and `ev`, the next chunk that needs more than the
+// fast chain -- so that the unrolled ring keeps it in SGPRs without spills: a chunk c != ev lies inside the open
+// fragment's data (one compare, then the chain). At chunk ev the usual end (kRecUsual, and the next fragment's data
+// runs past the chunk) is one gap mask and one close straight from the records; anything else runs the general loop
+// over the fragments touching the chunk. (Round 4's loop derived every position from the fragment table per end,
+// kept per-fragment fast-range bounds and stale-table clamps: it spilled 57 SGPRs and its fragment end cost ~160 VALU
+// + ~150 SALU instructions, SQ counters in profiles/r05_clock.)
 // FASTONLY (tools/kbench only): every chunk takes the fast chain (verdicts meaningless).
 template <bool FASTONLY = false>
-__device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
-                                              uint8_t* __restrict__ fok, const uint4* __restrict__ frd, uint64_t f0,
+__device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, uint64_t seg_len,
+                                              uint8_t* __restrict__ fok, const uint4* __restrict__ srec, uint64_t f0,
                                               uint32_t nfr, const uint32_t* __restrict__ lds, uint32_t lane,
                                               uint64_t* __restrict__ misc, uint32_t* __restrict__ s_rem,
                                               uint32_t wslot, const uint8_t* __restrict__ dummy) {
   constexpr int D = 8;  // chunks in flight per wave (kbench, round 4: 12 within noise of 8, 4 and 6 slower)
   if (nfr == 0) return;
-  const uint8_t* tb = reinterpret_cast<const uint8_t*>(lds);
-  const uint32_t* s_lop = lds + kS2Slice;
-  const uint32_t* s_kop = s_lop + kS2Lop;
+  const uint8_t* tb = reinterpret_cast<const uint8_t*>(lds + kS2SliceOff);
+  const uint32_t* s_lop = lds + kS2LopOff;
+  const uint32_t* s_kop = lds + kS2KopOff;
   const SliceLane2 sl = slice_lane2(lane);
-  const uint4* fd = frd + f0;
-  const uint4 v0 = fd[0], v1 = fd[nfr - 1u];
-  // the wave's chunks: [c_first, c_first + nch), absolute chunk indices
-  const uint64_t c_first = ((uint64_t)start_off + (uint64_t)v0.x * kBlock + (v0.y & 0xffffu)) / kSChunk;
-  const uint64_t ge_last = (uint64_t)start_off + (uint64_t)v1.x * kBlock + (v1.y & 0xffffu) + (v1.y >> 16);
-  uint64_t c_end = (ge_last + 4u + kSChunk - 1u) / kSChunk;
+  const uint4* rd = srec + f0;
+  const uint4 r0 = rd[0], r1 = rd[nfr - 1u];
+  // the wave's chunks: [cf, cf + nch), absolute chunk indices (the first fragment begins in chunk cf; the last one's J
+  // ends in the last)
+  const uint32_t cf = r0.y;
+  uint64_t c_end = ((uint64_t)r1.x * kSChunk + (r1.w & 1023u) + 4u + kSChunk - 1u) / kSChunk;
   if (c_end > c_safe_bound(seg_len)) c_end = c_safe_bound(seg_len);  // (a table bug: reported below, never silent)
-  if (v1.x - v0.x >= (1u << 16) || c_end < c_first) c_end = c_first;  // (ditto: no real wave spans that far)
-  const uint32_t nch = (uint32_t)(c_end - c_first);
-  const uint32_t blk0 = v0.x;
-  const int32_t adj = (int32_t)((int64_t)start_off + (int64_t)blk0 * kBlock - (int64_t)(c_first * kSChunk));
+  if (c_end < cf || c_end - cf > (1u << 20)) c_end = cf;               // (ditto: no real wave spans 1 GiB)
+  const uint32_t nch = (uint32_t)(c_end - cf);
   struct G32 { int32_t gs, ge; uint32_t J; };  // wave-relative data range, check word
   constexpr int32_t kFar = 0x40000000;
-  auto geo = [&](uint4 v) -> G32 {
-    const int32_t gs = (int32_t)((v.x - blk0) << 15) + (int32_t)(v.y & 0xffffu) + adj;
-    return G32{gs, gs + (int32_t)(v.y >> 16), v.z};
+  auto geo = [&](uint4 r) -> G32 {
+    return G32{(int32_t)(((r.y - cf) << 10) + ((r.w >> 10) & 1023u)), (int32_t)(((r.x - cf) << 10) + (r.w & 1023u)),
+               r.z};
   };
-  uint32_t i = 0;  // the current fragment (wave-relative)
-  G32 fc = geo(v0);
-  // fragment i + 1's raw descriptor: its scalar load is issued when fragment i becomes current and first used at the
-  // next chunk ev, so the fast chunks in between hide its latency (a decoded copy carried instead made the compiler
-  // wait for the load at once)
-  uint4 dn = fd[nfr > 1u ? 1u : 0u];
-  uint32_t ev = 0;  // the next chunk that is not inside the open fragment's data (fc begins in chunk 0)
+  uint32_t i = 0;   // the current fragment (wave-relative)
+  uint4 rc = r0;    // its record
+  uint4 rn = rd[1];  // the next fragment's (4 entries of slack after the last: an unconditional load)
+  uint32_t ev = 0;  // the next chunk that is not inside the open fragment's data (fragment 0 begins in chunk 0)
   uint32_t H = 0;
   uint64_t okm = 0;            // verdicts of fragments (i & ~63) + j, bit j
-  uint32_t bad = 0xffffffffu;  // first failing fragment (wave-relative)
+  uint32_t bad = 0xffffffffu;  // first failing fragment (wave-relative), found at the flushes
   auto flush = [&](uint32_t from, uint32_t n) {  // verdicts of fragments [from, from + n) (n <= 64)
     if (lane < n) fok[f0 + from + lane] = (uint8_t)((okm >> lane) & 1u);
+    const uint64_t fail = ~okm & (n == 64u ? ~0ull : (1ull << n) - 1ull);
+    if (fail != 0ull && bad == 0xffffffffu) bad = from + (uint32_t)__builtin_ctzll(fail);
   };
   // the closing fragment's zero test over the masked chunk words x (its data and J end at pb + 4, chunk-relative),
-  // then the next fragment's state, then the next fragment
-  auto close = [&](const uint32_t (&x)[kSPW], int32_t pb) {
-    const uint32_t e = (uint32_t)(pb + 4);  // the closing fragment's bytes end here (1 <= e <= kSChunk)
-    // lanes < Lf: all theirs; lane Lf: split at word K (K == kSPW: all its piece; K == 0: none of it)
-    const uint32_t Lf = e / kSPiece, K = ((e % kSPiece) + 3u) >> 2;
+  // its verdict, the next fragment's chain state; then the next fragment becomes current
+  // (the closing fragment's bytes end at e = pb + 4, 1 <= e <= kSChunk: lanes < Lfull hold only its bytes; lane Lfull
+  // is split at word K = 1..3 of its piece when K3 = K & 3 != 0, else no lane is)
+  auto close = [&](const uint32_t (&x)[kSPW], uint32_t Lfull, uint32_t K3) {
     uint32_t cap = 0;
-    const uint32_t s8 = chain_piece2<true>(tb, sl, H, x, K, &cap);
-    const uint32_t Lfull = K == (uint32_t)kSPW ? Lf + 1u : Lf;
-    const uint32_t Lsplit = (K != 0u && K != (uint32_t)kSPW) ? Lf : 64u;
+    const uint32_t s8 = chain_piece2<true>(tb, sl, H, x, K3, &cap);
+    const uint32_t Lsplit = K3 != 0u ? Lfull : 64u;
+    const uint32_t K = K3;
     const bool full = lane < Lfull, split = lane == Lsplit;
     // split lane: its captured state shifted by A_{8(4(4-K)+1008)}; lanes after it: the carried H shifted by
     // A_{8*1024} (table 0); then each lane's share G_l(A_l) = A_{8*16*(63-l)}(A_l), XOR-reduced over the wave
     const uint32_t A = full ? s8 : apply_op_b(s_kop + (split ? K : 0u) * 1024u, split ? cap : H);
     const uint32_t T = wave_scan_z(apply_fwd(s_lop, lane, A), [](uint32_t a, uint32_t b) { return a ^ b; });
-    const uint32_t ok = __builtin_amdgcn_readlane(T, 63) == 0u ? 1u : 0u;
-    okm |= (uint64_t)ok << (i & 63u);
-    if (!ok && bad == 0xffffffffu) bad = i;
+    if (__builtin_amdgcn_readlane(T, 63) == 0u) okm |= 1ull << (i & 63u);
     H = s8 ^ A;
     ++i;
     if ((i & 63u) == 0u) {
       flush(i - 64u, 64u);
       okm = 0;
     }
+    rc = rn;
+    rn = rd[i + 1u];  // (indexed from the wave's base: a pointer carried through the loop became a vector load)
+  };
+  auto close_pb = [&](const uint32_t (&x)[kSPW], int32_t pb) {
+    const uint32_t e = (uint32_t)(pb + 4), K = ((e % kSPiece) + 3u) >> 2;
+    close(x, e / kSPiece + (K == (uint32_t)kSPW ? 1u : 0u), K & 3u);
   };
   // chunk c == ev: the fragment ends (and beginnings) inside it, one close per end; then the next `ev`
   auto slow = [&](uint32_t c, const uint32_t (&w)[kSPW]) {
     const int32_t C0 = (int32_t)(c * kSChunk), C1 = C0 + kSChunk;
-    auto rel = [&](int32_t p) -> int32_t { return min(max(p - C0, -64), 4096); };
-    G32 fn = i + 1u < nfr ? geo(dn) : G32{kFar, kFar, 0u};
-    for (;;) {
-      if (fc.gs >= C1) break;  // not begun here (also once every fragment is done: fc.gs = kFar)
-      const bool closes = fc.ge + 4 <= C1;
-      // the next fragment shares the chain when its data runs to the chunk's end (bytes [gs, C1) all data, no J)
-      const bool next_in = closes && fn.gs < C1 && fn.ge >= C1;
+    uint32_t nev;
+    // (evaluated without short-circuits: a value computed on one path only became an SGPR phi whose undefined side the
+    // compiler filled with a readfirstlane of a ring register, waiting for that chunk's load)
+    // (ev is also the chunk a fragment begins in when it was not open: the wave's first one, or one after a header
+    // straddling two chunks)
+    const bool usual = ((rc.w & kRecUsual) != 0u) & (rc.x - cf == c) & (rn.x - cf > c) & (i + 1u < nfr);
+    if (usual) {
       uint32_t x[kSPW];
-      const int32_t pa = rel(fc.gs), pb = rel(fc.ge);
-      if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr)  // the usual end: a header between two data runs
-        mask_gap(x, w, pb, fc.J, lane, lds);
-      else
-        mask_chunk(x, w, pa, pb, next_in ? rel(fn.gs) : 4096, fc.J, lane, lds);
-      if (!closes) {  // the data (or J) runs on into the next chunk
-        H = chain_piece2<false>(tb, sl, H, x);
-        break;
+      mask_gap(x, w, (int32_t)(rc.w & 1023u), rc.z, lane, lds);
+      close(x, (rc.w >> 22) & 127u, rc.w >> 29);
+      nev = rc.x - cf;  // the next fragment (now current, open) ends in a later chunk
+    } else {
+      auto rel = [&](int32_t p) -> int32_t { return min(max(p - C0, -64), 4096); };
+      G32 fc = i < nfr ? geo(rc) : G32{kFar, kFar, 0u};
+      for (;;) {
+        if (fc.gs >= C1) break;  // not begun here (also once every fragment is done: fc.gs = kFar)
+        const G32 fn = i + 1u < nfr ? geo(rn) : G32{kFar, kFar, 0u};
+        const bool closes = fc.ge + 4 <= C1;
+        // the next fragment shares the chain when its data runs to the chunk's end (bytes [gs, C1) all data, no J)
+        const bool next_in = closes && fn.gs < C1 && fn.ge >= C1;
+        uint32_t x[kSPW];
+        const int32_t pa = rel(fc.gs), pb = rel(fc.ge);
+        if (next_in && pa <= 0 && fn.gs - fc.ge == (int32_t)kHdr)  // a header between two data runs
+          mask_gap(x, w, pb, fc.J, lane, lds);
+        else
+          mask_chunk(x, w, pa, pb, next_in ? rel(fn.gs) : 4096, fc.J, lane, lds);
+        if (!closes) {  // the data (or J) runs on into the next chunk
+          H = chain_piece2<false>(tb, sl, H, x);
+          break;
+        }
+        close_pb(x, pb);
+        fc = fn;
+        if (next_in) break;
       }
-      close(x, pb);
-      fc = fn;
-      dn = fd[i + 1u < nfr ? i + 1u : 0u];
-      if (next_in) break;
-      fn = i + 1u < nfr ? geo(dn) : G32{kFar, kFar, 0u};
+      // open: fc's bytes so far are in H; its data ends in chunk fc.ge / kSChunk (its J may straddle into the next)
+      nev = fc.gs < C1 ? max((uint32_t)fc.ge / (uint32_t)kSChunk, c + 1u) : c + 1u;
     }
-    // open: fc's bytes so far are in H; its data ends in chunk fc.ge / kSChunk (its J may straddle into the next)
-    const uint32_t nx = c + 1u;
-    ev = fc.gs < C1 ? max((uint32_t)fc.ge / (uint32_t)kSChunk, nx) : nx;
+    ev = nev;
   };
   auto step = [&](uint32_t c, const uint32_t (&w)[kSPW]) {
     if (FASTONLY || c != ev) H = chain_piece2<false>(tb, sl, H, w);
     else slow(c, w);
   };
   const uint64_t c_safe = seg_len / kSChunk;  // chunks [0, c_safe) lie inside the segment
-  const uint32_t nl = c_safe > c_first ? (uint32_t)min(c_safe - c_first, (uint64_t)nch) : 0u;  // pipelined chunks
+  const uint32_t nl = c_safe > cf ? (uint32_t)min(c_safe - cf, (uint64_t)nch) : 0u;  // pipelined chunks
   if (nl > 0u) {
-    const uint8_t* wseg = seg + c_first * kSChunk;
+    const uint8_t* wseg = seg + (uint64_t)cf * kSChunk;
     const uint32_t lane16 = lane * kSPiece;
-    uint32_t buf[D][kSPW];
+    // The ring of D chunk loads is issued and waited for by hand: the compiler's in-order vmcnt accounting, at every
+    // fragment end, either drained the whole ring or waited for the newest chunk (an undefined SGPR phi filled by a
+    // readfirstlane of a ring register). Each slot waits with vmcnt(D - 1): the D - 1 later chunks' loads (a verdict
+    // store in between only makes that wait longer, never short). Every ring register stays live until the final
+    // vmcnt(0), so none is reused while a load into it is in flight.
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u buf[D];
     // unconditional (no branch around a load); the loads issued past the last chunk read 1 KiB of the table image
-    // instead, which every workgroup has just read (an L2 hit)
-    auto issue = [&](uint32_t c, uint32_t (&w)[kSPW]) {
+    // instead, which every workgroup has just read (an L2 hit). Non-temporal: the segment is read once (kbench spat:
+    // 185 -> 160 us for the whole segment).
+    auto issue = [&](uint32_t c, v4u& w) {
       const uint8_t* p = c < nl ? wseg + (size_t)c * kSChunk : dummy;  // uniform: the lane offset is the VGPR part
-      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-      // non-temporal: the segment is read once (kbench spat: 185 -> 160 us for the whole segment)
-      const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p + lane16));
-      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+      asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=v"(w) : "v"(lane16), "s"(p) : "memory");
     };
 #pragma unroll
     for (int k = 0; k < D; ++k) issue((uint32_t)k, buf[k]);
@@ -1055,16 +1104,22 @@ __device__ __forceinline__ void stream_verify(const uint8_t* __restrict__ seg, u
       else __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int k = 0; k < D; ++k) {
-        // chunk c + k, then its registers take chunk c + k + D (no copy: a copy would make the loop carry two sets
-        // and wait for every load at the back-edge)
-        if (c + k < nl) step(c + k, buf[k]);
+        // chunk c + k, then its register takes chunk c + k + D
+        if (c + k < nl) {
+          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(buf[k]) : "n"(D - 1));
+          const uint32_t w[kSPW] = {buf[k].x, buf[k].y, buf[k].z, buf[k].w};
+          step(c + k, w);
+        }
         issue(c + k + D, buf[k]);
       }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(buf[0]), "v"(buf[1]), "v"(buf[2]), "v"(buf[3]), "v"(buf[4]), "v"(buf[5]),
+                 "v"(buf[6]), "v"(buf[7]));
+    static_assert(D == 8, "the final wait names every ring register");
   }
   for (uint32_t c = nl; c < nch; ++c) {  // chunks touching the segment's end
     uint32_t w[kSPW];
-    const uint4 A = load16_safe(seg, seg_len, (int64_t)((c_first + c) * kSChunk) + lane * kSPiece);
+    const uint4 A = load16_safe(seg, seg_len, (int64_t)(((uint64_t)cf + c) * kSChunk) + lane * kSPiece);
     w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
     step(c, w);
   }
@@ -1098,7 +1153,7 @@ template <int ABL = 0>
 __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                      uint32_t start_off, uint64_t nblocks,
                                                      const uint32_t* __restrict__ fbase, uint8_t* __restrict__ fok,
-                                                     const uint4* __restrict__ frags_ro,
+                                                     const uint4* __restrict__ srec,
                                                      uint64_t frag_cap, Tables tabs, EmitArgs ea,
                                                      uint32_t tail_panic, uint64_t gen,
                                                      bcw_decode_result* __restrict__ res,
@@ -1213,7 +1268,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     n_items += taken;
   };
   if (!(ABL & 32768))
-    stream_verify<(ABL & 8388608) != 0>(seg, seg_len, start_off, fok, frags_ro, f0, nfr, lds, lane, misc, s_rem,
+    stream_verify<(ABL & 8388608) != 0>(seg, seg_len, fok, srec, f0, nfr, lds, lane, misc, s_rem,
                                         (wave & 3u) * 4u + (wave >> 2),
                                         reinterpret_cast<const uint8_t*>(tabs.lds_image2));
   __builtin_amdgcn_s_setprio(0);
@@ -1283,7 +1338,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
   pr.begin(K_CHASE, stream, ev);
   k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
-                                        s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch, tabs.initc, s.chase_direct,
+                                        s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch, tabs.initc, s.chase_direct,
                                         s.equeue, s.test_abort_wg);
   s.test_abort_wg = 0;
   pr.end(K_CHASE, stream, ev);
@@ -1295,7 +1350,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   }
   pr.begin(K_CRC, stream, ev);
   k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.fok,
-                                                         reinterpret_cast<const uint4*>(s.frags), s.frag_cap, tabs, ea,
+                                                         s.srec, s.frag_cap, tabs, ea,
                                                          tail_panic, gen, d_result, s.misc, 0ull, nblocks,
                                                          (uint32_t)num_cus);
   pr.end(K_CRC, stream, ev);

@@ -31,12 +31,7 @@ constexpr int kPow2Ops = 16;
 
 // Device-side constant tables, built on the host once per context.
 struct Tables {
-  uint32_t* slice;   // [2][256] slice-by-2 CRC-32C tables (T0 = byte table, T1)
-  uint32_t* fwd;     // [64][8][16] lane shift operators F_l = A_{8*128*(63-l)} (nibble images)
-  uint32_t* carry;   // [8][16] A_{8*8192} (nibble images)
-  uint32_t* half;    // [8][16] A_{8*64} (nibble images)
   uint32_t* initc;   // [kBlock+1] A_{8L}(0xFFFFFFFF)
-  uint32_t* lds_image;  // k_crc's LDS table image, laid out exactly as in LDS (see kLdsImage)
   uint32_t* lds_image2; // the stream verify's LDS image (kS2Image)
   uint32_t* enc_ops;    // [kEncOpsWords] encode shift operators (nibble images, see build_enc_ops)
   uint32_t* pow2;       // [kPow2Ops][8][16] A_{8 * 2^k} (nibble images), k < 16: shifts by any distance < 64 KiB
@@ -46,22 +41,18 @@ struct Tables {
 constexpr int kOpInv = 40, kOpPow2 = 56, kOpPow2Inv = 88;
 constexpr int kEncOpsWords = 103 * 128;
 
-// k_crc LDS table image (dwords): slice-by-2 tables as 256-B rows {T1[e] x32, T0[e] x32} (lane l
-// reads bank l % 32), lane operators transposed to [8][16][64 lanes], then the carry and half operators.
-constexpr int kLdsSlice = 256 * 64;  // slice-by-4 rows (crc_window)
-constexpr int kLdsFwd = 8 * 16 * 64;
-constexpr int kLdsOps = 2 * 8 * 16;
-constexpr int kLdsImage = kLdsSlice + kLdsFwd + kLdsOps;
 // k_crc stream verify (bcw_decode.hip, stream_verify): absolute 1 KiB chunks, 16 B per lane (one fully contiguous
-// load per chunk). LDS image (dwords): slice-by-4 rows of 256 B {T3, T2, T1, T0} x 8 copies then the shifted tables
-// T'_k (a byte followed by k + 1008 zero bytes) x 8 copies; the lane operators G_l = A_{8*16*(63-l)} transposed to
-// [8][16][64 lanes]; the split operators A_{8*(4*(4-k) + 1008)} (k = 0..3) as byte tables [k][byte t][256]; and the
-// per-lane byte-select tables of the fragment-end masks (16 B entries, one per lane offset): GE (bytes >= n), JSEL
-// (the check word's bytes at piece offset m - 3), GAP (check word at piece offset g - 6, then 3 zero bytes).
+// load per chunk). LDS image (dwords): the lane operators G_l = A_{8*16*(63-l)} transposed to [8][16][64 lanes]
+// (first: byte offsets i * 4096 + v * 256 + 4 l, each table base a ds_read immediate); slice-by-4 rows of 256 B
+// {T3, T2, T1, T0} x 8 copies then the shifted tables T'_k (a byte followed by k + 1008 zero bytes) x 8 copies; the
+// split operators A_{8*(4*(4-k) + 1008)} (k = 0..3) as byte tables [k][byte t][256]; and the per-lane byte-select
+// tables of the fragment-end masks (16 B entries, one per lane offset): GE (bytes >= n), JSEL (the check word's bytes
+// at piece offset m - 3), GAP (check word at piece offset g - 6, then 3 zero bytes).
 constexpr int kSPiece = 16;
 constexpr int kSChunk = 64 * kSPiece;
 constexpr int kSPW = kSPiece / 4;  // words per lane
 constexpr int kS2Slice = 256 * 64, kS2Lop = 8 * 16 * 64, kS2Kop = kSPW * 4 * 256;
+constexpr int kS2LopOff = 0, kS2SliceOff = kS2Lop, kS2KopOff = kS2Lop + kS2Slice;
 constexpr int kS2GeN = 17, kS2JselN = 20, kS2GapN = 23;  // entries (4 dwords each)
 constexpr int kS2Ge = kS2Slice + kS2Lop + kS2Kop, kS2Jsel = kS2Ge + 4 * kS2GeN, kS2Gap = kS2Jsel + 4 * kS2JselN;
 constexpr int kS2Image = kS2Gap + 4 * kS2GapN + 4;  // (+ pad to 16 B)
@@ -83,6 +74,7 @@ struct Scratch {
   uint64_t tickets = 0;        // k_chase tickets issued so far (misc[M_TICKET] mirrors it)
   uint64_t epoch = 1;          // look-back epoch of the next launch
   Frag* frags = nullptr;       // [frag_cap]
+  uint4* srec = nullptr;       // [frag_cap + 4] stream record per fragment (k_chase -> k_crc, bcw_decode.hip kRecUsual)
   uint8_t* fok = nullptr;      // [frag_cap] CRC verdict per fragment (k_crc; dense: 64 verdicts are one 64 B store)
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
   uint32_t* equeue = nullptr;  // [8 x 32] k_crc emission work-queue heads, one 128 B line per XCD
@@ -197,8 +189,6 @@ struct DeviceGuard {
 bcw_ctx* index_ctx(const bcw_index* ix);
 
 // Host-side table builders (bcw_api.cpp).
-void build_slice_tables(uint32_t* t2x256);
-void build_lane_tables(uint32_t* fwd64x8x16, uint32_t* carry8x16, uint32_t* half8x16);
 void build_initc(uint32_t* initc);
 
 }  // namespace bcw

@@ -261,11 +261,11 @@ int main(int argc, char** argv) {
     if (kb_clock && !a.kb_stamps) a.kb_stamps = seq_stamps ? seq_stamps : clk_st;
     if (run_reps == 0) {
       hipMemsetAsync(s.equeue, 0, 1024, st);
-      kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, (const uint4*)s.frags, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid);
+      kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid);
       return 0.0f;
     }
     const float ms = timeit([&] { hipMemsetAsync(s.equeue, 0, 1024, st);  // the emission queues (k_chase resets them)
-                        kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, (const uint4*)s.frags, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid); },
+                        kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid); },
                   reps, st);
     if (kb_clock && a.kb_stamps == clk_st) last_mhz = clock_of(clk_st, grid * kCrcWaves);
     return ms;
@@ -425,7 +425,7 @@ int main(int argc, char** argv) {
   const float as = timeit([&] {
     hipMemsetAsync(&s.misc[M_DONE_CRC], 0, 8, st);  // the last workgroup finalizes
     hipMemsetAsync(s.equeue, 0, 1024, st);
-    k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, (const uint4*)s.frags, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
+    k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
                                           s.misc, 0ull, nblocks, (uint32_t)cus);
   }, reps, st);
   printf("k_crc + finalize %.4f ms\n", as);
@@ -440,7 +440,7 @@ int main(int argc, char** argv) {
     auto crun = [&](auto kern) {
       return timeit([&] {
         kern<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
-                                                              s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch,
+                                                              s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch,
                                                               ctx->tabs.initc, s.chase_direct, s.equeue, 0ull);
         s.tickets += (nblocks + 63) / 64;
         ++s.epoch;
