@@ -37,16 +37,17 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    # untimed steps right before the timed ones: after an idle period the first ~30 back-to-back decodes run through a
-    # clock transient of the chip (k_crc 210 -> 290 -> 210 us, rocprofv3 kernel trace); the timed
-    # steps measure the steady state after it
-    ap.add_argument("--warmup", type=int, default=40)
+    # untimed steps right before the timed ones (the driver's own value). After an idle period the chip lowers its
+    # shader clock under this load over the first ~10-60 back-to-back decodes (in-kernel clock 2.1 -> 1.3-1.5 GHz and
+    # back, profiles/r05_clock): with 5 warmup steps the timed ones sit in that dip, as a one-file
+    # compaction scan does
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seg-bytes", type=int, default=1 << 30)
     ap.add_argument("--config", default="B", choices=["B", "C"], help="B: 4 KiB values; C: Zipf 128 B-64 KiB")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the extra legs (all-core / pread CPU baselines, file-to-file end-to-end rates)")
+                    help="skip the extra legs (config C, all-core / pread CPU baselines, file-to-file end-to-end rates)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the all-core CPU baseline")
     ap.add_argument("--inflight", type=int, default=2,
                     help="segments in flight for the extra pipelined leg: steps rotate over this many contexts "
@@ -226,6 +227,62 @@ def end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec, 
     return res
 
 
+def config_c_leg(L, Context, torch, dev, args, make_table, roof_name, kernel_names):
+    """BASELINE.json configs[2] (C): a 1 GiB segment of Zipf(1.1) 128 B-64 KiB values, decoded exactly like the
+    headline (W untimed steps, then K timed, HIP events around every --event-every-th k_crc); an extra key, never
+    `value`"""
+    n, r = C.c_uint64(), C.c_uint64()
+    assert L.lib.bcw_synth_segment(args.seg_bytes, 0, 42, 20, 100, 4096, 1, BASE_TIME, None, 0, C.byref(n),
+                                   C.byref(r)) == 0
+    host = torch.empty(n.value, dtype=torch.uint8).pin_memory()
+    assert L.lib.bcw_synth_segment(args.seg_bytes, 0, 42, 20, 100, 4096, 1, BASE_TIME, C.c_void_p(host.data_ptr()),
+                                   n.value, C.byref(n), C.byref(r)) == 0
+    seg_len, n_rec = int(n.value), int(r.value)
+    d_seg = host.to(dev)
+    del host
+    table, cols = make_table(n_rec + 64)
+    d_res = torch.zeros(C.sizeof(L.DecodeResult), dtype=torch.uint8, device=dev)
+    params = L.DecodeParams(seg_len, BASE_TIME, 40, 20, 20, L.MODE_RECORD)
+    ctx = Context(torch.cuda.current_device())
+    stream = torch.cuda.Stream()
+    ctx.set_stream(stream.cuda_stream)
+
+    def step():
+        assert L.lib.bcw_decode_segment_async(ctx.handle, C.c_void_p(d_seg.data_ptr()), C.byref(params),
+                                              C.byref(table), C.c_void_p(d_res.data_ptr())) == 0
+    step()
+    torch.cuda.synchronize()
+    res = L.DecodeResult.from_buffer_copy(bytes(d_res.cpu().numpy()))
+    assert res.err_class == 0 and res.n_records == n_rec and res.first_bad_record == -1, "config C decode check"
+    n_frags = int(res.n_frags)
+    roof_k = kernel_names.index(roof_name)
+    for _ in range(args.warmup):
+        step()
+    L.lib.bcw_ctx_set_profiling(ctx.handle, 1 << roof_k)
+    L.lib.bcw_ctx_set_profiling_sample(ctx.handle, args.event_every)
+    nk = len(kernel_names)
+    L.lib.bcw_ctx_kernel_times(ctx.handle, None, None, nk)  # reset
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    tot = (C.c_double * nk)()
+    cnt = (C.c_uint64 * nk)()
+    L.lib.bcw_ctx_kernel_times(ctx.handle, tot, cnt, nk)
+    L.lib.bcw_ctx_set_profiling(ctx.handle, 0)
+    crc_ms = tot[roof_k] / max(1, cnt[roof_k])
+    alg = seg_len + 17 * n_frags + 48 * n_rec
+    ctx.close()
+    return {"value": round(seg_len * args.steps / 2 ** 30 / wall, 2), "unit": "GiB/s",
+            "ms_per_step": round(wall / args.steps * 1e3, 4), "steps": args.steps, "warmup": args.warmup,
+            "seg_bytes": seg_len, "records": n_rec, "fragments": n_frags,
+            "k_crc_ms": round(crc_ms, 4), "k_crc_frac": round(alg / (crc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "configs[2]: Zipf(s=1.1) values 128 B-64 KiB (numpy default_rng(42) semantics), same "
+                    "warmup/steps as the headline, measured after it in the same process"}
+
+
 def main():
     args = parse()
     from bitcaskdb_amd import shard
@@ -281,18 +338,20 @@ def main():
         return host, int(n.value), int(r.value)
 
     ptr_t = {"u8": L.u64p, "u4": L.u32p, "u1": L.u8p}
+
+    def make_table(cap):
+        cols = {}
+        for name, dt in L.TABLE_COLUMNS:
+            tdt = {"u8": torch.int64, "u4": torch.int32, "u1": torch.uint8}[dt]
+            cols[name] = torch.empty(cap, dtype=tdt, device=dev)
+        return L.RecordTable(cap, *[C.cast(C.c_void_p(cols[name].data_ptr()), ptr_t[dt])
+                                    for name, dt in L.TABLE_COLUMNS]), cols
     slots = []
     for j in range(nslot):
         host, seg_len, n_rec = build_segment(shard.segment_seed(42 + 1000 * j, rank))
         d_seg = host.to(dev, non_blocking=True)
         # ---- device record table + result ----
-        cap = n_rec + 64
-        cols = {}
-        for name, dt in L.TABLE_COLUMNS:
-            tdt = {"u8": torch.int64, "u4": torch.int32, "u1": torch.uint8}[dt]
-            cols[name] = torch.empty(cap, dtype=tdt, device=dev)
-        table = L.RecordTable(cap, *[C.cast(C.c_void_p(cols[name].data_ptr()), ptr_t[dt])
-                                     for name, dt in L.TABLE_COLUMNS])
+        table, cols = make_table(n_rec + 64)
         d_res = torch.zeros(C.sizeof(L.DecodeResult), dtype=torch.uint8, device=dev)
         params = L.DecodeParams(seg_len, BASE_TIME, 40, 20, 20, L.MODE_RECORD)
         sctx = Context(torch.cuda.current_device())
@@ -451,8 +510,10 @@ def main():
                 "pipeline_GBs": round(bytes_total / args.steps / (ms_per_step * 1e-3) / 1e9, 1),
                 "kernel_ms_all": {k: round(v, 4) for k, v in kern.items()}}
 
-    # ---- end-to-end through the host I/O staging (rank 0, N=1) ----
+    # ---- config C and end-to-end through the host I/O staging (rank 0, N=1) ----
     extras = {}
+    if world == 1 and not args.no_extras and args.config == "B":
+        extras["config_c"] = config_c_leg(L, Context, torch, dev, args, make_table, roof_name, names)
     if world == 1 and not args.no_extras:
         extras["e2e"] = end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec)
 

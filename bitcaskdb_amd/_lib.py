@@ -103,11 +103,11 @@ MODE_RECORD, MODE_HINT = 0, 1
 ST_OK, ST_INVALID, ST_PANIC, ST_UNSUPPORTED = 0, 1, 2, 3
 ERR_NONE, ERR_CRC, ERR_TYPE, ERR_PANIC, ERR_INTERNAL = 0, 1, 2, 3, 4
 SB_OK, SB_SHORT, SB_CRC, SB_MAGIC, SB_BLOCKSIZE = 0, 1, 2, 3, 4
-E_CAPACITY = -4
+E_INVAL, E_CAPACITY = -1, -4
 OPT_CHASE_DIRECT = 1  # bcw_ctx_set_option: k_chase direct-sum workgroup limit (0 forces the look-back)
 OPT_DECODE_CHUNKS = 3  # bcw_ctx_set_option: retired (only 1 accepted)
 OPT_DECODE_PATH = 2  # bcw_ctx_set_option: retired (only 1 accepted: k_chase + k_crc)
-OPT_TEST_ABORT_WAIT = 4  # bcw_ctx_set_option: test only, the next decode's k_chase workgroup value-1 gives up its wait
+OPT_TEST_ABORT_WAIT = 4  # bcw_ctx_set_option: fault injection (needs BCW_TEST_HOOKS=1): the next decode's k_chase workgroup value-1 gives up its wait
 E_IO = -6
 ENC_COMPACT, ENC_HINT = 0, 1
 ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC, ENC_ERR_TABLE, ENC_ERR_STALE = 0, 1, 2, 3, 4, 5

@@ -821,6 +821,9 @@ __device__ __forceinline__ void finalize(const EmitArgs& A, uint64_t nblocks, ui
   r.retry_frag_capacity = (nfr > frag_cap && abort_site == 0ull) ? nfr : 0;  // (a stale count is no capacity)
   r.generation = gen;
   *res = r;
+  // after a give-up the fragment table and verdicts are stale (aborted waves verify nothing): the fragment export
+  // (k_export_frags, bcw_decode_fragments) delivers no row for this decode
+  if (abort_site != 0ull) misc[M_NFRAGS] = 0;
   // for the next decode (the scratch setup sets them first)
   misc[M_DONE_CRC] = 0;
   misc[M_BAD_CRC] = ~0ull;

@@ -346,7 +346,8 @@ def _frag_error(res):
     if res.err_class == L.ERR_PANIC:
         return RefPanic("slice bounds out of range (startOff beyond file size)")
     if res.err_class == L.ERR_INTERNAL:
-        raise RuntimeError("bcw decode: a k_chase wait exceeded its bound (device-side protocol failure); no row was delivered")
+        raise RuntimeError("bcw decode: a device-side wait exceeded its bound or the fragment table disagreed with the "
+                           "chunk stream (protocol failure); no row was delivered")
     return None
 
 
@@ -474,7 +475,14 @@ class WalFile:
 
 
 _ENC_ERRORS = {L.ENC_ERR_EXPIRE: lambda: WalError("invalid expire"),
-               L.ENC_ERR_PANIC: lambda: RefPanic("index out of range (PutUvarint into [MaxVarintLen32]byte)")}
+               L.ENC_ERR_PANIC: lambda: RefPanic("index out of range (PutUvarint into [MaxVarintLen32]byte)"),
+               # nothing was appended: the encode's own decode of the source delivered no usable table (it reported
+               # BCW_ERR_INTERNAL, or its table is smaller than the decode), or another decode ran on the context in
+               # between. A compaction must not report success here: the caller would drop the source with no copy.
+               L.ENC_ERR_TABLE: lambda: RuntimeError("bcw encode: the source decode delivered no usable record table "
+                                                     "(BCW_ENC_ERR_TABLE); nothing was written"),
+               L.ENC_ERR_STALE: lambda: RuntimeError("bcw encode: the source decode is not the context's latest "
+                                                     "(BCW_ENC_ERR_STALE); nothing was written")}
 
 
 def _src_error(res, dec_class, status):
@@ -548,6 +556,8 @@ def new_hint_by_wal(wal: Wal, ns_size: int = 20, etag_size: int = 20, ctx: Conte
             dec = ctx.decode(wal.data, wal.start_off, wal.base_time, ns_size, etag_size)
             st = int(dec.table["status"][res.err_record])
         raise _src_error(res, res.src_err_class, st)
+    if res.err_class in _ENC_ERRORS:
+        raise _ENC_ERRORS[res.err_class]()
     return h
 
 

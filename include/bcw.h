@@ -194,9 +194,11 @@ const char* bcw_kernel_name(int kernel_id);
  *   BCW_OPT_DECODE_PATH,  retired in round 4 (the one-launch k_scan and the two-chunk decode lost to k_chase +
  *   BCW_OPT_DECODE_CHUNKS the stream-verify k_crc on every configuration): only the value 1
  *                         is accepted (BCW_OK, no effect), any other returns BCW_E_INVAL.
- *   BCW_OPT_TEST_ABORT_WAIT  test only: in the NEXT decode on the context, the k_chase workgroup value - 1 gives up
- *                         its predecessor wait at once (0: none, the default), as a wait that ran past its 200 ms
- *                         bound would; that decode reports BCW_ERR_INTERNAL with no rows. One-shot. */
+ *   BCW_OPT_TEST_ABORT_WAIT  fault injection for the test suite, not for production: accepted only when the
+ *                         process runs with the environment variable BCW_TEST_HOOKS=1 (else BCW_E_INVAL). In the
+ *                         NEXT decode on the context, the k_chase workgroup value - 1 gives up its predecessor wait
+ *                         at once (0: none, the default), as a wait that ran past its 200 ms bound would; that decode
+ *                         reports BCW_ERR_INTERNAL with no rows. One-shot. */
 #define BCW_OPT_CHASE_DIRECT 1
 #define BCW_OPT_DECODE_PATH 2
 #define BCW_OPT_DECODE_CHUNKS 3
@@ -236,7 +238,8 @@ int bcw_decode_segment(bcw_ctx* ctx, const uint8_t* h_seg, const bcw_decode_para
 /* Fragment table of the most recent decode on this context (device arrays), global order. */
 int bcw_decode_fragments_async(bcw_ctx* ctx, const bcw_frag_table* d_frags);
 /* Same, into host arrays (synchronous). *n_total receives the number of fragments the framing
- * has (rows beyond h_frags->capacity are not copied). */
+ * has (rows beyond h_frags->capacity are not copied). After a decode that reported BCW_ERR_INTERNAL both
+ * deliver no row (n_total 0): that decode's fragment table and verdicts are not valid. */
 int bcw_decode_fragments(bcw_ctx* ctx, const bcw_frag_table* h_frags, uint64_t* n_total);
 
 /* ---- host WAL writer (wal.go:490-553 with Record.Encode record.go:57-138) ----

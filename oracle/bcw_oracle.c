@@ -195,16 +195,20 @@ int oc_super_load(const uint8_t* p, size_t n, oc_super* o) {
 /* writer: wal.go:482-553. The in-memory image holds the whole file (super block included), so  */
 /* writeOffset(true) = len - 40 and writeOffset(false) = len.                                   */
 /* ------------------------------------------------------------------------------------------ */
-struct oc_writer { uint8_t* buf; uint64_t len, cap; };
+/* len: the logical file size; vbase: bytes before buf[0] that are only counted (a writer opened at a position far into
+ * a large file, oc_writer_new_at: WriteRecord's layout depends on the position only through its phase in the block
+ * grid, the returned offsets on the position itself) */
+struct oc_writer { uint8_t* buf; uint64_t len, cap, vbase; };
 
 static void w_append(oc_writer* w, const void* p, uint64_t n) {
-  if (w->len + n > w->cap) {
+  const uint64_t used = w->len - w->vbase;
+  if (used + n > w->cap) {
     uint64_t nc = w->cap ? w->cap : 1u << 16;
-    while (nc < w->len + n) nc *= 2;
+    while (nc < used + n) nc *= 2;
     w->buf = (uint8_t*)realloc(w->buf, nc);
     w->cap = nc;
   }
-  oc_memcpy(w->buf + w->len, p, n);
+  oc_memcpy(w->buf + used, p, n);
   w->len += n;
 }
 
@@ -213,6 +217,13 @@ oc_writer* oc_writer_new(uint64_t create_time, uint64_t base_time) {
   uint8_t sb[40];
   oc_super_encode(sb, create_time, base_time);
   w_append(w, sb, 40);
+  return w;
+}
+
+/* a writer whose file already holds `size` bytes (>= 40: the super block and earlier records), none of them kept */
+oc_writer* oc_writer_new_at(uint64_t size) {
+  oc_writer* w = (oc_writer*)calloc(1, sizeof *w);
+  w->len = w->vbase = size < OC_SUPER_SIZE ? OC_SUPER_SIZE : size;
   return w;
 }
 
@@ -247,7 +258,9 @@ uint64_t oc_writer_write(oc_writer* w, const uint8_t* rec, size_t n) {
 }
 
 uint64_t oc_writer_size(const oc_writer* w) { return w->len; }
+/* the materialized bytes: file offsets [oc_writer_base(w), oc_writer_size(w)) */
 const uint8_t* oc_writer_data(const oc_writer* w) { return w->buf; }
+uint64_t oc_writer_base(const oc_writer* w) { return w->vbase; }
 void oc_writer_free(oc_writer* w) { if (w) { free(w->buf); free(w); } }
 
 /* ------------------------------------------------------------------------------------------ */

@@ -97,6 +97,9 @@ int oc_super_load(const uint8_t* p, size_t n, oc_super* out);
 /* ---- writer (wal.go:490-553), growable in-memory file image ---- */
 typedef struct oc_writer oc_writer;
 oc_writer* oc_writer_new(uint64_t create_time, uint64_t base_time);
+/* a writer whose file already holds `size` bytes, none of them materialized: data() starts at file offset base() */
+oc_writer* oc_writer_new_at(uint64_t size);
+uint64_t oc_writer_base(const oc_writer* w);
 uint64_t oc_writer_write(oc_writer* w, const uint8_t* rec, size_t n); /* returns record offset */
 uint64_t oc_writer_size(const oc_writer* w);
 const uint8_t* oc_writer_data(const oc_writer* w);

@@ -48,6 +48,10 @@ lib.oc_writer_write.restype = C.c_uint64
 lib.oc_writer_write.argtypes = [vp, vp, C.c_size_t]
 lib.oc_writer_size.restype = C.c_uint64
 lib.oc_writer_size.argtypes = [vp]
+lib.oc_writer_new_at.restype = vp
+lib.oc_writer_new_at.argtypes = [C.c_uint64]
+lib.oc_writer_base.restype = C.c_uint64
+lib.oc_writer_base.argtypes = [vp]
 lib.oc_writer_data.restype = vp
 lib.oc_writer_data.argtypes = [vp]
 lib.oc_writer_free.argtypes = [vp]
@@ -182,8 +186,10 @@ def put_uvarint(v: int) -> bytes:
 class Writer:
     """oc_writer: WAL file image (wal.go:490-553)."""
 
-    def __init__(self, create_time: int, base_time: int):
-        self.h = lib.oc_writer_new(create_time, base_time)
+    def __init__(self, create_time: int, base_time: int, at: int | None = None):
+        """at: open the writer at file size `at` (>= 40) with none of those bytes kept (oc_writer_new_at): the
+        appended bytes are data(), at file offsets [base(), size())"""
+        self.h = lib.oc_writer_new(create_time, base_time) if at is None else lib.oc_writer_new_at(at)
 
     def write(self, rec: bytes) -> int:
         return int(lib.oc_writer_write(self.h, _ptr(rec), len(rec)))
@@ -191,8 +197,11 @@ class Writer:
     def size(self) -> int:
         return int(lib.oc_writer_size(self.h))
 
+    def base(self) -> int:
+        return int(lib.oc_writer_base(self.h))
+
     def data(self) -> bytes:
-        return _bytes_at(lib.oc_writer_data(self.h), self.size())
+        return _bytes_at(lib.oc_writer_data(self.h), self.size() - self.base())
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -3,6 +3,9 @@ import sys
 
 import pytest
 
+# the library's fault-injection option (BCW_OPT_TEST_ABORT_WAIT) is refused unless the process opts in
+os.environ.setdefault("BCW_TEST_HOOKS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))

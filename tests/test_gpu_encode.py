@@ -225,3 +225,28 @@ def test_roundtrip_decode_of_encoded(ctx):
     assert hdec.n_records == int(keep.sum())
     np.testing.assert_array_equal(hdec.table["aux0"], written)
     del sb
+
+
+@pytest.mark.parametrize("wal_pos,hint_pos", [((1 << 35) + 12345, (1 << 32) + 777),
+                                              ((1 << 32) - 3_000_000, (1 << 28) - 100_000),
+                                              ((1 << 40) + 32768 - 3, (1 << 33) + 7)])
+def test_compact_config_e_large_offsets(ctx, wal_pos, hint_pos):
+    """config E's regime (a 42.3 GB dst WAL): appends of config-E-shape records (NsSize 20, 100 B keys, 4 KiB values)
+    at dst positions past 2^32 and 2^35 (WriteRecord offsets above 32 bits, hint `off` varints of 5 and 6 bytes,
+    hint.go:32-48) and crossing 2^32 inside the batch, hint positions past 2^28 / 2^32 -- against oc_compact_append on
+    writers opened at those positions (wal.go:482-516: the layout depends on the position only through its block
+    phase, the returned offsets and hint fields on the position itself)"""
+    src = np.frombuffer(O.synth(8 << 20, 0, 77, 20, 100, 4096, 0, BASE), dtype=np.uint8)
+    n_rec = len(O.decode(src, 40, BASE, 20, 20, want_bytes=False).recs)
+    keep = np.ones(n_rec, dtype=np.uint8)
+    keep[::97] = 0  # a few dropped rows: the dense layout has gaps in the source
+    dst, hint = O.Writer(BASE, BASE, at=wal_pos), O.Writer(BASE, BASE, at=hint_pos)
+    ec, er, nin, offs = O.compact_append(dst, hint, 5, src, 40, BASE, BASE, 20, 20, keep)
+    assert ec == 0 and nin == n_rec
+    assert int(offs[keep.astype(bool)].max()) > wal_pos  # the offsets really are that large
+    res, wal, hb, goffs = ctx.encode(src, L.ENC_COMPACT, 40, BASE, 5, wal_pos, hint_pos, 20, 20, keep)
+    assert res.err_class == 0 and res.n_in == nin
+    assert res.wal_end == dst.size() and res.hint_end == hint.size()
+    assert wal == dst.data(), "dst WAL bytes differ"
+    assert hb == hint.data(), "hint WAL bytes differ"
+    np.testing.assert_array_equal(goffs[:nin], offs[:nin])

@@ -203,9 +203,11 @@ def test_forced_wait_abort(direct):
         p = cases.params()
         seg = np.frombuffer(data, dtype=np.uint8)
         c.set_option(L.OPT_TEST_ABORT_WAIT, 6)
-        got = c.decode(seg, p["start_off"], p["base_time"], p["ns_size"], p["etag_size"], p["mode"])
+        got = c.decode(seg, p["start_off"], p["base_time"], p["ns_size"], p["etag_size"], p["mode"], with_frags=True)
         r = got.result
         assert r.err_class == L.ERR_INTERNAL
+        # the aborted decode's fragment table and verdicts are stale: the export delivers no row
+        assert all(len(v) == 0 for v in got.frags.values())
         assert r.err_frag == 9 if direct else r.err_frag in (10, 11)  # the site (the largest one that gave up)
         assert r.n_records == 0 and r.n_records_total == 0 and r.retry_frag_capacity == 0
         assert r.first_bad_record == -1 and r.err_file_off == 0
@@ -218,6 +220,30 @@ def test_forced_wait_abort(direct):
                                        np.ones(got.result.n_blocks * 8, dtype=np.uint8))
             assert res.err_class == L.ENC_ERR_TABLE and res.n_in == 0 and res.n_written == 0
             assert wal == b"" and hb == b""
+            # ... and the wrappers raise instead of returning an empty output as a success: a compaction
+            # that wrote nothing must not let its caller drop the source, an empty hint must not look valid
+            from bitcaskdb_amd import wal as W
+            src = W.load_wal(data, fid=4)
+            for call in (lambda: W.compact_one_wal(W.WalFile(9, BASE), W.WalFile(9, BASE), src,
+                                                    np.ones(got.result.n_blocks * 8, dtype=np.uint8), ctx=c),
+                         lambda: W.new_hint_by_wal(src, ctx=c)):
+                c.set_option(L.OPT_TEST_ABORT_WAIT, 6)
+                with pytest.raises(RuntimeError):
+                    call()
         c.sync()
+    finally:
+        c.close()
+
+
+@pytest.mark.gpu
+def test_abort_hook_needs_opt_in(monkeypatch):
+    """BCW_OPT_TEST_ABORT_WAIT is a fault-injection hook: refused (BCW_E_INVAL) unless BCW_TEST_HOOKS=1"""
+    from bitcaskdb_amd import Context
+    c = Context(0)
+    try:
+        monkeypatch.delenv("BCW_TEST_HOOKS", raising=False)
+        assert L.lib.bcw_ctx_set_option(c.handle, L.OPT_TEST_ABORT_WAIT, 6) == L.E_INVAL
+        monkeypatch.setenv("BCW_TEST_HOOKS", "1")
+        assert L.lib.bcw_ctx_set_option(c.handle, L.OPT_TEST_ABORT_WAIT, 0) == 0
     finally:
         c.close()

@@ -248,3 +248,21 @@ def test_meta_app_size_zero_and_expire_panic():
     base = 1_700_000_000
     assert O.record_encode(b"", b"k", b"v", b"", base + (1 << 35) - 1, False, b"", base) is not None
     assert O.record_encode(b"", b"k", b"v", b"", base + (1 << 35), False, b"", base) is None  # reference panics
+
+
+def test_writer_virtual_start():
+    """oc_writer_new_at (the large-offset encode tests' reference): a writer opened at file size P keeps none of the
+    first P bytes but lays out and returns offsets exactly as a writer that really wrote them (wal.go:482-516)"""
+    BASE = 1_700_000_000
+    rng = random.Random(11)
+    for target in (40, 41, 32768 + 40 - 7, 3 * 32768 + 123, 5 * 32768 + 40 - 3):
+        w = O.Writer(BASE, BASE)
+        while w.size() < target:
+            w.write(bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, min(5000, target - w.size() + 8)))))
+        P = w.size()
+        v = O.Writer(BASE, BASE, at=P)
+        assert v.size() == P and v.base() == P
+        for _ in range(40):
+            rec = bytes(rng.getrandbits(8) for _ in range(rng.choice([1, 6, 7, 100, 4222, 32761, 40000])))
+            assert w.write(rec) == v.write(rec)
+        assert w.size() == v.size() and w.data()[P:] == v.data()
