@@ -415,7 +415,6 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   s.nblocks_cap = nb;
   s.frag_cap = fc;
   s.nlb = nwg;
-  s.tickets = 0;
   s.epoch = 1;
   s.chase_direct = c->chase_direct;
   // on the codec's stream: a null-stream hipMemset is not ordered before kernels on a non-blocking

@@ -24,7 +24,6 @@ enum { M_FIRST_BAD = 0,  // first record whose parse fails (atomicMin in k_crc's
        M_NFRAGS = 4, M_DONE_CRC = 5,
        M_T_CRC0 = 10, M_T_FIN = 11,  // wall_clock64 stamps (diagnostics)
        M_ABORT = 12,     // k_chase: the wait site that timed out (0: none); reported as BCW_ERR_INTERNAL
-       M_TICKET = 13,    // k_chase workgroup tickets (monotonic across launches)
        M_BAD_CRC = 14,   // first fragment failing its CRC (atomicMin in k_crc; reset by the finalize)
        M_BAD_TYPE = 15 };  // first fragment of an unknown type (atomicMin in k_chase; reset by k_crc's finalize)
 
@@ -112,9 +111,8 @@ __device__ __forceinline__ uint32_t wg256_excl_scan(uint32_t v, uint32_t* sm4, u
 // workgroup chases one block (keeping its first kChaseHold headers in LDS), the wave scans the counts,
 // publishes its aggregate and walks back over earlier workgroups' published values for its fragment
 // base, then writes the fragment table (a block with more headers chases its tail again; the lines are
-// cache-resident by then). Workgroups take tickets in launch order, so a workgroup only ever waits on
-// ones already running. Look-back words: epoch << 40 | flag << 38 | count (flag 1: aggregate,
-// 2: inclusive prefix). One wave per workgroup spreads the blocks over every CU: the chase is a chain
+// cache-resident by then). A workgroup only waits on lower workgroup ids (dispatched before it). Look-back words:
+// epoch << 40 | flag << 38 | count (flag 1: aggregate, 2: inclusive prefix). One wave per workgroup spreads the blocks over every CU: the chase is a chain
 // of scattered header reads, bound by latency and by each CU's address-processing rate.
 //
 // The chase is the iterator's header loop (wal_iterator.go:45-77: the block's buffer is
@@ -214,7 +212,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                               Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t frag_cap,
                                               uint64_t* __restrict__ lb,
                                               uint64_t* __restrict__ lbe, uint64_t* __restrict__ misc,
-                                              uint64_t ticket_base, uint64_t epoch, const uint32_t* __restrict__ initc,
+                                              uint64_t epoch, const uint32_t* __restrict__ initc,
                                               uint32_t direct_max, uint32_t* __restrict__ equeue,
                                               uint64_t test_abort_wg) {
   // {crc, start | len << 16} and type of each lane's first 64 headers: 36 KiB, so a k_chase workgroup still fits beside
@@ -227,10 +225,11 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   __shared__ uint8_t s_type[kHold][64];
   const uint32_t lane = threadIdx.x;
   const uint64_t tc0 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
-  uint64_t wg = 0;
-  if (lane == 0) wg = atomicAdd(reinterpret_cast<unsigned long long*>(&misc[M_TICKET]), 1ull) - ticket_base;
-  wg = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)wg) |
-       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wg >> 32)) << 32);
+  // the workgroup id orders the look-back: workgroups are dispatched in id order (within each XCD), so one only waits
+  // on ids already running; the bounded waits (Spin) turn any other schedule into BCW_ERR_INTERNAL, never a hang.
+  // (Round 4 took tickets from one atomic counter: its 512 returning atomics on one word ended 5-7 us apart, and the
+  // last ticket's chase gated every base: k_chase B 22.1 -> 16.8 us, C 31.3 -> 24.3 us without them, kbench.)
+  const uint64_t wg = blockIdx.x;
   const uint64_t b = wg * 64 + lane;
   uint32_t bufsize = 0;
   uint64_t boff = 0;
@@ -1341,11 +1340,10 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
   pr.begin(K_CHASE, stream, ev);
   k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
-                                        s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch, tabs.initc, s.chase_direct,
+                                        s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.epoch, tabs.initc, s.chase_direct,
                                         s.equeue, s.test_abort_wg);
   s.test_abort_wg = 0;
   pr.end(K_CHASE, stream, ev);
-  s.tickets += nb_grid;
   if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse
     (void)hipMemsetAsync(s.lb, 0, s.nlb * sizeof(uint64_t), stream);
     (void)hipMemsetAsync(s.lbe, 0, s.nlb * sizeof(uint64_t), stream);

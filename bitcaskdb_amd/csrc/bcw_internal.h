@@ -71,7 +71,6 @@ struct Scratch {
   uint64_t* lb = nullptr;      // [nblocks/64+2] k_chase look-back words (zeroed at allocation)
   uint64_t* lbe = nullptr;     // [nblocks/64+2] k_chase look-back words of the Full/Last counts (> kDirect groups)
   uint64_t nlb = 0;
-  uint64_t tickets = 0;        // k_chase tickets issued so far (misc[M_TICKET] mirrors it)
   uint64_t epoch = 1;          // look-back epoch of the next launch
   Frag* frags = nullptr;       // [frag_cap]
   uint4* srec = nullptr;       // [frag_cap + 4] stream record per fragment (k_chase -> k_crc, bcw_decode.hip kRecUsual)

@@ -440,9 +440,8 @@ int main(int argc, char** argv) {
     auto crun = [&](auto kern) {
       return timeit([&] {
         kern<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
-                                                              s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.tickets, s.epoch,
+                                                              s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.epoch,
                                                               ctx->tabs.initc, s.chase_direct, s.equeue, 0ull);
-        s.tickets += (nblocks + 63) / 64;
         ++s.epoch;
       }, reps, st);
     };
