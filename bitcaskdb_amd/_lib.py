@@ -84,6 +84,21 @@ class IndexResult(C.Structure):
     _fields_ = [("n_in", C.c_uint64), ("n_done", C.c_uint64), ("err_class", C.c_int32), ("_pad", C.c_int32)]
 
 
+class RecoverFile(C.Structure):
+    _fields_ = [("fid", C.c_uint64), ("wal", C.c_void_p), ("wal_p", DecodeParams), ("hint", C.c_void_p),
+                ("hint_p", DecodeParams)]
+
+
+class RecoverStatus(C.Structure):
+    _fields_ = [("used", C.c_int32), ("rc", C.c_int32), ("hint_dres", DecodeResult), ("wal_dres", DecodeResult),
+                ("hint_ires", IndexResult), ("wal_ires", IndexResult)]
+
+
+class CompactSrc(C.Structure):
+    _fields_ = [("fid", C.c_uint64), ("data", C.c_void_p), ("len", C.c_uint64), ("start_off", C.c_uint32),
+                ("_pad", C.c_uint32), ("out", EncodeOut)]
+
+
 class IndexInfo(C.Structure):
     _fields_ = [("live", C.c_uint64), ("slots_used", C.c_uint64), ("slot_capacity", C.c_uint64),
                 ("arena_used", C.c_uint64), ("arena_capacity", C.c_uint64), ("overflow", C.c_uint64)]
@@ -114,6 +129,7 @@ ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC, ENC_ERR_TABLE, ENC_ERR
 IDX_PUT, IDX_DELETE, IDX_SOFT_DELETE = 0, 1, 2
 IDX_FOUND, IDX_NOT_FOUND, IDX_SOFT_DELETED = 0, 1, 2
 IDX_ERR_FULL = 6
+RECOVER_NOT_RUN, RECOVER_HINT, RECOVER_HINT_WAL, RECOVER_WAL = 0, 1, 2, 3
 RD_OK, RD_BEYOND, RD_CORRUPTED, RD_CRC, RD_SIZE, RD_TYPE, RD_INCOMPLETE, RD_PANIC = range(8)
 
 
@@ -166,6 +182,13 @@ def _load():
         "bcw_compact_filter_async": (C.c_int, [vp, vp, C.POINTER(DecodeParams), C.POINTER(RecordTable), vp,
                                                C.c_uint64, vp, vp]),
         "bcw_index_export": (C.c_int, [vp, vp, C.c_uint64, u64p, u64p, u64p, u64p, C.c_uint64, u64p, u64p]),
+        "bcw_index_export_fids": (C.c_int, [vp, u64p, C.c_uint64, vp, C.c_uint64, u64p, u64p, u64p, u64p,
+                                            C.c_uint64, u64p, u64p]),
+        "bcw_recover_wals": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, C.POINTER(RecoverFile), C.c_uint64,
+                                       C.POINTER(RecoverStatus), C.POINTER(C.c_int64)]),
+        "bcw_compact_wals": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, C.POINTER(CompactSrc), C.c_uint64,
+                                       C.POINTER(EncodeParams), C.POINTER(EncodeResult), C.POINTER(IndexResult),
+                                       u64p]),
         "bcw_compact_segment": (C.c_int, [vp, vp, vp, C.POINTER(EncodeParams), C.c_uint64, C.POINTER(EncodeOut),
                                           C.POINTER(EncodeResult), C.POINTER(IndexResult)]),
         "bcw_index_recover_segment": (C.c_int, [vp, vp, vp, C.POINTER(DecodeParams), C.c_uint64, C.c_int,

@@ -7,7 +7,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRCS = [os.path.join(HERE, "csrc", f) for f in ("bcw_api.cpp", "bcw_decode.hip", "bcw_encode.hip", "bcw_index.hip", "bcw_io.cpp", "bcw_read.hip")]
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("bcw_api.cpp", "bcw_decode.hip", "bcw_encode.hip", "bcw_fanout.cpp", "bcw_index.hip", "bcw_io.cpp", "bcw_read.hip")]
 OUT = os.path.join(HERE, "libbcw.so")
 ARCH = os.environ.get("BCW_OFFLOAD_ARCH", "gfx950")
 

@@ -725,7 +725,7 @@ int bcw_encode_segment_async(bcw_ctx* c, const uint8_t* d_src, const bcw_encode_
 
 }  // extern "C"
 
-namespace {
+namespace bcw {
 // Sync-API staging: the source segment into the context's device buffer, decoded into the context's
 // device table (grown until it holds every record), the fragment scratch retried until it fits.
 int sync_decode(bcw_ctx* c, const uint8_t* h_src, const bcw_decode_params& dp, bcw_decode_result& dres) {
@@ -820,7 +820,7 @@ int encode_to_host(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out*
     for (uint64_t i = nr; i < h->rec_off_cap && i < dres.n_records; ++i) h->rec_off[i] = ~0ull;
   return BCW_OK;
 }
-}  // namespace
+}  // namespace bcw
 
 extern "C" {
 

@@ -581,12 +581,25 @@ __global__ __launch_bounds__(256) void k_ix_rehash(const Slot* __restrict__ old,
 }
 
 // ---- export of the live entries (the Go shim loads them into its ShardMap after a GPU rebuild) --------
+// fids (sorted, nf > 0): only entries whose value fid is one of them (the slice of the index that points into
+// a set of WAL files: the compaction fan-out's filter snapshot)
+__device__ __forceinline__ bool fid_in(const uint64_t* __restrict__ fids, uint32_t nf, uint64_t f) {
+  if (nf == 0) return true;
+  uint32_t lo = 0, hi = nf;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (fids[m] < f) lo = m + 1; else hi = m;
+  }
+  return lo < nf && fids[lo] == f;
+}
+
 __global__ __launch_bounds__(256) void k_ix_count(const Slot* __restrict__ slots, uint64_t cap,
-                                                  const uint8_t* __restrict__ arena, uint64_t* __restrict__ blk_n,
+                                                  const uint8_t* __restrict__ arena, const uint64_t* __restrict__ fids,
+                                                  uint32_t nf, uint64_t* __restrict__ blk_n,
                                                   uint64_t* __restrict__ blk_b) {
   const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
   uint64_t c = 0, b = 0;
-  if (i < cap && slots[i].kref && slots[i].live) {
+  if (i < cap && slots[i].kref && slots[i].live && fid_in(fids, nf, slots[i].fid)) {
     c = 1;
     b = *reinterpret_cast<const uint32_t*>(arena + (slots[i].kref - 1) + 8);
   }
@@ -604,7 +617,8 @@ __global__ __launch_bounds__(256) void k_ix_count(const Slot* __restrict__ slots
 }
 
 __global__ __launch_bounds__(256) void k_ix_export(const Slot* __restrict__ slots, uint64_t cap,
-                                                   const uint8_t* __restrict__ arena, const uint64_t* __restrict__ blk_n,
+                                                   const uint8_t* __restrict__ arena, const uint64_t* __restrict__ fids,
+                                                   uint32_t nf, const uint64_t* __restrict__ blk_n,
                                                    const uint64_t* __restrict__ blk_b, uint8_t* __restrict__ keys,
                                                    uint64_t* __restrict__ koff, uint64_t* __restrict__ fid,
                                                    uint64_t* __restrict__ off, uint64_t* __restrict__ size) {
@@ -612,7 +626,7 @@ __global__ __launch_bounds__(256) void k_ix_export(const Slot* __restrict__ slot
   uint64_t c = 0, b = 0;
   Slot S{};
   if (i < cap) S = slots[i];
-  const bool act = i < cap && S.kref && S.live;
+  const bool act = i < cap && S.kref && S.live && fid_in(fids, nf, S.fid);
   if (act) {
     c = 1;
     b = *reinterpret_cast<const uint32_t*>(arena + (S.kref - 1) + 8);
@@ -791,6 +805,73 @@ Src table_src(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_params* p, cons
 }
 
 }  // namespace
+
+namespace bcw {
+int ix_export(bcw_index* x, const uint64_t* h_fids, uint64_t n_fids, IxSink& sink, uint64_t* n_out,
+              uint64_t* key_bytes) {
+  DeviceGuard dg(x->ctx->device);
+  if (!dg.ok) return BCW_E_HIP;
+  hipStream_t st = x->ctx->cur;
+  std::vector<uint64_t> fids(h_fids, h_fids + n_fids);
+  std::sort(fids.begin(), fids.end());
+  fids.erase(std::unique(fids.begin(), fids.end()), fids.end());
+  if (fids.size() > 0xffffffffull) return BCW_E_INVAL;
+  const uint32_t nf = (uint32_t)fids.size();
+  const uint64_t fb = (8 * (uint64_t)nf + 15) & ~15ull, nblk = (x->cap + 255) / 256;
+  // staging: fids | per-block entry counts | per-block key bytes (then their exclusive prefixes) | outputs
+  int rc = ix_stage(x, fb + nblk * 16 + 64);
+  if (rc != BCW_OK) return rc;
+  uint64_t* d_fids = (uint64_t*)x->stage;
+  uint64_t* blk_n = (uint64_t*)((uint8_t*)x->stage + fb);
+  uint64_t* blk_b = blk_n + nblk;
+  if (nf && hipMemcpyAsync(d_fids, fids.data(), 8 * (uint64_t)nf, hipMemcpyHostToDevice, st) != hipSuccess)
+    return BCW_E_HIP;
+  k_ix_count<<<(uint32_t)nblk, 256, 0, st>>>(x->slots, x->cap, x->arena, d_fids, nf, blk_n, blk_b);
+  std::vector<uint64_t> hn(nblk), hb(nblk);
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(hn.data(), blk_n, nblk * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(hb.data(), blk_b, nblk * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return BCW_E_HIP;
+  uint64_t tn = 0, tb = 0;
+  for (uint64_t b = 0; b < nblk; ++b) {
+    const uint64_t a = hn[b], k = hb[b];
+    hn[b] = tn;
+    hb[b] = tb;
+    tn += a;
+    tb += k;
+  }
+  *n_out = tn;
+  *key_bytes = tb;
+  rc = sink.room(tn, tb);
+  if (rc != BCW_OK || tn == 0) return rc;
+  const uint64_t tbp = (tb + 15) & ~15ull;
+  rc = ix_stage(x, fb + nblk * 16 + tbp + 8 * (tn + 1) + 24 * tn + 64);  // a regrow drops the contents
+  if (rc != BCW_OK) return rc;
+  d_fids = (uint64_t*)x->stage;
+  uint64_t* pn = (uint64_t*)((uint8_t*)x->stage + fb);
+  uint64_t* pb = pn + nblk;
+  uint8_t* keys = (uint8_t*)(pb + nblk);
+  uint64_t* koff = (uint64_t*)(keys + tbp);
+  uint64_t* fid = koff + tn + 1;
+  uint64_t* off = fid + tn;
+  uint64_t* size = off + tn;
+  bool ok = (!nf || hipMemcpyAsync(d_fids, fids.data(), 8 * (uint64_t)nf, hipMemcpyHostToDevice, st) == hipSuccess) &&
+            hipMemcpyAsync(pn, hn.data(), nblk * 8, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(pb, hb.data(), nblk * 8, hipMemcpyHostToDevice, st) == hipSuccess;
+  if (ok)
+    k_ix_export<<<(uint32_t)nblk, 256, 0, st>>>(x->slots, x->cap, x->arena, d_fids, nf, pn, pb, keys, koff, fid, off,
+                                                  size);
+  ok = ok && hipGetLastError() == hipSuccess &&
+       hipMemcpyAsync(sink.keys, keys, tb, hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipMemcpyAsync(sink.koff, koff, 8 * (tn + 1), hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipMemcpyAsync(sink.fid, fid, 8 * tn, hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipMemcpyAsync(sink.off, off, 8 * tn, hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipMemcpyAsync(sink.size, size, 8 * tn, hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipStreamSynchronize(st) == hipSuccess;
+  return ok ? BCW_OK : BCW_E_HIP;
+}
+}  // namespace bcw
 
 extern "C" {
 
@@ -1053,56 +1134,31 @@ int bcw_compact_filter_async(bcw_index* x, const uint8_t* d_seg, const bcw_decod
 
 int bcw_index_export(bcw_index* x, uint8_t* h_keys, uint64_t keys_cap, uint64_t* h_key_off, uint64_t* h_fid,
                      uint64_t* h_off, uint64_t* h_size, uint64_t entries_cap, uint64_t* n_out, uint64_t* key_bytes) {
-  if (!x || !n_out || !key_bytes) return BCW_E_INVAL;
-  DeviceGuard dg(x->ctx->device);
-  if (!dg.ok) return BCW_E_HIP;
-  hipStream_t st = x->ctx->cur;
-  const uint64_t nblk = (x->cap + 255) / 256;
-  int rc = ix_stage(x, nblk * 16 + 64);
-  if (rc != BCW_OK) return rc;
-  uint64_t* blk_n = (uint64_t*)x->stage;
-  uint64_t* blk_b = blk_n + nblk;
-  k_ix_count<<<(uint32_t)nblk, 256, 0, st>>>(x->slots, x->cap, x->arena, blk_n, blk_b);
-  std::vector<uint64_t> hn(nblk), hb(nblk);
-  if (hipMemcpyAsync(hn.data(), blk_n, nblk * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(hb.data(), blk_b, nblk * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return BCW_E_HIP;
-  uint64_t tn = 0, tb = 0;
-  for (uint64_t b = 0; b < nblk; ++b) {
-    const uint64_t a = hn[b], k = hb[b];
-    hn[b] = tn;
-    hb[b] = tb;
-    tn += a;
-    tb += k;
-  }
-  *n_out = tn;
-  *key_bytes = tb;
-  if (tn > entries_cap || tb > keys_cap) return BCW_E_CAPACITY;
-  if (tn == 0) { if (h_key_off) h_key_off[0] = 0; return BCW_OK; }
-  if (!h_keys || !h_key_off || !h_fid || !h_off || !h_size) return BCW_E_INVAL;
-  const uint64_t tbp = (tb + 15) & ~15ull;
-  void* mem = nullptr;
-  if (hipMalloc(&mem, nblk * 16 + tbp + 8 * (tn + 1) + 24 * tn) != hipSuccess) return BCW_E_NOMEM;
-  uint64_t* pn = (uint64_t*)mem;
-  uint64_t* pb = pn + nblk;
-  uint8_t* keys = (uint8_t*)(pb + nblk);
-  uint64_t* koff = (uint64_t*)(keys + tbp);
-  uint64_t* fid = koff + tn + 1;
-  uint64_t* off = fid + tn;
-  uint64_t* size = off + tn;
-  bool ok = hipMemcpyAsync(pn, hn.data(), nblk * 8, hipMemcpyHostToDevice, st) == hipSuccess &&
-            hipMemcpyAsync(pb, hb.data(), nblk * 8, hipMemcpyHostToDevice, st) == hipSuccess;
-  if (ok) k_ix_export<<<(uint32_t)nblk, 256, 0, st>>>(x->slots, x->cap, x->arena, pn, pb, keys, koff, fid, off, size);
-  ok = ok && hipGetLastError() == hipSuccess &&
-       hipMemcpyAsync(h_keys, keys, tb, hipMemcpyDeviceToHost, st) == hipSuccess &&
-       hipMemcpyAsync(h_key_off, koff, 8 * (tn + 1), hipMemcpyDeviceToHost, st) == hipSuccess &&
-       hipMemcpyAsync(h_fid, fid, 8 * tn, hipMemcpyDeviceToHost, st) == hipSuccess &&
-       hipMemcpyAsync(h_off, off, 8 * tn, hipMemcpyDeviceToHost, st) == hipSuccess &&
-       hipMemcpyAsync(h_size, size, 8 * tn, hipMemcpyDeviceToHost, st) == hipSuccess &&
-       hipStreamSynchronize(st) == hipSuccess;
-  (void)hipFree(mem);
-  return ok ? BCW_OK : BCW_E_HIP;
+  return bcw_index_export_fids(x, nullptr, 0, h_keys, keys_cap, h_key_off, h_fid, h_off, h_size, entries_cap, n_out,
+                               key_bytes);
+}
+
+int bcw_index_export_fids(bcw_index* x, const uint64_t* h_fids, uint64_t n_fids, uint8_t* h_keys, uint64_t keys_cap,
+                          uint64_t* h_key_off, uint64_t* h_fid, uint64_t* h_off, uint64_t* h_size,
+                          uint64_t entries_cap, uint64_t* n_out, uint64_t* key_bytes) {
+  if (!x || !n_out || !key_bytes || (n_fids && !h_fids)) return BCW_E_INVAL;
+  struct Fixed : IxSink {
+    uint64_t ecap, kcap;
+    int room(uint64_t n, uint64_t kb) override {
+      if (n > ecap || kb > kcap) return BCW_E_CAPACITY;
+      return n == 0 || (keys && koff && fid && off && size) ? BCW_OK : BCW_E_INVAL;
+    }
+  } sink;
+  sink.ecap = entries_cap;
+  sink.kcap = keys_cap;
+  sink.keys = h_keys;
+  sink.koff = h_key_off;
+  sink.fid = h_fid;
+  sink.off = h_off;
+  sink.size = h_size;
+  const int rc = ix_export(x, h_fids, n_fids, sink, n_out, key_bytes);
+  if (rc == BCW_OK && *n_out == 0 && h_key_off) h_key_off[0] = 0;
+  return rc;
 }
 
 uint64_t bcw_murmur3_sum64(const uint8_t* p, uint64_t n) {

@@ -190,6 +190,30 @@ bcw_ctx* index_ctx(const bcw_index* ix);
 // Host-side table builders (bcw_api.cpp).
 void build_initc(uint32_t* initc);
 
+// The sync API's steps (bcw_api.cpp), shared with the multi-context fan-out (bcw_fanout.cpp): upload + decode into
+// the context's device table; the keep mask's scratch; the decode parameters of a source WAL file; the encode of
+// the context's decoded source with its keep mask, outputs copied to the host.
+int sync_decode(bcw_ctx* c, const uint8_t* h_src, const bcw_decode_params& dp, bcw_decode_result& dres);
+int ensure_keep(bcw_ctx* c, uint64_t rows);
+bcw_decode_params src_params(const uint8_t* h_src, const bcw_encode_params* p);
+int encode_to_host(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out* h, bcw_encode_result* h_result,
+                   const bcw_decode_result& dres);
+
+// Export of an index's live entries (bcw_index.hip) into host arrays the sink provides once the sizes are known:
+// room(n, key_bytes) fills the five pointers (koff has n + 1 entries) or refuses (BCW_E_CAPACITY). h_fids / n_fids
+// (n_fids > 0): only entries whose value fid is one of them.
+struct IxSink {
+  virtual ~IxSink() = default;
+  virtual int room(uint64_t n, uint64_t key_bytes) = 0;
+  uint8_t* keys = nullptr;
+  uint64_t* koff = nullptr;
+  uint64_t* fid = nullptr;
+  uint64_t* off = nullptr;
+  uint64_t* size = nullptr;
+};
+int ix_export(bcw_index* x, const uint64_t* h_fids, uint64_t n_fids, IxSink& sink, uint64_t* n_out,
+              uint64_t* key_bytes);
+
 }  // namespace bcw
 
 // The context behind the C-ABI handle (bcw.h): one device, one launch stream, constant tables and

@@ -169,10 +169,17 @@ class Index:
         return IndexStats(int(info.live), int(info.slots_used), int(info.slot_capacity), int(info.arena_used),
                           int(info.arena_capacity), int(info.overflow))
 
-    def export(self) -> dict:
-        """every live entry: {merged key: (fid, off, size)}"""
+    def export(self, fids=None) -> dict:
+        """every live entry: {merged key: (fid, off, size)}; fids: only entries whose value fid is one of them
+        (bcw_index_export_fids)"""
+        fa = np.ascontiguousarray(sorted(set(fids)) if fids is not None else [], dtype=np.uint64)
+        nf = int(fa.size)
+        fp = fa.ctypes.data_as(L.u64p) if nf else None
+        if fids is not None and nf == 0:
+            return {}
         n, kb = C.c_uint64(), C.c_uint64()
-        rc = L.lib.bcw_index_export(self._h, None, 0, None, None, None, None, 0, C.byref(n), C.byref(kb))
+        rc = L.lib.bcw_index_export_fids(self._h, fp, nf, None, 0, None, None, None, None, 0, C.byref(n),
+                                         C.byref(kb))
         if rc not in (0, L.E_CAPACITY):
             raise RuntimeError(f"bcw_index_export: {L.lib.bcw_strerror(rc).decode()}")
         if n.value == 0:
@@ -181,9 +188,10 @@ class Index:
         keys = np.zeros(max(kcap, 1), dtype=np.uint8)
         koff = np.zeros(cap + 1, dtype=np.uint64)
         fid, off, size = (np.zeros(cap, dtype=np.uint64) for _ in range(3))
-        rc = L.lib.bcw_index_export(self._h, keys.ctypes.data_as(C.c_void_p), kcap, koff.ctypes.data_as(L.u64p),
-                                    fid.ctypes.data_as(L.u64p), off.ctypes.data_as(L.u64p),
-                                    size.ctypes.data_as(L.u64p), cap, C.byref(n), C.byref(kb))
+        rc = L.lib.bcw_index_export_fids(self._h, fp, nf, keys.ctypes.data_as(C.c_void_p), kcap,
+                                         koff.ctypes.data_as(L.u64p), fid.ctypes.data_as(L.u64p),
+                                         off.ctypes.data_as(L.u64p), size.ctypes.data_as(L.u64p), cap, C.byref(n),
+                                         C.byref(kb))
         if rc != 0:
             raise RuntimeError(f"bcw_index_export: {L.lib.bcw_strerror(rc).decode()}")
         kbytes = keys.tobytes()
@@ -211,10 +219,14 @@ def _iteration_error(dres, ires, hint: bool):
     return _frag_error(dres)
 
 
-def recover_from_wals(index: Index, files, ns_size: int = 20, etag_size: int = 20):
+def recover_from_wals(index: Index, files, ns_size: int = 20, etag_size: int = 20, contexts=None):
     """recoverFromWals (db_impl.go:268-314): for every fid in ascending order, Put every record of its hint
     file (IterateHint); if that iteration fails, Put every record of the data WAL (IterateRecord), keeping
-    the puts already applied. files: {fid: (Wal data, Wal hint or None)}. Raises the data WAL's error."""
+    the puts already applied. files: {fid: (Wal data, Wal hint or None)}. Raises the data WAL's error.
+    contexts (a list of Context, any devices): the files are decoded concurrently, round-robin over them, and
+    the index still receives each file's puts in ascending fid (bcw_recover_wals)."""
+    if contexts:
+        return _recover_fanout(index, files, ns_size, etag_size, contexts)
     for fid in sorted(files):
         wal, hint = files[fid]
         if hint is not None:
@@ -231,6 +243,124 @@ def recover_from_wals(index: Index, files, ns_size: int = 20, etag_size: int = 2
         err = _iteration_error(dres, ires, False)
         if err is not None:
             raise err
+
+
+_NUL = np.zeros(1, dtype=np.uint8)
+
+
+def _ctx_array(contexts):
+    arr = (C.c_void_p * len(contexts))(*[c.handle for c in contexts])
+    return arr, len(contexts)
+
+
+def _recover_fanout(index: Index, files, ns_size: int, etag_size: int, contexts):
+    fids = sorted(files)
+    keep = []  # the segments stay referenced for the call
+    arr = (L.RecoverFile * max(len(fids), 1))()
+    for k, fid in enumerate(fids):
+        wal, hint = files[fid]
+        w = np.ascontiguousarray(wal.data)
+        keep.append(w)
+        arr[k].fid = fid
+        arr[k].wal = w.ctypes.data if w.size else None
+        arr[k].wal_p = L.DecodeParams(w.size, wal.base_time, wal.start_off, ns_size, etag_size, L.MODE_RECORD)
+        if hint is not None:
+            h = np.ascontiguousarray(hint.data)
+            keep.append(h)
+            arr[k].hint = h.ctypes.data if h.size else _NUL.ctypes.data  # present, even when empty
+            arr[k].hint_p = L.DecodeParams(h.size, hint.base_time, hint.start_off, ns_size, 0, L.MODE_HINT)
+        else:
+            arr[k].hint = None
+            arr[k].hint_p = L.DecodeParams(0, 0, 0, ns_size, 0, L.MODE_HINT)
+    st = (L.RecoverStatus * max(len(fids), 1))()
+    stop = C.c_int64(-1)
+    ctxs, n_ctx = _ctx_array(contexts)
+    rc = L.lib.bcw_recover_wals(index.handle, ctxs, n_ctx, arr, len(fids), st, C.byref(stop))
+    if rc != 0:
+        raise RuntimeError(f"bcw_recover_wals: {L.lib.bcw_strerror(rc).decode()}")
+    if stop.value < 0:
+        return
+    s = st[stop.value]
+    if s.rc != 0:
+        raise RuntimeError(f"bcw_recover_wals (fid {fids[stop.value]}): {L.lib.bcw_strerror(s.rc).decode()}")
+    if s.used in (L.RECOVER_HINT, L.RECOVER_HINT_WAL) and s.hint_ires.err_class:
+        raise RuntimeError(f"index put failed: {s.hint_ires.err_class}")
+    if s.used == L.RECOVER_HINT:  # the hint decode gave up (BCW_ERR_INTERNAL): raises
+        _iteration_error(s.hint_dres, s.hint_ires, True)
+        raise RuntimeError("bcw_recover_wals: stopped at a hint without an error")
+    if s.wal_ires.err_class:
+        raise RuntimeError(f"index put failed: {s.wal_ires.err_class}")
+    err = _iteration_error(s.wal_dres, s.wal_ires, False)
+    if err is not None:
+        raise err
+
+
+def compact_wals_filtered(dst: WalFile, hint: WalFile, srcs, index: Index, ns_size: int = 20, etag_size: int = 20,
+                          contexts=None):
+    """doCompactionWork's loop (compaction.go:201-211): compact_one_wal_filtered of every source Wal in order
+    into one dst / hint pair. contexts (a list of Context, any devices): the sources are uploaded, decoded and
+    filtered concurrently, round-robin over them; the encodes append in source order (bcw_compact_wals).
+    Returns [(dst offsets per source row, rows kept)] per source; raises the first source's error after the
+    appends the reference makes before it."""
+    if not contexts:
+        return [compact_one_wal_filtered(dst, hint, s, index, ns_size, etag_size) for s in srcs]
+    out = []
+    k0 = 0
+    caps = {}
+    while k0 < len(srcs):
+        part = srcs[k0:]
+        n = len(part)
+        arr = (L.CompactSrc * n)()
+        keep = []
+        bufs = []
+        for k, src in enumerate(part):
+            seg = np.ascontiguousarray(src.data)
+            m = int(seg.size)
+            wcap, hcap, nrows = caps.get(k0 + k, (m + m // 8 + 4096, m // 16 + 4096, max(16, m // 12 + 16)))
+            wal = np.zeros(max(wcap, 1), dtype=np.uint8)
+            hb = np.zeros(max(hcap, 1), dtype=np.uint8)
+            offs = np.full(nrows, np.iinfo(np.uint64).max, dtype=np.uint64)
+            keep.append(seg)
+            bufs.append((wal, hb, offs))
+            arr[k].fid = src.fid
+            arr[k].data = seg.ctypes.data if m else None
+            arr[k].len = m
+            arr[k].start_off = src.start_off
+            arr[k].out = L.EncodeOut(wal.ctypes.data_as(L.u8p), wcap, hb.ctypes.data_as(L.u8p), hcap,
+                                     offs.ctypes.data_as(L.u64p), nrows)
+        p = L.EncodeParams(0, dst.base_time, dst.fid, dst.size(), hint.size(), 0, L.ENC_COMPACT, ns_size, etag_size)
+        res = (L.EncodeResult * n)()
+        filt = (L.IndexResult * n)()
+        done = C.c_uint64(0)
+        ctxs, n_ctx = _ctx_array(contexts)
+        rc = L.lib.bcw_compact_wals(index.handle, ctxs, n_ctx, arr, n, C.byref(p), res, filt, C.byref(done))
+        for k in range(int(done.value)):
+            r, (wal, hb, offs) = res[k], bufs[k]
+            dst.data += wal[:int(r.wal_need)].tobytes()
+            hint.data += hb[:int(r.hint_need)].tobytes()
+            out.append((offs[:int(r.n_in)].copy(), int(filt[k].n_done)))
+        if rc == L.E_CAPACITY:
+            k = int(done.value)
+            r, m = res[k], int(part[k].data.size)
+            wcap, hcap, nrows = caps.get(k0 + k, (m + m // 8 + 4096, m // 16 + 4096, max(16, m // 12 + 16)))
+            caps[k0 + k] = (max(wcap, int(r.wal_need)), max(hcap, int(r.hint_need)), max(nrows, int(r.n_in)))
+            k0 += k
+            continue
+        if rc != 0:
+            raise RuntimeError(f"bcw_compact_wals: {L.lib.bcw_strerror(rc).decode()}")
+        if done.value:
+            r = res[int(done.value) - 1]
+            src = part[int(done.value) - 1]
+            if r.err_class == L.ENC_ERR_SRC:
+                st = L.ST_OK
+                if r.err_record >= 0:
+                    dec = index.ctx.decode(src.data, src.start_off, src.base_time, ns_size, etag_size)
+                    st = int(dec.table["status"][r.err_record])
+                raise _src_error(r, r.src_err_class, st)
+            if r.err_class in _ENC_ERRORS:
+                raise _ENC_ERRORS[r.err_class]()
+        break
+    return out
 
 
 def compact_one_wal_filtered(dst: WalFile, hint: WalFile, src: Wal, index: Index, ns_size: int = 20,

@@ -410,6 +410,11 @@ int bcw_compact_filter_async(bcw_index* ix, const uint8_t* d_seg, const bcw_deco
  * entries_cap + 1 entries). Returns BCW_E_CAPACITY when too small (*n_out / *key_bytes tell the sizes). */
 int bcw_index_export(bcw_index* ix, uint8_t* h_keys, uint64_t keys_cap, uint64_t* h_key_off, uint64_t* h_fid,
                      uint64_t* h_off, uint64_t* h_size, uint64_t entries_cap, uint64_t* n_out, uint64_t* key_bytes);
+/* bcw_index_export restricted to the live entries whose value fid is one of h_fids[0, n_fids) (n_fids 0: all):
+ * the slice of the index that points into a set of WAL files (the compaction fan-out's filter snapshot). */
+int bcw_index_export_fids(bcw_index* ix, const uint64_t* h_fids, uint64_t n_fids, uint8_t* h_keys, uint64_t keys_cap,
+                          uint64_t* h_key_off, uint64_t* h_fid, uint64_t* h_off, uint64_t* h_size,
+                          uint64_t entries_cap, uint64_t* n_out, uint64_t* key_bytes);
 /* Synchronous compaction of one source WAL with the device filter: decode -> doFilter against the index
  * -> Record.Encode + WriteRecord + hint append (compaction.go:294-327 with doFilter compaction.go:329-348
  * and no user CompactionFilter), host in / host out like bcw_encode_segment. h_filter (may be NULL)
@@ -423,6 +428,66 @@ int bcw_compact_segment(bcw_ctx* ctx, bcw_index* ix, const uint8_t* h_src, const
  * by the data WAL of the same fid. ix must belong to ctx (BCW_E_INVAL otherwise). */
 int bcw_index_recover_segment(bcw_ctx* ctx, bcw_index* ix, const uint8_t* h_seg, const bcw_decode_params* p,
                               uint64_t fid, int use_record_fid, bcw_decode_result* h_dres, bcw_index_result* h_out);
+/* ---- one process, several devices: the fan-outs of a Go caller that drives several GPUs -------------------------
+ * Each takes n_ctx contexts (any devices, one host thread each) and the index; INTEGRATION.md shows the cgo loop.
+ * The puts into the index and the appends to the dst files keep the reference's order; only the decodes (and
+ * their uploads) run concurrently. */
+typedef struct bcw_recover_file {
+  uint64_t fid;
+  const uint8_t* wal;       /* the data WAL file */
+  bcw_decode_params wal_p;  /* BCW_MODE_RECORD */
+  const uint8_t* hint;      /* the hint WAL file, NULL when LoadWal of the hint failed (db_impl.go:288-291) */
+  bcw_decode_params hint_p; /* BCW_MODE_HINT */
+} bcw_recover_file;
+
+#define BCW_RECOVER_NOT_RUN 0
+#define BCW_RECOVER_HINT 1      /* the hint's puts (its iteration succeeded, or it stopped recovery) */
+#define BCW_RECOVER_HINT_WAL 2  /* the hint's puts, then the data WAL's (the hint iteration failed) */
+#define BCW_RECOVER_WAL 3       /* the data WAL's puts (no hint file) */
+typedef struct bcw_recover_status {
+  int32_t used; /* BCW_RECOVER_* */
+  int32_t rc;   /* BCW_OK or the error of this file's calls */
+  bcw_decode_result hint_dres, wal_dres;
+  bcw_index_result hint_ires, wal_ires;
+} bcw_recover_status;
+
+/* recoverFromWals (db_impl.go:268-314). Files (any order) are taken in ascending fid; the k-th goes to
+ * ctxs[k % n_ctx], whose thread decodes its hint (and its data WAL when the hint iteration fails) into a staging
+ * index of its own, concurrently with the other contexts. The staging index holds the file's last put per key:
+ * the index receives those, file by file, in ascending fid -- the state the reference's serial Put loop leaves.
+ * Recovery stops at the first file whose data WAL iteration fails (rejected row or fragment error), whose put
+ * failed (hint/wal_ires.err_class), whose hint decode gave up (BCW_ERR_INTERNAL) or whose calls failed (rc):
+ * that file's puts are applied (the reference returns its error after them), later files' are not.
+ * st (n_files entries, in files[] order) receives each file's outcome; *stop_file the files[] index of the
+ * stopping file, -1 when every file was applied. Returns BCW_OK, or an error of the index's own calls. */
+int bcw_recover_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const bcw_recover_file* files,
+                     uint64_t n_files, bcw_recover_status* st, int64_t* stop_file);
+
+typedef struct bcw_compact_src {
+  uint64_t fid;          /* the source WAL's fid (doFilter's srcFid) */
+  const uint8_t* data;   /* the source WAL file */
+  uint64_t len;
+  uint32_t start_off;    /* its super block startOff */
+  uint32_t _pad;
+  bcw_encode_out out;    /* this source's appended dst WAL bytes, hint bytes and offsets per row */
+} bcw_compact_src;
+
+/* doCompactionWork's loop (compaction.go:201-211) of compactOneWal with doFilter (compaction.go:294-348, no user
+ * CompactionFilter): the sources, in the given order, append to one dst WAL and one hint WAL. Source k goes to
+ * ctxs[k % n_ctx], whose thread uploads, decodes and filters it concurrently with the other contexts; the encodes
+ * run in source order, each starting where the previous one ended. The filter reads a snapshot of the index's
+ * entries that point into the sources' fids, taken when the call starts (bcw_index_export_fids): the same
+ * keep mask as a lookup in the index when no write lands in between (the reference's compaction races writes
+ * in the same window, compaction.go:181-200). dst: dst_base_time, fid, wal_pos, hint_pos, ns_size, etag_size
+ * (src_len, src_start_off and mode are per source / BCW_ENC_COMPACT). res / filt (n_src entries): each source's
+ * bcw_compact_segment outcome. *n_done: sources whose output is final -- the last one may carry an error
+ * (res.err_class != 0: the caller raises it, as doCompactionWork returns it after its appends). Returns
+ * BCW_E_CAPACITY when source *n_done's output did not fit its bcw_encode_out (res[*n_done] tells the sizes:
+ * resume from it with wal_pos = res[*n_done - 1].wal_end), else BCW_OK or an error of the calls. */
+int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const bcw_compact_src* srcs,
+                     uint64_t n_src, const bcw_encode_params* dst, bcw_encode_result* res, bcw_index_result* filt,
+                     uint64_t* n_done);
+
 /* IndexOperator.Hash (index.go:15-19): murmur3 (spaolacci/murmur3 v1.1.0) New64().Sum64() on the host */
 uint64_t bcw_murmur3_sum64(const uint8_t* p, uint64_t n);
 
