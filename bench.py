@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra legs (config C, all-core / pread CPU baselines, file-to-file end-to-end rates)")
+    ap.add_argument("--encode-records", type=int, default=10_000_000,
+                    help="records of the extra encode_e leg (BASELINE.json configs[4], config E: 10 M); 0 skips it")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the all-core CPU baseline")
     ap.add_argument("--inflight", type=int, default=2,
                     help="segments in flight for the extra pipelined leg: steps rotate over this many contexts "
@@ -283,6 +285,25 @@ def config_c_leg(L, Context, torch, dev, args, make_table, roof_name, kernel_nam
                     "warmup/steps as the headline, measured after it in the same process"}
 
 
+def encode_e_leg(args):
+    """BASELINE.json configs[4] (E): the compaction re-encode (compactOneWal: Record.Encode + WriteRecord + hint
+    append, every record kept) of --encode-records records of the config-E shape, device-resident; the same warmup
+    and steps as the headline, timed with HIP events on the codec's stream (tools/bench_encode.py measure); an
+    extra key, never `value`. Its parity: the dst WAL equals the source from byte 40 and the hint decodes back to the
+    returned offsets."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_encode  # noqa: E402
+    m = bench_encode.measure(args.encode_records, args.steps, args.warmup)
+    alg = m["src_bytes"] + m["wal_bytes"] + m["hint_bytes"]
+    wr = m["kernel_ms"].get("k_write")
+    return {"value": m["value"], "unit": m["unit"], "encode_ms": m["encode_ms"], "records": m["records"],
+            "src_bytes": m["src_bytes"], "steps": args.steps, "warmup": args.warmup,
+            "decode_plus_encode_ms": m["decode_plus_encode_ms"], "kernel_ms": m["kernel_ms"],
+            "writer_TBs": round(alg / (wr * 1e-3) / 1e12, 3) if wr else None, "parity": m["parity"],
+            "note": "writer_TBs: algorithmic bytes (src read + dst WAL + hint written) / the writer phase (k_wcopy + "
+                    "k_write + k_write_general + k_hwrite, one profiling slot named k_write)"}
+
+
 def main():
     args = parse()
     from bitcaskdb_amd import shard
@@ -514,6 +535,8 @@ def main():
     extras = {}
     if world == 1 and not args.no_extras and args.config == "B":
         extras["config_c"] = config_c_leg(L, Context, torch, dev, args, make_table, roof_name, names)
+    if world == 1 and not args.no_extras and args.config == "B" and args.encode_records > 0:
+        extras["encode_e"] = encode_e_leg(args)
     if world == 1 and not args.no_extras:
         extras["e2e"] = end_to_end(L, ctx, stream, host, d_seg, step, table, d_res, seg_len, n_rec)
 

@@ -204,7 +204,8 @@ constexpr uint32_t kSumHasE = 1u << 16;
 constexpr int kEqStride = 32;  // k_crc's per-XCD emission queue heads: 128 B apart
 
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no predecessor sum, 2 no table writes,
-// 16 phase cycles (chase, sum, writes; s_memtime) summed into misc[7..9]
+// 16 phase cycles (chase, sum, writes; s_memtime) summed into misc[7..9], 32 per-workgroup wall-clock stamps (entry,
+// chase end, sum end, end) into lbe[4 wg ..] (kbench passes a buffer of its own; direct-sum sizes only)
 template <int ABL = 0>
 __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
                                               uint64_t nblocks, uint32_t* __restrict__ fbase,
@@ -225,6 +226,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   __shared__ uint8_t s_type[kHold][64];
   const uint32_t lane = threadIdx.x;
   const uint64_t tc0 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
+  if ((ABL & 32) && threadIdx.x == 0) lbe[4 * blockIdx.x] = wall_clock64();
   // the workgroup id orders the look-back: workgroups are dispatched in id order (within each XCD), so one only waits
   // on ids already running; the bounded waits (Spin) turn any other schedule into BCW_ERR_INTERNAL, never a hang.
   // (Round 4 took tickets from one atomic counter: its 512 returning atomics on one word ended 5-7 us apart, and the
@@ -259,6 +261,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                    }
                                  });
   const uint64_t tc1 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
+  if ((ABL & 32) && lane == 0) lbe[4 * wg + 1] = wall_clock64();
   const uint32_t incl = wave_add_scan(n, lane);
   const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
   const uint32_t incl_e = wave_add_scan(ne, lane);
@@ -283,16 +286,31 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
       const uint64_t q = lane + 64u * k;
       v[k] = q < wg ? __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
     }
+    // the words not yet published are polled again all together (one round trip per poll, not one per word: polled
+    // one word at a time, the sum ended ~5 us after the last chase on B, kbench k_chase stamps)
+    Spin sp;  // bounded (BCW_ERR_INTERNAL)
+    if (force) sp.lim = 0;
+    for (;;) {
+      bool wait = force;
+#pragma unroll
+      for (int k = 0; k < kDirect / 64; ++k) wait |= (v[k] >> 40) != epoch;
+      if (!__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(wait) != 0ull))) break;
+      if (!sp.go(misc, 9)) {
+#pragma unroll
+        for (int k = 0; k < kDirect / 64; ++k)
+          if ((v[k] >> 40) != epoch) v[k] = 0;
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < kDirect / 64; ++k) {
+        const uint64_t q = lane + 64u * k;
+        if ((v[k] >> 40) != epoch) v[k] = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     uint64_t c = 0, ce = 0;
 #pragma unroll
     for (int k = 0; k < kDirect / 64; ++k) {
       const uint64_t q = lane + 64u * k;
-      Spin sp;  // bounded (BCW_ERR_INTERNAL)
-      if (force) sp.lim = 0;
-      while (force || (v[k] >> 40) != epoch) {
-        if (!sp.go(misc, 9)) { v[k] = 0; break; }
-        v[k] = __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
       if (q < wg) {
         c += v[k] & 0x7ffffu;
         ce += (v[k] >> 19) & 0x7ffffu;
@@ -350,6 +368,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   }
   const uint64_t g0 = excl + incl - n;
   const uint64_t tc2 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
+  if ((ABL & 32) && lane == 0) lbe[4 * wg + 2] = wall_clock64();
   if (b < nblocks && !(ABL & 2)) {
     fbase[b] = (uint32_t)(g0 < 0xffffffffull ? g0 : 0xffffffffull);
     const uint64_t r0 = excl_e + incl_e - ne;
@@ -384,6 +403,10 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
         put_frag(frags, srec, g0 + k, frag_cap, (uint32_t)b, boff, start, len, crc, type, initc,
                  adj(k, start | (len << 16)));
       }, hres, (uint32_t)kHold);
+  }
+  if (ABL & 32) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) lbe[4 * wg + 3] = wall_clock64();
   }
   if (ABL & 16) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1269,13 +1292,14 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     }
     n_items += taken;
   };
+  if (ABL & 64) emit_items(~0ull);  // (kbench: emission before the stream)
   if (!(ABL & 32768))
     stream_verify<(ABL & 8388608) != 0>(seg, seg_len, fok, srec, f0, nfr, lds, lane, misc, s_rem,
                                         (wave & 3u) * 4u + (wave >> 2),
                                         reinterpret_cast<const uint8_t*>(tabs.lds_image2));
   __builtin_amdgcn_s_setprio(0);
   const uint64_t t_crc = ea.kb_stamps ? wall_clock64() : 0;
-  emit_items(~0ull);
+  if (!(ABL & 64)) emit_items(~0ull);
   asm volatile("" ::: "memory");  // (reload the tail arguments from LDS, see CrcTail)
   CrcTail T;
   {  // wave-uniform: into SGPRs

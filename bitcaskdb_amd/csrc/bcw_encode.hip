@@ -1408,6 +1408,7 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_re
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
 }
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 constexpr int kCU = 2;  // units per lane in flight (8 waves per SIMD: the wave count hides the latency; 4: 35.9 ms)
 
 
@@ -1444,11 +1445,9 @@ __device__ __forceinline__ void copy_run(uint8_t* dst, const uint8_t* src, uint6
       if (k >= nu) continue;
       const uint64_t ua = (u0 + k) << 4;
       uint8_t* d = dst + (int64_t)(ua - da);
-      if (ok[q] && ua >= da && ua + 16 <= de) {
-        __builtin_nontemporal_store(v[q].x, reinterpret_cast<uint32_t*>(d));
-        __builtin_nontemporal_store(v[q].y, reinterpret_cast<uint32_t*>(d) + 1);
-        __builtin_nontemporal_store(v[q].z, reinterpret_cast<uint32_t*>(d) + 2);
-        __builtin_nontemporal_store(v[q].w, reinterpret_cast<uint32_t*>(d) + 3);
+      if (ok[q] && ua >= da && ua + 16 <= de) {  // one 16 B non-temporal store (d is 16 B aligned)
+        const v4u w = {v[q].x, v[q].y, v[q].z, v[q].w};
+        __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(d));
       } else {
         const uint32_t b0 = ua < da ? (uint32_t)(da - ua) : 0u, b1 = ua + 16 > de ? (uint32_t)(de - ua) : 16u;
         if (ok[q]) {

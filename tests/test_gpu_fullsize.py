@@ -99,11 +99,9 @@ def test_config_e_compaction_200k(ctx):
 
 @pytest.fixture
 def lookback_ctx():
-    """a context on the two-launch path whose k_chase takes the decoupled look-back at every size
-    (BCW_OPT_DECODE_PATH 1, BCW_OPT_CHASE_DIRECT 0)"""
+    """a context whose k_chase takes the decoupled look-back at every size (BCW_OPT_CHASE_DIRECT 0)"""
     from bitcaskdb_amd import Context
     c = Context(0)
-    c.set_option(L.OPT_DECODE_PATH, 1)
     c.set_option(L.OPT_CHASE_DIRECT, 0)
     yield c
     c.close()

@@ -18,6 +18,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 BASE_TIME = 1_700_000_000
@@ -140,21 +142,36 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="skip the index rebuild / compaction filter leg")
     args = ap.parse_args()
+    line = measure(args.records, args.steps, args.warmup, with_index=not args.no_index)
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    s = json.dumps(line)
+    print(s, flush=True)
+    if args.out:
+        with open(args.out, "w") as fh:
+            fh.write(s + "\n")
+    if not (line["parity"]["wal_equals_source"] and line["parity"]["hint_decodes_to_offsets"]):
+        raise SystemExit("config E parity check failed")
+
+
+def measure(records: int, steps: int, warmup: int, with_index: bool = False) -> dict:
+    """the config-E encode of `records` records (synthesised on the host, uploaded once): warmup untimed encodes,
+    then `steps` timed ones (HIP events on the codec's stream); also used by bench.py's encode_e key"""
     import torch
     from bitcaskdb_amd import _lib as L
     from bitcaskdb_amd import Context
 
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", torch.cuda.current_device())
     t0 = time.time()
     n, r = C.c_uint64(), C.c_uint64()
-    assert L.lib.bcw_synth_segment(1 << 62, args.records, 42, 20, 100, 4096, 0, BASE_TIME, None, 0, C.byref(n),
+    assert L.lib.bcw_synth_segment(1 << 62, records, 42, 20, 100, 4096, 0, BASE_TIME, None, 0, C.byref(n),
                                    C.byref(r)) == 0
-    host = torch.empty(n.value, dtype=torch.uint8).pin_memory()
-    assert L.lib.bcw_synth_segment(1 << 62, args.records, 42, 20, 100, 4096, 0, BASE_TIME,
-                                   C.c_void_p(host.data_ptr()), n.value, C.byref(n), C.byref(r)) == 0
+    host = np.empty(n.value, dtype=np.uint8)  # (pageable: pinning 42 GB costs more than the copy it saves)
+    assert L.lib.bcw_synth_segment(1 << 62, records, 42, 20, 100, 4096, 0, BASE_TIME,
+                                   C.c_void_p(host.ctypes.data), n.value, C.byref(n), C.byref(r)) == 0
     seg_len, n_rec = int(n.value), int(r.value)
     print(f"synth {seg_len} B, {n_rec} records in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
-    d_src = host.to(dev, non_blocking=True)
+    d_src = torch.from_numpy(host).to(dev)
     torch.cuda.synchronize()
     del host
 
@@ -206,7 +223,7 @@ def main():
                                               C.c_void_p(d_eres.data_ptr())) == 0
 
     decode_checked(d_src.data_ptr(), dparams)
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         encode()
     torch.cuda.synchronize()
     res = L.EncodeResult.from_buffer_copy(bytes(d_eres.cpu().numpy()))
@@ -249,11 +266,11 @@ def main():
     L.lib.bcw_ctx_kernel_times(ctx.handle, None, None, nk)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
-    for _ in range(args.steps):
+    for _ in range(steps):
         encode()
     e1.record(stream)
     torch.cuda.synchronize()
-    enc_ms = e0.elapsed_time(e1) / args.steps
+    enc_ms = e0.elapsed_time(e1) / steps
     tot = (C.c_double * nk)()
     cnt = (C.c_uint64 * nk)()
     L.lib.bcw_ctx_kernel_times(ctx.handle, tot, cnt, nk)
@@ -261,12 +278,12 @@ def main():
     # decode + encode (a whole compactOneWal of the segment)
     L.lib.bcw_ctx_set_profiling(ctx.handle, 0)
     e0.record(stream)
-    for _ in range(args.steps):
+    for _ in range(steps):
         decode()
         encode()
     e1.record(stream)
     torch.cuda.synchronize()
-    both_ms = e0.elapsed_time(e1) / args.steps
+    both_ms = e0.elapsed_time(e1) / steps
     alg = seg_len + wal_bytes + hint_bytes  # source read once + both outputs written
     pack_ms = kern.get("k_write", 0)
     line = {
@@ -280,18 +297,11 @@ def main():
         "layout_events": {"wal": int(res.wal_events), "hint": int(res.hint_events)},
         "parity": {"wal_equals_source": same, "hint_decodes_to_offsets": hint_ok},
     }
-    if not args.no_index:
-        line["index"] = index_leg(L, ctx, stream, d_src, dparams, table, d_res, n_rec, args.steps, decode_checked,
+    if with_index:
+        line["index"] = index_leg(L, ctx, stream, d_src, dparams, table, d_res, n_rec, steps, decode_checked,
                                   encode, keep)
-    if not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-    s = json.dumps(line)
-    print(s, flush=True)
-    if args.out:
-        with open(args.out, "w") as fh:
-            fh.write(s + "\n")
-    if not (same and hint_ok):
-        raise SystemExit("config E parity check failed")
+    ctx.close()
+    return line
 
 
 if __name__ == "__main__":

@@ -274,6 +274,7 @@ int main(int argc, char** argv) {
   auto runv = [&](int v) -> float {
     switch (v) {
       case 8: return run(k_crc<8>, cus, ea);              // no emission
+      case 64: return run(k_crc<64>, cus, ea);            // emission before the stream
       case 8388608: return run(k_crc<8388608>, cus, ea);  // every chunk on the fast chain
       case 8388616: return run(k_crc<8388616>, cus, ea);  // the same without emission
       case 32768: return run(k_crc<32768>, cus, ea);      // emission only (no CRC pass)
@@ -454,6 +455,39 @@ int main(int argc, char** argv) {
       const float p0 = timeit([&] { k_chase_probe<0><<<pg, 64, 0, st>>>(d, n, 40, nblocks, pout); }, reps, st);
       const float p1 = timeit([&] { k_chase_probe<1><<<pg, 64, 0, st>>>(d, n, 40, nblocks, pout); }, reps, st);
       printf("chase probe: chase_block with a count-only visit %.4f ms, plain one-header chain %.4f ms\n", p0, p1);
+    }
+    {  // per-workgroup wall-clock stamps (entry, chase end, sum end, end) of one launch, relative to the first entry
+      const uint64_t nwg = (nblocks + 63) / 64;
+      uint64_t* stp;
+      CK(hipMalloc(&stp, nwg * 32));
+      for (int rep = 0; rep < 3; ++rep) {
+        k_chase<32><<<(uint32_t)nwg, 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags, s.srec, s.frag_cap,
+                                                  s.lb, stp, s.misc, s.epoch, ctx->tabs.initc, s.chase_direct, s.equeue,
+                                                  0ull);
+        ++s.epoch;
+        CK(hipStreamSynchronize(st));
+      }
+      std::vector<uint64_t> h4(nwg * 4);
+      CK(hipMemcpy(h4.data(), stp, nwg * 32, hipMemcpyDeviceToHost));
+      uint64_t t0 = ~0ull;
+      for (uint64_t w = 0; w < nwg; ++w) t0 = std::min(t0, h4[4 * w]);
+      std::vector<double> col[4];
+      for (uint64_t w = 0; w < nwg; ++w)
+        for (int k = 0; k < 4; ++k) col[k].push_back((h4[4 * w + k] - t0) / 100.0);
+      const char* nm[4] = {"entry", "chase end", "sum end", "end"};
+      for (int k = 0; k < 4; ++k) {
+        std::vector<double> c = col[k];
+        std::sort(c.begin(), c.end());
+        printf("  k_chase stamps %-9s us: min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f\n", nm[k], c[0], c[c.size() / 10],
+               c[c.size() / 2], c[c.size() * 9 / 10], c.back());
+      }
+      // entry by workgroup id (dispatch order), every 32nd
+      printf("  k_chase entry by wg (every 32nd):");
+      for (uint64_t w = 0; w < nwg; w += 32) printf(" %.2f", col[0][w]);
+      printf("\n  k_chase chase end by wg (every 32nd):");
+      for (uint64_t w = 0; w < nwg; w += 32) printf(" %.2f", col[1][w]);
+      printf("\n");
+      CK(hipFree(stp));
     }
     CK(hipMemset(&s.misc[7], 0, 24));
     crun(k_chase<16>);
