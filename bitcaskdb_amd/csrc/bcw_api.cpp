@@ -441,6 +441,7 @@ int bcw_decode_segment_async(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_
       !t->emit_frag || !t->hdr_size || !t->flags || !t->etag_off || !t->status)
     return BCW_E_INVAL;
   if (p->mode == BCW_MODE_HINT && (!t->aux0 || !t->aux1)) return BCW_E_INVAL;
+  if (p->seg_len > BCW_MAX_SEGMENT) return BCW_E_INVAL;  // k_crc's item arithmetic is 32-bit (< 2^24 blocks)
   DeviceGuard dg(c->device);
   if (!dg.ok) return BCW_E_HIP;
   c->last_start_off = p->start_off;

@@ -174,11 +174,11 @@ __device__ __forceinline__ uint32_t chase_block(const uint8_t* __restrict__ seg,
 // 29-31: K, the fragment's J ends in word K of lane Lfull's piece (0 or 4: no lane is split), as stream_verify's
 // close derives them from pb.
 constexpr uint32_t kRecUsual = 1u << 20, kRecAdj = 1u << 21;
-__device__ __forceinline__ void put_frag_ic(Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t g,
-                                            uint64_t frag_cap, uint32_t b, uint64_t boff, uint32_t start_len,
-                                            uint32_t crc, uint32_t type, uint32_t ic, bool adj) {
+__device__ __forceinline__ uint32_t check_word(uint32_t crc, uint32_t ic) { return ~rotl32(crc - 0xa282ead8u, 15) ^ ic; }
+__device__ __forceinline__ void put_frag_J(Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t g,
+                                           uint64_t frag_cap, uint32_t b, uint64_t boff, uint32_t start_len,
+                                           uint32_t J, uint32_t type, bool adj) {
   if (g >= frag_cap) return;
-  const uint32_t J = ~rotl32(crc - 0xa282ead8u, 15) ^ ic;
   *reinterpret_cast<uint4*>(frags + g) = make_uint4(b, start_len, J, type & 0xffu);
   const uint64_t gs = boff + (start_len & 0xffffu), ge = gs + (start_len >> 16);
   const uint32_t cb = (uint32_t)(gs / kSChunk), ce = (uint32_t)(ge / kSChunk);
@@ -191,7 +191,7 @@ __device__ __forceinline__ void put_frag_ic(Frag* __restrict__ frags, uint4* __r
 __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t g,
                                          uint64_t frag_cap, uint32_t b, uint64_t boff, uint32_t start, uint32_t len,
                                          uint32_t crc, uint32_t type, const uint32_t* __restrict__ initc, bool adj) {
-  put_frag_ic(frags, srec, g, frag_cap, b, boff, start | (len << 16), crc, type, initc[len], adj);
+  put_frag_J(frags, srec, g, frag_cap, b, boff, start | (len << 16), check_word(crc, initc[len]), type, adj);
 }
 
 // Block summary for the record state machine (wal_iterator.go:69-96), written by k_chase from the headers alone:
@@ -275,7 +275,24 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   const uint64_t nwg_all = (nblocks + 63) / 64;
   const bool force = wg + 1 == test_abort_wg;  // BCW_OPT_TEST_ABORT_WAIT (wave-uniform)
   uint64_t excl = 0, excl_e = 0;
+  const uint32_t nh = n < (uint32_t)kHold ? n : (uint32_t)kHold;
+  // the held headers' check words J (their initc[len] loads issued 16 at a time), computed while the predecessors'
+  // counts are awaited: only the stores are left for after the sum (s_hold[k][0] holds J from here on)
+  auto held_checks = [&]() {
+    if (ABL & 2) return;
+    constexpr uint32_t kWb = 16;
+    static_assert(kHold % kWb == 0, "held-header batches stay inside s_hold");
+    for (uint32_t k0 = 0; k0 < nh; k0 += kWb) {
+      uint32_t ic[kWb];
+#pragma unroll
+      for (uint32_t q = 0; q < kWb; ++q) ic[q] = initc[k0 + q < nh ? s_hold[k0 + q][1][lane] >> 16 : 0u];
+#pragma unroll
+      for (uint32_t q = 0; q < kWb; ++q)
+        if (k0 + q < nh) s_hold[k0 + q][0][lane] = check_word(s_hold[k0 + q][0][lane], ic[q]);
+    }
+  };
   if (ABL & 1) {
+    held_checks();
   } else if (nwg_all <= (uint64_t)direct_max) {  // direct_max <= kDirect (bcw_ctx_set_option)
     if (lane == 0)
       __hip_atomic_store(&lb[wg], tag | (kLbAgg << 38) | tot | ((uint64_t)tot_e << 19), __ATOMIC_RELAXED,
@@ -286,6 +303,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
       const uint64_t q = lane + 64u * k;
       v[k] = q < wg ? __hip_atomic_load(&lb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
     }
+    held_checks();
     // the words not yet published are polled again all together (one round trip per poll, not one per word: polled
     // one word at a time, the sum ended ~5 us after the last chase on B, kbench k_chase stamps)
     Spin sp;  // bounded (BCW_ERR_INTERNAL)
@@ -329,6 +347,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
       __hip_atomic_store(&lb[wg], tag | fl | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&lbe[wg], tag | fl | tot_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    held_checks();
     // both counts walk back together; each stops at its own nearest inclusive prefix (the two words of a
     // predecessor turn inclusive one after the other)
     bool dn = false, de = false;
@@ -376,27 +395,15 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     bsum[b] = make_uint2(tacc | (tnz << 16), tst | (ne ? kSumHasE : 0u));
     if (badk != 0xffffffffu)  // the first unknown-type fragment of the segment (reset by the previous finalize)
       atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_TYPE]), (unsigned long long)(g0 + badk));
-    // the held headers' entries, kWb at a time: their initc[len] loads are issued together (one at a time, each
-    // entry waited one L2 round trip for its load: config C k_chase's table writes took ~17 us of its ~70). The
-    // block's last fragment is adjacent to the next block's first when it ends exactly at this full block's end and
-    // the next block holds a header.
+    // the held headers' entries (their J computed during the wait, held_checks). The block's last fragment is
+    // adjacent to the next block's first when it ends exactly at this full block's end and the next block holds a
+    // header.
     const bool next_hdr = b + 1 < nblocks && seg_len - (boff + kBlock) >= kHdr;
     auto adj = [&](uint32_t k, uint32_t sl_k) { return k + 1u < n || (next_hdr && (sl_k & 0xffffu) + (sl_k >> 16) == kBlock); };
-    const uint32_t nh = n < (uint32_t)kHold ? n : (uint32_t)kHold;
-    constexpr uint32_t kWb = 16;
-    static_assert(kHold % kWb == 0, "held-header batches stay inside s_hold");
-    for (uint32_t k0 = 0; k0 < nh; k0 += kWb) {
-      uint32_t sl[kWb], ic[kWb];
-#pragma unroll
-      for (uint32_t q = 0; q < kWb; ++q) {
-        sl[q] = s_hold[k0 + q][1][lane];
-        ic[q] = initc[k0 + q < nh ? sl[q] >> 16 : 0u];
-      }
-#pragma unroll
-      for (uint32_t q = 0; q < kWb; ++q)
-        if (k0 + q < nh)
-          put_frag_ic(frags, srec, g0 + k0 + q, frag_cap, (uint32_t)b, boff, sl[q], s_hold[k0 + q][0][lane],
-                      s_type[k0 + q][lane], ic[q], adj(k0 + q, sl[q]));
+    for (uint32_t k = 0; k < nh; ++k) {
+      const uint32_t sl = s_hold[k][1][lane];
+      put_frag_J(frags, srec, g0 + k, frag_cap, (uint32_t)b, boff, sl, s_hold[k][0][lane], s_type[k][lane],
+                 adj(k, sl));
     }
     if (n > (uint32_t)kHold)  // the tail of a block with more headers than held, chased again from the first of them
       chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
@@ -767,6 +774,11 @@ struct ItemMeta {
   uint2 s;  // emit_prefetch of block bb
   uint32_t f0, f1, rec;
 };
+// a wave-uniform load of a table k_chase wrote (read-only in k_crc) through the constant address space: a scalar
+// load, although the table pointer was reloaded from LDS (as a generic pointer it was a flat load from a VGPR address)
+__device__ __forceinline__ uint32_t ld_const(const uint32_t* p, uint64_t i) {
+  return ((const __attribute__((address_space(4))) uint32_t*)p)[i];
+}
 // item `it` of a chunk [cb0, cb1) of the segment's blocks: blocks [cb0 + it bpw, + bpw), cut at cb1
 __device__ __forceinline__ ItemMeta item_meta(const EmitArgs& A, uint64_t it, uint64_t bpw, uint64_t cb0, uint64_t cb1,
                                               uint32_t lane) {
@@ -774,9 +786,9 @@ __device__ __forceinline__ ItemMeta item_meta(const EmitArgs& A, uint64_t it, ui
   m.bb = cb0 + it * bpw < cb1 ? cb0 + it * bpw : cb1 - 1;  // a clamped (unconditional) load for an exhausted queue
   const uint64_t be = m.bb + bpw < cb1 ? m.bb + bpw : cb1;
   m.s = emit_prefetch(A, m.bb, lane);
-  m.f0 = A.fbase[m.bb];
-  m.f1 = A.fbase[be];
-  m.rec = A.rbase[m.bb];
+  m.f0 = ld_const(A.fbase, m.bb);
+  m.f1 = ld_const(A.fbase, be);
+  m.rec = ld_const(A.rbase, m.bb);
   return m;
 }
 
@@ -1257,15 +1269,20 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
         __builtin_amdgcn_readfirstlane(
             (uint32_t)__hip_atomic_load(&T.misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u)
       return;
-    const uint64_t cb0t = T.cb0, cb1t = T.cb1, cnt = cb1t - cb0t, fcap = T.frag_cap;
-    // blocks per item for ~64 fragments each
+    const uint64_t cb0t = T.cb0, cb1t = T.cb1, fcap = T.frag_cap;
+    // blocks per item for ~64 fragments each, and this workgroup's items. 32-bit arithmetic: a segment in HBM has
+    // fewer than 2^24 blocks (512 GiB; bcw_decode_segment_async refuses more), and the 64-bit divisions' VGPR
+    // temporaries were spilled to scratch across the item loop.
+    const uint32_t cnt = (uint32_t)(cb1t - cb0t), G = gridDim.x, wg = blockIdx.x;
     const uint64_t fc0 = A.fbase[cb0t], fc1 = A.fbase[cb1t];
-    const uint64_t nf_all = fc1 > fc0 ? (fc1 - fc0 < fcap ? fc1 - fc0 : fcap) : 0;
-    uint64_t bpw = nf_all ? (64 * cnt) / nf_all : cnt;
-    if (bpw < 1) bpw = 1;
-    const uint64_t B0 = cnt * ((uint64_t)blockIdx.x * kCrcWaves) / nw;  // chunk-relative
-    const uint64_t B1 = cnt * ((uint64_t)(blockIdx.x + 1) * kCrcWaves) / nw;
-    const uint64_t i0 = (B0 + bpw - 1) / bpw, nitems = (B1 + bpw - 1) / bpw;
+    const uint32_t nf_all = (uint32_t)(fc1 > fc0 ? (fc1 - fc0 < fcap ? fc1 - fc0 : fcap) : 0);
+    uint32_t bpw = nf_all ? (64u * cnt) / nf_all : cnt;
+    if (bpw < 1u) bpw = 1u;
+    bpw = __builtin_amdgcn_readfirstlane(bpw);  // (uniform values the division left in VGPRs: into SGPRs)
+    const uint32_t cq = cnt / G, cr = cnt % G;  // B(w) = cnt * w / G without a 64-bit product
+    const uint32_t B0 = cq * wg + (cr * wg) / G, B1 = cq * (wg + 1u) + (cr * (wg + 1u)) / G;  // chunk-relative
+    const uint64_t i0 = __builtin_amdgcn_readfirstlane((B0 + bpw - 1u) / bpw),
+                   nitems = __builtin_amdgcn_readfirstlane((B1 + bpw - 1u) / bpw);
     auto deq = [&]() -> uint64_t {
       uint32_t j = 0;
       if (lane == 0) j = atomicAdd(&s_eq, 1u);
@@ -1298,7 +1315,12 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
                                         (wave & 3u) * 4u + (wave >> 2),
                                         reinterpret_cast<const uint8_t*>(tabs.lds_image2));
   __builtin_amdgcn_s_setprio(0);
-  const uint64_t t_crc = ea.kb_stamps ? wall_clock64() : 0;
+  if (ea.kb_stamps && lane == 0) {  // (kbench: this wave's CRC end and fragments, written now so that nothing of it
+                                   // stays live across the emission)
+    uint64_t* q = ea.kb_stamps + 8 * gw;
+    q[0] = wall_clock64();
+    q[3] = nfr;
+  }
   if (!(ABL & 64)) emit_items(~0ull);
   asm volatile("" ::: "memory");  // (reload the tail arguments from LDS, see CrcTail)
   CrcTail T;
@@ -1310,8 +1332,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   }
   const EmitArgs& A = T.ea;
   if (A.kb_stamps && lane == 0) {
-    uint64_t* q = A.kb_stamps + 8 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
-    q[0] = t_crc; q[1] = wall_clock64(); q[2] = n_items; q[3] = nfr;
+    uint64_t* q = A.kb_stamps + 8 * ((uint64_t)__builtin_amdgcn_workgroup_id_x() * kCrcWaves + wave);
+    q[1] = wall_clock64(); q[2] = n_items;
     q[6] = __builtin_amdgcn_s_memtime();
   }
   // ---- completion: each wave's stores and atomics are done (vmcnt(0)) before it counts itself done in LDS;

@@ -204,6 +204,9 @@ const char* bcw_kernel_name(int kernel_id);
 #define BCW_OPT_DECODE_CHUNKS 3
 #define BCW_OPT_TEST_ABORT_WAIT 4
 #define BCW_CHASE_DIRECT_MAX 1024
+/* the largest segment a decode accepts (2^24 blocks of 32 KiB: 512 GiB, beyond one MI355X's 288 GB of HBM);
+ * bcw_decode_segment(_async) returns BCW_E_INVAL above it */
+#define BCW_MAX_SEGMENT (1ull << 39)
 int bcw_ctx_set_option(bcw_ctx* ctx, int option, uint64_t value);
 /* Size the context's fragment scratch for at least n fragments on the next decode (after a decode
  * reported retry_frag_capacity). n must be < 2^32 - 16 (BCW_E_INVAL otherwise, nothing stored). */
