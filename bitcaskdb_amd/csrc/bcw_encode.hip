@@ -1409,12 +1409,12 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
 }
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-constexpr int kCU = 2;  // units per lane in flight (8 waves per SIMD: the wave count hides the latency; 4: 35.9 ms)
+constexpr int kCU = 2;  // units per lane in flight (k_wcopy: 74 VGPRs, 6 waves per SIMD; 1, 3 and 4 measured equal)
 
 
-// copy m bytes from src to dst (global pointers, any alignment), one wave. Every unit (16 B aligned to
-// the output) takes its source bytes from two aligned 16 B loads; partial units at the run's ends
-// store only their bytes, from registers.
+// copy m bytes from src to dst (global pointers, any alignment), one wave. Every whole unit (16 B aligned to
+// the output) takes its source bytes from two aligned 16 B loads; the partial units at the run's ends are written
+// bytewise, one byte per lane, after the loop.
 __device__ __forceinline__ void copy_run(uint8_t* dst, const uint8_t* src, uint64_t m, const uint8_t* seg,
                                          uint64_t seg_len, uint32_t lane) {
   if (m == 0) return;
@@ -1445,18 +1445,24 @@ __device__ __forceinline__ void copy_run(uint8_t* dst, const uint8_t* src, uint6
       if (k >= nu) continue;
       const uint64_t ua = (u0 + k) << 4;
       uint8_t* d = dst + (int64_t)(ua - da);
-      if (ok[q] && ua >= da && ua + 16 <= de) {  // one 16 B non-temporal store (d is 16 B aligned)
+      if (ua < da || ua + 16 > de) continue;  // a partial unit at the run's ends: below, one byte per lane
+      if (ok[q]) {  // one 16 B non-temporal store (d is 16 B aligned)
         const v4u w = {v[q].x, v[q].y, v[q].z, v[q].w};
         __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(d));
-      } else {
-        const uint32_t b0 = ua < da ? (uint32_t)(da - ua) : 0u, b1 = ua + 16 > de ? (uint32_t)(de - ua) : 16u;
-        if (ok[q]) {
-          for (uint32_t b = b0; b < b1; ++b) d[b] = (uint8_t)sel_byte(v[q], b);
-        } else {  // the source window touches the segment's ends: bytewise
-          for (uint32_t b = b0; b < b1; ++b) d[b] = seg[(int64_t)(ua + b + delta - sbeg)];
-        }
+      } else {  // the source window touches the segment's ends: bytewise
+        for (uint32_t b = 0; b < 16u; ++b) d[b] = seg[(int64_t)(ua + b + delta - sbeg)];
       }
     }
+  }
+  // the bytes of the partial units at the run's two ends (at most 15 + 15), one per lane: lanes [0, n0) the first
+  // unit's from the run's start, lanes [n0, n0 + n1) the last unit's up to its end (as a byte loop per end lane these
+  // took ~2.4 of the writer phase's ~25 ms at config E: up to 15 dependent iterations for two lanes)
+  const uint64_t ulast = (de - 1) & ~15ull;
+  const uint32_t n0 = (da & 15u) ? (uint32_t)(min(de, (da & ~15ull) + 16) - da) : 0u;
+  const uint32_t n1 = ((de & 15u) && ulast >= da + n0) ? (uint32_t)(de - ulast) : 0u;
+  if (lane < n0 + n1) {
+    const uint64_t off = lane < n0 ? lane : (ulast - da) + (lane - n0);  // run-relative byte
+    dst[off] = seg[(int64_t)(da + off + delta - sbeg)];
   }
 }
 
