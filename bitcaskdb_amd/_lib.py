@@ -101,7 +101,8 @@ class CompactSrc(C.Structure):
 
 class IndexInfo(C.Structure):
     _fields_ = [("live", C.c_uint64), ("slots_used", C.c_uint64), ("slot_capacity", C.c_uint64),
-                ("arena_used", C.c_uint64), ("arena_capacity", C.c_uint64), ("overflow", C.c_uint64)]
+                ("arena_used", C.c_uint64), ("arena_capacity", C.c_uint64), ("overflow", C.c_uint64),
+                ("limited", C.c_uint64), ("evicted", C.c_uint64), ("evicted_bytes", C.c_uint64)]
 
 
 # the table's column names, C types and numpy dtypes (one place, used by wal.py and bench.py)
@@ -173,6 +174,7 @@ def _load():
         "bcw_index_destroy": (C.c_int, [vp]),
         "bcw_index_reserve": (C.c_int, [vp, C.c_uint64, C.c_uint64]),
         "bcw_index_stats": (C.c_int, [vp, C.POINTER(IndexInfo)]),
+        "bcw_index_set_limit": (C.c_int, [vp, C.c_uint64]),
         "bcw_index_apply": (C.c_int, [vp, C.c_uint64, vp, u64p, u8p, u64p, u64p, u64p]),
         "bcw_index_apply_stat": (C.c_int, [vp, C.c_uint64, vp, u64p, u8p, u64p, u64p, u64p, u8p, u64p, u64p]),
         "bcw_index_clear": (C.c_int, [vp]),

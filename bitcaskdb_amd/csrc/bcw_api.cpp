@@ -310,6 +310,11 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
       }
       put_bytes(kS2Gap + 4 * g, b);
     }
+    for (int m = 0; m < kS2XrN; ++m) {  // XR[m]: 0xff at [m - 3, m + 1), none at the last entry
+      uint8_t b[16];
+      for (int q = 0; q < 16; ++q) b[q] = (m < kS2XrN - 1 && q >= m - 3 && q < m + 1) ? 0xff : 0x00;
+      put_bytes(kS2Xr + 4 * m, b);
+    }
   }
   bool ok = hipMalloc(&c->tabs.lds_image2, image2.size() * 4) == hipSuccess &&
             hipMemcpy(c->tabs.lds_image2, image2.data(), image2.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
@@ -337,7 +342,6 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.srec);
   (void)hipFree(s.fok);
   (void)hipFree(s.misc);
-  (void)hipFree(s.equeue);
   s = Scratch{};
 }
 
@@ -411,13 +415,14 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
             hipMalloc(&s.lbe, nwg * 8) == hipSuccess && hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
             hipMalloc(&s.srec, (fc + 4) * sizeof(uint4)) == hipSuccess &&
             hipMalloc(&s.fok, fc) == hipSuccess &&
-            hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess && hipMalloc(&s.equeue, 8 * 128) == hipSuccess;
+            hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;
   s.frag_cap = fc;
   s.nlb = nwg;
   s.epoch = 1;
   s.chase_direct = c->chase_direct;
+  s.decode_path = c->decode_path;
   // on the codec's stream: a null-stream hipMemset is not ordered before kernels on a non-blocking
   // stream, and a look-back word zeroed after k_chase published it would never be seen again
   // misc[15] (the first unknown-type fragment, an atomicMin in k_chase) starts at UINT64_MAX; every decode's
@@ -509,8 +514,12 @@ int bcw_ctx_set_option(bcw_ctx* c, int option, uint64_t value) {
       c->s.chase_direct = (uint32_t)value;
       c->chase_direct = (uint32_t)value;
       return BCW_OK;
-    case BCW_OPT_DECODE_PATH:    // retired options (bcw.h): only their one remaining value is accepted
-    case BCW_OPT_DECODE_CHUNKS:
+    case BCW_OPT_DECODE_PATH:  // 2: one launch (k_decode, the default), 1: two launches (k_chase + k_crc)
+      if (value != 1 && value != 2) return BCW_E_INVAL;
+      c->s.decode_path = (uint32_t)value;
+      c->decode_path = (uint32_t)value;
+      return BCW_OK;
+    case BCW_OPT_DECODE_CHUNKS:  // retired (bcw.h): only its one remaining value is accepted
       return value == 1 ? BCW_OK : BCW_E_INVAL;
     case BCW_OPT_TEST_ABORT_WAIT: {  // fault injection: refused unless the process opted in (BCW_TEST_HOOKS=1)
       const char* hooks = getenv("BCW_TEST_HOOKS");
@@ -782,8 +791,8 @@ bcw_decode_params src_params(const uint8_t* h_src, const bcw_encode_params* p) {
 }
 
 // the encode of the context's decoded source with the context's keep mask, outputs copied to the host
-int encode_to_host(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out* h, bcw_encode_result* h_result,
-                   const bcw_decode_result& dres) {
+int encode_run(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out* h, bcw_encode_result* h_result,
+               bcw_encode_out* d_out) {
   const uint64_t rows = c->d_tab.capacity;
   const uint64_t need = h->wal_cap + h->hint_cap + rows * 8;
   if (need > c->d_eout_cap) {
@@ -795,8 +804,10 @@ int encode_to_host(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out*
     c->d_eout_cap = need;
   }
   uint8_t* m = (uint8_t*)c->d_eout;
-  bcw_encode_out d{};
+  bcw_encode_out& d = *d_out;
+  d = bcw_encode_out{};
   d.rec_off = (uint64_t*)m;
+  d.rec_off_cap = rows;
   m += rows * 8;
   d.wal = m;
   d.wal_cap = h->wal_cap;
@@ -810,17 +821,28 @@ int encode_to_host(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out*
   HIPCHK(hipStreamSynchronize(c->cur));
   if (!h_result->fits) return BCW_E_CAPACITY;
   if (h->rec_off && h->rec_off_cap < h_result->n_in) return BCW_E_CAPACITY;
-  if (h->wal && h_result->wal_need && p->mode == BCW_ENC_COMPACT)
-    HIPCHK(hipMemcpyAsync(h->wal, d.wal, h_result->wal_need, hipMemcpyDeviceToHost, c->cur));
-  if (h->hint && h_result->hint_need)
-    HIPCHK(hipMemcpyAsync(h->hint, d.hint, h_result->hint_need, hipMemcpyDeviceToHost, c->cur));
+  return BCW_OK;
+}
+
+int encode_copy_out(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out* h, const bcw_encode_result& r,
+                    const bcw_encode_out& d, const bcw_decode_result& dres) {
+  if (h->wal && r.wal_need && p->mode == BCW_ENC_COMPACT)
+    HIPCHK(hipMemcpyAsync(h->wal, d.wal, r.wal_need, hipMemcpyDeviceToHost, c->cur));
+  if (h->hint && r.hint_need) HIPCHK(hipMemcpyAsync(h->hint, d.hint, r.hint_need, hipMemcpyDeviceToHost, c->cur));
   // rows >= n_in are never written (UINT64_MAX): copy only rows the encode can have written
-  const uint64_t nr = std::min(h_result->n_in, rows);
+  const uint64_t nr = std::min(r.n_in, d.rec_off_cap);
   if (h->rec_off && nr) HIPCHK(hipMemcpyAsync(h->rec_off, d.rec_off, nr * 8, hipMemcpyDeviceToHost, c->cur));
   HIPCHK(hipStreamSynchronize(c->cur));
   if (h->rec_off)
     for (uint64_t i = nr; i < h->rec_off_cap && i < dres.n_records; ++i) h->rec_off[i] = ~0ull;
   return BCW_OK;
+}
+
+int encode_to_host(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out* h, bcw_encode_result* h_result,
+                   const bcw_decode_result& dres) {
+  bcw_encode_out d{};
+  const int rc = encode_run(c, p, h, h_result, &d);
+  return rc != BCW_OK ? rc : encode_copy_out(c, p, h, *h_result, d, dres);
 }
 }  // namespace bcw
 

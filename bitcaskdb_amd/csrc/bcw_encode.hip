@@ -1951,11 +1951,12 @@ hipError_t launch_encode(const EncLaunch& L, EncScratch& s, hipStream_t st, Prof
     if (abl != 2) {
       // as many workgroups as are resident at once (each takes a fixed share of the records: a grid of 8 per CU with
       // 6 resident ran its last 2 per CU after the others, at a third of the occupancy)
-      static int wc_res = 0;
-      if (wc_res == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wc_res, k_wcopy, kCT, 0) != hipSuccess ||
-                          wc_res < 1))
-        wc_res = 4;
-      k_wcopy<<<(uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, (uint64_t)L.num_cus * wc_res)), kCT, 0,
+      // (cached per context: the query runs on the context's device, and no state is shared between contexts)
+      if (s.wcopy_resident == 0 &&
+          (hipOccupancyMaxActiveBlocksPerMultiprocessor(&s.wcopy_resident, k_wcopy, kCT, 0) != hipSuccess ||
+           s.wcopy_resident < 1))
+        s.wcopy_resident = 4;
+      k_wcopy<<<(uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, (uint64_t)L.num_cus * s.wcopy_resident)), kCT, 0,
                 st>>>(W);
       k_write<16><<<wgrid(16), kWT, 0, st>>>(W);
       k_write_general<PM_DST><<<std::min<uint32_t>(rgrid, (uint32_t)L.num_cus * 4), 256, 0, st>>>(W, 0, s.dsrc, nullptr,

@@ -100,6 +100,18 @@ bool recover_one(bcw_ctx* c, bcw_index* stg, const bcw_recover_file& F, bcw_reco
          frag_error(S.wal_dres.err_class);
 }
 
+// every context non-null and named once: each worker thread owns its context's scratch (decode tables, keep mask,
+// staging), so one context listed twice would have two threads decoding into the same buffers (bcw.h: a context
+// belongs to one caller thread at a time)
+bool distinct_contexts(bcw_ctx* const* ctxs, uint32_t n) {
+  for (uint32_t w = 0; w < n; ++w) {
+    if (!ctxs[w]) return false;
+    for (uint32_t v = 0; v < w; ++v)
+      if (ctxs[v] == ctxs[w]) return false;
+  }
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -107,8 +119,7 @@ extern "C" {
 int bcw_recover_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const bcw_recover_file* files,
                      uint64_t n_files, bcw_recover_status* st, int64_t* stop_file) {
   if (!ix || !ctxs || !n_ctx || (n_files && (!files || !st)) || !stop_file) return BCW_E_INVAL;
-  for (uint32_t w = 0; w < n_ctx; ++w)
-    if (!ctxs[w]) return BCW_E_INVAL;
+  if (!distinct_contexts(ctxs, n_ctx)) return BCW_E_INVAL;
   for (uint64_t i = 0; i < n_files; ++i) {
     const bcw_recover_file& F = files[i];
     if ((F.wal_p.seg_len && !F.wal) || F.wal_p.mode != BCW_MODE_RECORD) return BCW_E_INVAL;
@@ -184,8 +195,7 @@ int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const 
                      uint64_t n_src, const bcw_encode_params* dst, bcw_encode_result* res, bcw_index_result* filt,
                      uint64_t* n_done) {
   if (!ix || !ctxs || !n_ctx || !dst || !n_done || (n_src && (!srcs || !res || !filt))) return BCW_E_INVAL;
-  for (uint32_t w = 0; w < n_ctx; ++w)
-    if (!ctxs[w]) return BCW_E_INVAL;
+  if (!distinct_contexts(ctxs, n_ctx)) return BCW_E_INVAL;
   for (uint64_t k = 0; k < n_src; ++k) {
     if (srcs[k].len && !srcs[k].data) return BCW_E_INVAL;
     res[k] = bcw_encode_result{};
@@ -208,6 +218,7 @@ int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const 
   std::mutex mu;
   std::condition_variable cv;
   uint64_t turn = 0;  // the source whose encode runs next
+  std::vector<uint8_t> copied(n_src, 0);  // sources whose outputs reached the host
   uint64_t wal_pos = dst->wal_pos, hint_pos = dst->hint_pos;
   bool quit = false;
   int err = BCW_OK;
@@ -257,7 +268,9 @@ int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const 
                             hipStreamSynchronize(c->cur) != hipSuccess))
           r = BCW_E_HIP;
       }
-      // the encode, in source order
+      // the encode, in source order: the turn is held until its result (the dst / hint ends) is in; the copies of
+      // its outputs to the host then run beside the next source's encode (only the ends chain the sources,
+      // compaction.go:294-327 appends each source where the previous one ended)
       {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return quit || turn == k; });
@@ -265,9 +278,10 @@ int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const 
         p.wal_pos = wal_pos;
         p.hint_pos = hint_pos;
       }
+      bcw_encode_out dout{};
       if (r == BCW_OK) {
         DeviceGuard dg(c->device);
-        r = dg.ok ? encode_to_host(c, &p, &S.out, &res[k], dres) : BCW_E_HIP;
+        r = dg.ok ? encode_run(c, &p, &S.out, &res[k], &dout) : BCW_E_HIP;
       }
       {
         std::lock_guard<std::mutex> lk(mu);
@@ -277,9 +291,24 @@ int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const 
         } else {
           wal_pos = res[k].wal_end;
           hint_pos = res[k].hint_end;
-          *n_done = k + 1;
           if (res[k].err_class != BCW_ENC_ERR_NONE) quit = true;  // doCompactionWork returns the error
           turn = k + 1;
+        }
+      }
+      cv.notify_all();
+      if (r != BCW_OK) return;
+      {
+        DeviceGuard dg(c->device);
+        r = dg.ok ? encode_copy_out(c, &p, &S.out, res[k], dout, dres) : BCW_E_HIP;
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (r != BCW_OK) {
+          if (err == BCW_OK) err = r;
+          quit = true;
+        } else {
+          copied[k] = 1;
+          while (*n_done < n_src && copied[*n_done]) ++*n_done;  // the leading sources whose output is final
         }
       }
       cv.notify_all();

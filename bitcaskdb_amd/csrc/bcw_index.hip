@@ -54,7 +54,9 @@ static_assert(sizeof(Slot) == 64, "Slot layout");
 constexpr uint64_t kProv = 1ull << 63;  // provisional slot reference (claim -> commit inside one batch)
 
 // device counters (C_NEED: arena bytes the rows of a decoded table would take, k_ix_need)
-enum { C_ARENA = 0, C_SLOTS = 1, C_LIVE = 2, C_OVERFLOW = 3, C_NIN = 4, C_DONE = 5, C_FAIL = 6, C_NEED = 7, C_NUM = 8 };
+// C_EVICTED / C_EVICTED_BYTES: keys evicted by the capacity bound (k_ix_evict) and the sum of their value sizes
+enum { C_ARENA = 0, C_SLOTS = 1, C_LIVE = 2, C_OVERFLOW = 3, C_NIN = 4, C_DONE = 5, C_FAIL = 6, C_NEED = 7,
+       C_EVICTED = 8, C_EVICTED_BYTES = 9, C_NUM = 10 };
 
 // op sources
 enum { SRC_FLAT = 0, SRC_RECORD = 1, SRC_HINT = 2 };
@@ -655,6 +657,72 @@ __global__ __launch_bounds__(256) void k_ix_export(const Slot* __restrict__ slot
   for (uint64_t q = 0; q < b; ++q) keys[pb + q] = src[q];
 }
 
+// ---- the capacity bound (bcw_index_set_limit): map.go's ShardMap keeps 16 shards (hash % 16) of Limited / 16 keys
+// each and, when an insert would exceed a shard's limit, evicts the entry of minimum expire among sampled ones
+// (SimpleMap.Set map.go:185-187, evict map.go:395-420, evictMinExpireEntry map.go:319). The device restates the
+// bound with a deterministic policy: an entry's expire is the sequence number of the last op that set it (the
+// index's logical clock in place of genExpire's wall seconds), and at the end of every batch each shard holding more
+// than its limit evicts its entries of smallest sequence number (exact LRU order, every entry sampled) until it holds
+// its limit. One workgroup per shard: count its live keys, radix-select (11-bit digits over npass passes) the
+// (n - limit)-th smallest sequence number T (sequence numbers are unique), then evict every entry with seq <= T (live
+// = 0, as Delete: the slot stays claimed). The evicted keys and their value sizes are counted (C_EVICTED*), the
+// WriteStat of an eviction (index.go:144-165 reports the evicted value from Set's eviction path).
+__global__ __launch_bounds__(1024) void k_ix_evict(Slot* __restrict__ slots, uint64_t cap, uint64_t lim,
+                                                   uint64_t* __restrict__ cnt, uint32_t npass) {
+  __shared__ uint32_t hist[2048];
+  __shared__ unsigned long long s_acc[3];
+  __shared__ uint64_t s_sel[2];  // prefix so far, rank left
+  const uint32_t shard = blockIdx.x, tid = threadIdx.x;
+  if (tid < 3) s_acc[tid] = 0;
+  __syncthreads();
+  uint64_t n = 0;
+  for (uint64_t i = tid; i < cap; i += blockDim.x) n += (slots[i].live != 0 && (slots[i].hash & 15u) == shard) ? 1 : 0;
+  atomicAdd(&s_acc[0], (unsigned long long)n);
+  __syncthreads();
+  const uint64_t total = s_acc[0];
+  if (total <= lim) return;
+  if (tid == 0) { s_sel[0] = 0; s_sel[1] = total - lim; }
+  for (int p = (int)npass - 1; p >= 0; --p) {
+    const uint32_t sh = 11u * (uint32_t)p;
+    const uint64_t hi = (uint32_t)p + 1u >= npass ? 0ull : ~((1ull << (sh + 11u)) - 1ull);  // digits already chosen
+    for (uint32_t b = tid; b < 2048u; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const uint64_t pre = s_sel[0];
+    for (uint64_t i = tid; i < cap; i += blockDim.x) {
+      const Slot& q = slots[i];
+      if (q.live != 0 && (q.hash & 15u) == shard && (q.seq & hi) == (pre & hi))
+        atomicAdd(&hist[(q.seq >> sh) & 2047u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {  // the digit holding the rank-th smallest (a serial scan: evictions are rare)
+      uint64_t rank = s_sel[1], c = 0;
+      uint32_t b = 0;
+      for (; b < 2047u && c + hist[b] < rank; ++b) c += hist[b];
+      s_sel[0] = pre | ((uint64_t)b << sh);
+      s_sel[1] = rank - c;
+    }
+    __syncthreads();
+  }
+  const uint64_t T = s_sel[0];
+  uint64_t ev = 0, evb = 0;
+  for (uint64_t i = tid; i < cap; i += blockDim.x) {
+    Slot& q = slots[i];
+    if (q.live != 0 && (q.hash & 15u) == shard && q.seq <= T) {
+      q.live = 0;
+      ++ev;
+      evb += q.size;
+    }
+  }
+  atomicAdd(&s_acc[1], (unsigned long long)ev);
+  atomicAdd(&s_acc[2], (unsigned long long)evb);
+  __syncthreads();
+  if (tid == 0 && s_acc[1]) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[C_EVICTED]), s_acc[1]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[C_EVICTED_BYTES]), s_acc[2]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[C_LIVE]), (unsigned long long)(0ull - s_acc[1]));
+  }
+}
+
 }  // namespace ix
 }  // namespace bcw
 
@@ -670,6 +738,7 @@ struct bcw_index {
   uint64_t* cnt = nullptr;  // device counters
   uint64_t slots_ub = 0, arena_ub = 0;  // host upper bounds of the device counters
   uint64_t seq_base = 1;                // sequence number of the next op
+  uint64_t limited = 0;                 // the capacity bound (bcw_index_set_limit; 0: none)
   // per-op scratch
   uint64_t* op_kref = nullptr;
   uint64_t* op_hash = nullptr;
@@ -776,6 +845,14 @@ int ix_stage(bcw_index* x, uint64_t bytes) {
   return BCW_OK;
 }
 
+// the capacity bound after a batch (k_ix_evict), when one is set
+void ix_bound(bcw_index* x) {
+  if (!x->limited) return;
+  uint32_t npass = 1;
+  while (npass < 6 && (x->seq_base >> (11u * npass)) != 0) ++npass;  // digits of the largest sequence number
+  k_ix_evict<<<16, 1024, 0, x->ctx->cur>>>(x->slots, x->cap, x->limited / 16, x->cnt, npass);
+}
+
 // the five launches of a batch (ops [0, n) of src); old_*: optional WriteStat outputs of k_ix_claim
 void ix_batch(bcw_index* x, const Src& s, uint64_t n, const bcw_decode_result* R, uint64_t gen, const OpVals& v,
               uint8_t* old_found = nullptr, uint64_t* old_fid = nullptr, uint64_t* old_size = nullptr) {
@@ -790,6 +867,7 @@ void ix_batch(bcw_index* x, const Src& s, uint64_t n, const bcw_decode_result* R
   k_ix_commit<<<grid, 256, 0, st>>>(s, n, x->cnt, x->slots, x->arena, x->arena_cap, x->op_hash, x->op_slot);
   k_ix_write<<<grid, 256, 0, st>>>(s, n, x->cnt, v, x->slots, x->op_slot, x->seq_base);
   x->seq_base += n;
+  ix_bound(x);
 }
 
 Src table_src(bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_params* p, const bcw_record_table* t, int kind) {
@@ -930,7 +1008,19 @@ int bcw_index_stats(bcw_index* x, bcw_index_info* out) {
   out->arena_used = c[C_ARENA];
   out->arena_capacity = x->arena_cap;
   out->overflow = c[C_OVERFLOW];
+  out->limited = x->limited;
+  out->evicted = c[C_EVICTED];
+  out->evicted_bytes = c[C_EVICTED_BYTES];
   return BCW_OK;
+}
+
+int bcw_index_set_limit(bcw_index* x, uint64_t limited) {
+  if (!x || (limited != 0 && limited < 16)) return BCW_E_INVAL;
+  DeviceGuard dg(x->ctx->device);
+  if (!dg.ok) return BCW_E_HIP;
+  x->limited = limited;
+  ix_bound(x);  // an index already past the new bound is brought within it at once
+  return hipGetLastError() == hipSuccess && hipStreamSynchronize(x->ctx->cur) == hipSuccess ? BCW_OK : BCW_E_HIP;
 }
 
 int bcw_index_apply_stat(bcw_index* x, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off,

@@ -53,9 +53,12 @@ constexpr int kSChunk = 64 * kSPiece;
 constexpr int kSPW = kSPiece / 4;  // words per lane
 constexpr int kS2Slice = 256 * 64, kS2Lop = 8 * 16 * 64, kS2Kop = kSPW * 4 * 256;
 constexpr int kS2LopOff = 0, kS2SliceOff = kS2Lop, kS2KopOff = kS2Lop + kS2Slice;
-constexpr int kS2GeN = 17, kS2JselN = 20, kS2GapN = 23;  // entries (4 dwords each)
+// XR (the one-launch decode's stream, stream_verify2): 0xff at piece bytes [m - 3, m + 1) (m < 19), none at m = 19 --
+// the init value of CRC-32C XORed into a fragment's first four bytes
+constexpr int kS2GeN = 17, kS2JselN = 20, kS2GapN = 23, kS2XrN = 20;  // entries (4 dwords each)
 constexpr int kS2Ge = kS2Slice + kS2Lop + kS2Kop, kS2Jsel = kS2Ge + 4 * kS2GeN, kS2Gap = kS2Jsel + 4 * kS2JselN;
-constexpr int kS2Image = kS2Gap + 4 * kS2GapN + 4;  // (+ pad to 16 B)
+constexpr int kS2Xr = kS2Gap + 4 * kS2GapN;
+constexpr int kS2Image = kS2Xr + 4 * kS2XrN + 4;  // (+ pad to 16 B)
 #ifndef BCW_CRC_WAVES
 #define BCW_CRC_WAVES 16
 #endif
@@ -76,9 +79,9 @@ struct Scratch {
   uint4* srec = nullptr;       // [frag_cap + 4] stream record per fragment (k_chase -> k_crc, bcw_decode.hip kRecUsual)
   uint8_t* fok = nullptr;      // [frag_cap] CRC verdict per fragment (k_crc; dense: 64 verdicts are one 64 B store)
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
-  uint32_t* equeue = nullptr;  // [8 x 32] k_crc emission work-queue heads, one 128 B line per XCD
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
   uint64_t test_abort_wg = 0;  // BCW_OPT_TEST_ABORT_WAIT for the next launch only (k_chase workgroup + 1; 0: none)
+  uint32_t decode_path = 1;    // BCW_OPT_DECODE_PATH: 2 one launch (k_decode), 1 two launches (k_chase + k_crc)
 };
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
@@ -140,6 +143,7 @@ struct EncScratch {
   void* recdesc = nullptr;    // [rows] 128 B payload descriptors (k_recdesc_w -> k_write), dst WAL
   uint32_t* wl = nullptr;     // [rows] dst records k_wcopy leaves to k_write<16> / k_write_general
   uint64_t* emisc = nullptr;  // [64] counters
+  int wcopy_resident = 0;     // k_wcopy workgroups resident per CU (occupancy query on the context's device, once)
   // the payload descriptors are built on an auxiliary stream while the serial layout scans run
   hipStream_t aux = nullptr;
   hipEvent_t ev_scan = nullptr, ev_hscan = nullptr, ev_desc = nullptr;
@@ -198,6 +202,12 @@ int ensure_keep(bcw_ctx* c, uint64_t rows);
 bcw_decode_params src_params(const uint8_t* h_src, const bcw_encode_params* p);
 int encode_to_host(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out* h, bcw_encode_result* h_result,
                    const bcw_decode_result& dres);
+// encode_to_host in two steps (bcw_compact_wals): the encode and its result (the dst / hint ends the next source
+// starts from), then the copies of the outputs to the host. *d_out: the device-side outputs between the two.
+int encode_run(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out* h, bcw_encode_result* h_result,
+               bcw_encode_out* d_out);
+int encode_copy_out(bcw_ctx* c, const bcw_encode_params* p, const bcw_encode_out* h, const bcw_encode_result& r,
+                    const bcw_encode_out& d, const bcw_decode_result& dres);
 
 // Export of an index's live entries (bcw_index.hip) into host arrays the sink provides once the sizes are known:
 // room(n, key_bytes) fills the five pointers (koff has n + 1 entries) or refuses (BCW_E_CAPACITY). h_fids / n_fids
@@ -247,6 +257,7 @@ struct bcw_ctx {
   bcw_index_result* d_ires = nullptr;  // sync index calls
   uint32_t last_start_off = 0;
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // BCW_OPT_CHASE_DIRECT
+  uint32_t decode_path = 1;                      // BCW_OPT_DECODE_PATH
   uint64_t test_abort_wg = 0;                    // BCW_OPT_TEST_ABORT_WAIT (one-shot)
   uint64_t last_nfrag_cap = 0;
   bcw::Prof prof;

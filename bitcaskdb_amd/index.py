@@ -53,6 +53,9 @@ class IndexStats:
     arena_used: int
     arena_capacity: int
     overflow: int
+    limited: int = 0
+    evicted: int = 0
+    evicted_bytes: int = 0
 
 
 class Index:
@@ -167,7 +170,16 @@ class Index:
         if rc != 0:
             raise RuntimeError(f"bcw_index_stats: {L.lib.bcw_strerror(rc).decode()}")
         return IndexStats(int(info.live), int(info.slots_used), int(info.slot_capacity), int(info.arena_used),
-                          int(info.arena_capacity), int(info.overflow))
+                          int(info.arena_capacity), int(info.overflow), int(info.limited), int(info.evicted),
+                          int(info.evicted_bytes))
+
+    def set_limit(self, limited: int):
+        """IndexLimited (db.go:71): at most `limited` keys, 16 shards of limited / 16 (map.go's ShardMap), least
+        recently set entries evicted after every batch (bcw_index_set_limit: the deterministic stand-in for the
+        reference's Rand-sampled eviction, map.go:395-420). 0: unbounded."""
+        rc = L.lib.bcw_index_set_limit(self._h, limited)
+        if rc != 0:
+            raise RuntimeError(f"bcw_index_set_limit: {L.lib.bcw_strerror(rc).decode()}")
 
     def export(self, fids=None) -> dict:
         """every live entry: {merged key: (fid, off, size)}; fids: only entries whose value fid is one of them
@@ -343,7 +355,10 @@ def compact_wals_filtered(dst: WalFile, hint: WalFile, srcs, index: Index, ns_si
             k = int(done.value)
             r, m = res[k], int(part[k].data.size)
             wcap, hcap, nrows = caps.get(k0 + k, (m + m // 8 + 4096, m // 16 + 4096, max(16, m // 12 + 16)))
-            caps[k0 + k] = (max(wcap, int(r.wal_need)), max(hcap, int(r.hint_need)), max(nrows, int(r.n_in)))
+            grown = (max(wcap, int(r.wal_need)), max(hcap, int(r.hint_need)), max(nrows, int(r.n_in)))
+            if grown == (wcap, hcap, nrows):  # not an output shortfall (a staging or fragment capacity refusal)
+                raise RuntimeError(f"bcw_compact_wals: {L.lib.bcw_strerror(rc).decode()}")
+            caps[k0 + k] = grown
             k0 += k
             continue
         if rc != 0:
@@ -385,7 +400,10 @@ def compact_one_wal_filtered(dst: WalFile, hint: WalFile, src: Wal, index: Index
         rc = L.lib.bcw_compact_segment(ctx.handle, index.handle, seg.ctypes.data_as(C.c_void_p) if n else None,
                                        C.byref(p), src.fid, C.byref(out), C.byref(res), C.byref(fres))
         if rc == L.E_CAPACITY:
-            wcap, hcap, nrows = max(wcap, int(res.wal_need)), max(hcap, int(res.hint_need)), max(nrows, int(res.n_in))
+            grown = (max(wcap, int(res.wal_need)), max(hcap, int(res.hint_need)), max(nrows, int(res.n_in)))
+            if grown == (wcap, hcap, nrows):  # not an output shortfall (a staging or fragment capacity refusal)
+                raise RuntimeError(f"bcw_compact_segment: {L.lib.bcw_strerror(rc).decode()}")
+            wcap, hcap, nrows = grown
             continue
         if rc != 0:
             raise RuntimeError(f"bcw_compact_segment: {L.lib.bcw_strerror(rc).decode()}")

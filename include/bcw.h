@@ -363,6 +363,9 @@ typedef struct bcw_index_info {
   uint64_t arena_used;    /* key arena bytes */
   uint64_t arena_capacity;
   uint64_t overflow;      /* != 0: an operation found no slot (index inconsistent) */
+  uint64_t limited;       /* the capacity bound (bcw_index_set_limit), 0: none */
+  uint64_t evicted;       /* keys evicted by the bound so far */
+  uint64_t evicted_bytes; /* their value sizes (the WriteStat.FreeBytes of the evictions, index.go:144-165) */
 } bcw_index_info;
 
 /* keys / arena_bytes: initial sizing (both grow on demand) */
@@ -370,6 +373,14 @@ int bcw_index_create(bcw_ctx* ctx, uint64_t keys, uint64_t arena_bytes, bcw_inde
 int bcw_index_destroy(bcw_index* ix);
 int bcw_index_reserve(bcw_index* ix, uint64_t keys, uint64_t arena_bytes);
 int bcw_index_stats(bcw_index* ix, bcw_index_info* out);
+/* IndexLimited (db.go:71, db_impl.go:165): bound the index to `limited` keys (0: unbounded, else >= 16), kept as
+ * map.go's ShardMap keeps it -- 16 shards by hash % 16, Limited / 16 keys each -- with a deterministic eviction in
+ * place of the reference's Rand-sampled one (map.go:395-420; exact parity with Rand is not possible): an entry's
+ * expire is the sequence number of the last op that set it, and after every batch (apply, put / recover of a
+ * decoded table, the fan-out's ordered puts) each shard over its limit evicts its least recently set entries until
+ * it holds its limit. A Get of an evicted key fails (ErrKeyNotFound), so the compaction filter drops its rows. The
+ * evictions are counted in bcw_index_info (evicted, evicted_bytes). Applies the bound at once. */
+int bcw_index_set_limit(bcw_index* ix, uint64_t limited);
 /* Index.Put / Delete / SoftDelete of n merged keys (host arrays; key i = h_keys[h_key_off[i], h_key_off[i+1]),
  * h_ops[i] = BCW_IDX_*), applied in order (the Go shim mirrors DBImpl.writeIndex, db_impl.go:433-452).
  * Synchronous. */
@@ -434,7 +445,10 @@ int bcw_index_recover_segment(bcw_ctx* ctx, bcw_index* ix, const uint8_t* h_seg,
 /* ---- one process, several devices: the fan-outs of a Go caller that drives several GPUs -------------------------
  * Each takes n_ctx contexts (any devices, one host thread each) and the index; INTEGRATION.md shows the cgo loop.
  * The puts into the index and the appends to the dst files keep the reference's order; only the decodes (and
- * their uploads) run concurrently. */
+ * their uploads) run concurrently. Every context is named once (BCW_E_INVAL otherwise: each worker thread owns its
+ * context's decode scratch). The index's own context may be one of ctxs: the index calls the caller's thread makes
+ * meanwhile (the ordered puts, the filter snapshot) use only that context's device and stream, their staging
+ * buffers are the index's own, and HIP orders the two threads' work on the one stream. */
 typedef struct bcw_recover_file {
   uint64_t fid;
   const uint8_t* wal;       /* the data WAL file */
@@ -460,7 +474,9 @@ typedef struct bcw_recover_status {
  * the index receives those, file by file, in ascending fid -- the state the reference's serial Put loop leaves.
  * Recovery stops at the first file whose data WAL iteration fails (rejected row or fragment error), whose put
  * failed (hint/wal_ires.err_class), whose hint decode gave up (BCW_ERR_INTERNAL) or whose calls failed (rc):
- * that file's puts are applied (the reference returns its error after them), later files' are not.
+ * that file's puts are applied (the reference returns its error after them), later files' are not. A failed put
+ * (a staging or index capacity error, hint_ires / wal_ires.err_class) has no counterpart in the reference, whose
+ * Index.Put does not fail: it stops recovery here as in the serial path (parity unpinned for that case).
  * st (n_files entries, in files[] order) receives each file's outcome; *stop_file the files[] index of the
  * stopping file, -1 when every file was applied. Returns BCW_OK, or an error of the index's own calls. */
 int bcw_recover_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const bcw_recover_file* files,

@@ -99,6 +99,22 @@ def test_recover_fanout_two_contexts(ctx, ctx2, ctx3, with_index_ctx):
     assert (a.live, a.slots_used, a.arena_used, a.overflow) == (b.live, b.slots_used, b.arena_used, 0)
 
 
+def test_fanout_refuses_a_context_listed_twice(ctx, ctx2):
+    """each worker thread owns its context's decode scratch: a context named twice is BCW_E_INVAL, for
+    recovery and compaction alike, and nothing is applied"""
+    files = _files(13, 3)
+    ix = IX.Index(ctx)
+    with pytest.raises(RuntimeError, match="invalid"):
+        IX.recover_from_wals(ix, _wals(files), contexts=[ctx2, ctx2])
+    assert ix.export() == {}
+    srcs, _, _, _ = _compaction_setup(14, 2)
+    dst, hint = W.WalFile(77, BASE), W.WalFile(77, BASE)
+    n0, h0 = dst.size(), hint.size()
+    with pytest.raises(RuntimeError, match="invalid"):
+        IX.compact_wals_filtered(dst, hint, [W.load_wal(d, fid) for fid, d in srcs], ix, contexts=[ctx, ctx2, ctx])
+    assert (dst.size(), hint.size()) == (n0, h0)
+
+
 def test_recover_fanout_into_populated_index(ctx, ctx2):
     """recovery into an index that already holds entries: recovered keys override them, the others stay"""
     files = _files(12, 4)

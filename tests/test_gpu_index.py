@@ -309,3 +309,129 @@ def test_hint_recovery_wide_namespace(ctx):
     got = []
     W.iterate_hint(W.load_wal(hint, 4), lambda h: got.append((h.ns, h.key, h.off)), ns_size=300)
     assert got == [(ns, b"k%05d" % i + bytes(i % 200), offs[i]) for i in range(300)]
+
+
+class _BoundModel:
+    """the device's capacity policy (bcw_index_set_limit) restated: ops in order on a logical clock (an entry's
+    stamp is its last Put / SoftDelete), and after every batch each of the 16 shards (murmur3 Sum64 % 16,
+    map.go:395-428's ShardMap) holding more than limited / 16 keys evicts its least recently set ones"""
+
+    def __init__(self, limited):
+        self.lim = limited // 16
+        self.d = {}
+        self.t = 0
+        self.evicted = self.evicted_bytes = 0
+
+    def op(self, op, k, f=0, o=0, z=0):
+        self.t += 1
+        if op == L.IDX_DELETE:
+            self.d.pop(k, None)
+        elif op == L.IDX_SOFT_DELETE:
+            self.d[k] = (0, 0, 0, self.t)
+        else:
+            self.d[k] = (f, o, z, self.t)
+
+    def bound(self):
+        by = {}
+        for k, v in self.d.items():
+            by.setdefault(O.murmur3_sum64(k) & 15, []).append((v[3], k))
+        for lst in by.values():
+            if len(lst) > self.lim:
+                for _, k in sorted(lst)[:len(lst) - self.lim]:
+                    self.evicted += 1
+                    self.evicted_bytes += self.d[k][2]
+                    del self.d[k]
+
+    def export(self):
+        return {k: v[:3] for k, v in self.d.items()}
+
+
+def _shard_counts(entries):
+    c = [0] * 16
+    for k in entries:
+        c[O.murmur3_sum64(k) & 15] += 1
+    return c
+
+
+@pytest.mark.parametrize("limited", [16 * 8, 16 * 40])
+def test_index_capacity_bound_batches(ctx, limited):
+    """IndexLimited (db.go:71, db_impl.go:165) on the device index: random Put / Delete / SoftDelete batches over a
+    key space several times the bound. After every batch the index equals the policy model (entries, evicted count
+    and bytes) and no shard holds more than limited / 16 keys (map.go:185-187's bound; the least-recently-set order
+    stands in for the reference's Rand-sampled pool, map.go:319-370)"""
+    rng = random.Random(limited)
+    keys = [ns + k for ns, k in _keyset(rng, 4 * limited)]
+    ix = IX.Index(ctx, keys=1024)
+    ix.set_limit(limited)
+    m = _BoundModel(limited)
+    for batch in range(25):
+        n = rng.choice([1, 7, 60, 400])
+        ops, ks, fs, os_, zs = [], [], [], [], []
+        for _ in range(n):
+            op = rng.choice([0, 0, 0, 0, 0, 1, 2])
+            k = rng.choice(keys)
+            f, o, z = rng.randrange(1, 50), rng.randrange(40, 1 << 40), rng.randrange(5, 1 << 20)
+            ops.append(op)
+            ks.append(k)
+            fs.append(f)
+            os_.append(o)
+            zs.append(z)
+            m.op(op, k, f, o, z)
+        ix.apply(ops, ks, fs, os_, zs)
+        m.bound()
+        exp = ix.export()
+        assert exp == m.export(), batch
+        assert max(_shard_counts(exp)) <= limited // 16
+        s = ix.stats()
+        assert (s.live, s.limited, s.evicted, s.evicted_bytes, s.overflow) == (len(exp), limited, m.evicted,
+                                                                              m.evicted_bytes, 0), batch
+    assert m.evicted > 0
+    # a Get of an evicted key fails like a deleted one's (ErrKeyNotFound)
+    gone = [k for k in keys if k not in m.d][:50]
+    st, _, _, _ = ix.get_many(gone)
+    assert all(int(x) == 1 for x in st)
+    ix.close()
+
+
+def test_index_capacity_bound_recovery(ctx):
+    """recovery (recoverFromWal's Put loop, db_impl.go:286-313) into a bounded index: each hint / WAL is one batch;
+    the index equals the policy model after every file and never holds more than the bound; set_limit on a fuller
+    index applies the bound at once; the fan-out recovery (bcw_recover_wals) into a bounded index respects it too
+    (its per-file batches hold each file's last put per key, so which keys survive may differ from the serial
+    path's: the bound, not the set, is the property there)"""
+    files = _wal_set(8, nfiles=4, n=500, nkeys=1500, vlens=(10, 300, 5000))
+    limited = 16 * 20
+    ix = IX.Index(ctx)
+    ix.set_limit(limited)
+    m = _BoundModel(limited)
+    for fid in sorted(files):
+        data, _ = files[fid]
+        dec = O.decode(data, 40, BASE, 20, 20, want_bytes=True)
+        dres, ires = ix.recover_segment(data, L.MODE_RECORD, fid, 40, BASE, 20, 20)
+        assert dres.err_class == 0 and ires.n_done == len(dec.recs) == 500
+        for r, pay in zip(dec.recs, dec.payloads):
+            ko, kl = int(r["hdr_size"]), int(r["key_len"])
+            m.op(L.IDX_PUT, bytes(pay[1:21]) + bytes(pay[ko:ko + kl]), fid, int(r["foff"]) - 7, int(r["size"]))
+        m.bound()
+        exp = ix.export()
+        assert exp == m.export(), fid
+        assert len(exp) <= limited and max(_shard_counts(exp)) <= limited // 16
+    # an unbounded index, bounded afterwards
+    un = IX.Index(ctx)
+    for fid in sorted(files):
+        un.recover_segment(files[fid][0], L.MODE_RECORD, fid, 40, BASE, 20, 20)
+    assert un.stats().live > limited
+    un.set_limit(limited)
+    assert max(_shard_counts(un.export())) <= limited // 16 and un.stats().evicted > 0
+    # the fan-out into a bounded index
+    ctx2 = W.Context(0)
+    fan = IX.Index(ctx)
+    fan.set_limit(limited)
+    wals = {fid: (W.load_wal(d, fid), W.load_wal(h, fid)) for fid, (d, h) in files.items()}
+    IX.recover_from_wals(fan, wals, contexts=[ctx2])
+    exp = fan.export()
+    assert 0 < len(exp) <= limited and max(_shard_counts(exp)) <= limited // 16
+    assert all(f in files for f, _, _ in exp.values())
+    ctx2.close()
+    for x in (ix, un, fan):
+        x.close()

@@ -142,7 +142,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="skip the index rebuild / compaction filter leg")
     args = ap.parse_args()
-    line = measure(args.records, args.steps, args.warmup, with_index=not args.no_index)
+    line = measure(args.records, args.steps, args.warmup, with_index=not args.no_index, realistic=True)
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     s = json.dumps(line)
@@ -150,11 +150,12 @@ def main():
     if args.out:
         with open(args.out, "w") as fh:
             fh.write(s + "\n")
-    if not (line["parity"]["wal_equals_source"] and line["parity"]["hint_decodes_to_offsets"]):
+    if not (line["parity"]["wal_equals_source"] and line["parity"]["hint_decodes_to_offsets"]
+            and all(line["realistic"]["parity"].values())):
         raise SystemExit("config E parity check failed")
 
 
-def measure(records: int, steps: int, warmup: int, with_index: bool = False) -> dict:
+def measure(records: int, steps: int, warmup: int, with_index: bool = False, realistic: bool = False) -> dict:
     """the config-E encode of `records` records (synthesised on the host, uploaded once): warmup untimed encodes,
     then `steps` timed ones (HIP events on the codec's stream); also used by bench.py's encode_e key"""
     import torch
@@ -300,8 +301,98 @@ def measure(records: int, steps: int, warmup: int, with_index: bool = False) -> 
     if with_index:
         line["index"] = index_leg(L, ctx, stream, d_src, dparams, table, d_res, n_rec, steps, decode_checked,
                                   encode, keep)
+    if realistic:
+        line["realistic"] = realistic_leg(L, ctx, stream, d_src, seg_len, n_rec, dparams, table, cols, d_res, d_eres,
+                                          keep, d_wal, d_hint, d_off, wal_cap, hint_cap, steps, warmup, decode_checked)
     ctx.close()
     return line
+
+
+def realistic_leg(L, ctx, stream, d_src, seg_len, n_rec, dparams, table, cols, d_res, d_eres, keep, d_wal, d_hint,
+                  d_off, wal_cap, hint_cap, steps, warmup, decode_checked):
+    """the realistic compaction of the same source: a seeded 70 % keep mask (the index's doFilter
+    verdicts, compaction.go:303) and a dst baseTime 500,000 s below the source's (compaction.go:25-29), so the dst
+    layout is shifted against the source's and the records split across dst blocks are others than the source's
+    (their piece CRCs hashed, bcw_encode.hip k_wcopy). Timed like the identity encode. Parity here is
+    self-consistency (the full-size oracle comparison of exactly this shape is tests/test_gpu_fullsize.py
+    test_config_e_full_size_realistic_chunks): the dst WAL decodes on the device to the kept rows with no error, its
+    record sizes equal the kept source rows', and the hint WAL decodes to the returned offsets of the kept rows.
+    split_records: dst records written in two or more fragments."""
+    import torch
+    dev = d_src.device
+    dst_base = BASE_TIME - 500_000
+    rng = np.random.default_rng(7)
+    km = rng.random(n_rec) < 0.7
+    keep.zero_()
+    keep[:n_rec] = torch.from_numpy(km.astype(np.uint8)).to(dev)
+    kept = int(km.sum())
+    eparams = L.EncodeParams(seg_len, dst_base, 1, 40, 40, 40, L.ENC_COMPACT, 20, 20)
+    out = L.EncodeOut(C.cast(C.c_void_p(d_wal.data_ptr()), L.u8p), wal_cap,
+                      C.cast(C.c_void_p(d_hint.data_ptr()), L.u8p), hint_cap,
+                      C.cast(C.c_void_p(d_off.data_ptr()), L.u64p))
+
+    def encode():
+        assert L.lib.bcw_encode_segment_async(ctx.handle, C.c_void_p(d_src.data_ptr()), C.byref(eparams),
+                                              C.byref(table), C.c_void_p(d_res.data_ptr()),
+                                              C.c_void_p(keep.data_ptr()), C.byref(out),
+                                              C.c_void_p(d_eres.data_ptr())) == 0
+
+    decode_checked(d_src.data_ptr(), dparams)
+    src_size = cols["size"][:n_rec].clone()
+    for _ in range(max(warmup, 1)):
+        encode()
+    torch.cuda.synchronize()
+    res = L.EncodeResult.from_buffer_copy(bytes(d_eres.cpu().numpy()))
+    assert res.fits and res.err_class == 0 and res.n_written == kept, (res.fits, res.err_class, res.n_written, kept)
+    wal_bytes, hint_bytes = int(res.wal_need), int(res.hint_need)
+    L.lib.bcw_ctx_set_profiling(ctx.handle, -1)
+    nk = int(L.lib.bcw_ctx_kernel_times(ctx.handle, None, None, 0))
+    names = [L.lib.bcw_kernel_name(k).decode() for k in range(nk)]
+    L.lib.bcw_ctx_kernel_times(ctx.handle, None, None, nk)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        encode()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    enc_ms = e0.elapsed_time(e1) / steps
+    tot = (C.c_double * nk)()
+    cnt = (C.c_uint64 * nk)()
+    L.lib.bcw_ctx_kernel_times(ctx.handle, tot, cnt, nk)
+    L.lib.bcw_ctx_set_profiling(ctx.handle, 0)
+    kern = {names[k]: round(tot[k] / cnt[k], 4) for k in range(nk) if cnt[k]}
+    kept_rows = torch.from_numpy(np.nonzero(km)[0]).to(dev)
+    offs_kept = d_off[kept_rows].clone()
+    size_kept = src_size[kept_rows]
+    # the dst WAL decodes to the kept rows: their count, no error, the kept sources' sizes; split records counted
+    sb = (C.c_uint8 * 40)()
+    L.lib.bcw_write_super_block(sb, dst_base, dst_base)
+    img = torch.empty(40 + wal_bytes, dtype=torch.uint8, device=dev)
+    img[:40] = torch.frombuffer(bytearray(bytes(sb)), dtype=torch.uint8).to(dev)
+    img[40:] = d_wal[:wal_bytes]
+    torch.cuda.synchronize()
+    dres = decode_checked(img.data_ptr(), L.DecodeParams(40 + wal_bytes, dst_base, 40, 20, 20, L.MODE_RECORD))
+    wal_ok = (dres.err_class == 0 and dres.n_records == kept and int(dres.first_bad_record) == -1
+              and bool(torch.equal(cols["size"][:kept], size_kept)))
+    split = int((cols["first_frag"][:kept] != cols["emit_frag"][:kept]).sum().item())
+    del img
+    himg = torch.empty(40 + hint_bytes, dtype=torch.uint8, device=dev)
+    himg[:40] = torch.frombuffer(bytearray(bytes(sb)), dtype=torch.uint8).to(dev)
+    himg[40:] = d_hint[:hint_bytes]
+    torch.cuda.synchronize()
+    hres = decode_checked(himg.data_ptr(), L.DecodeParams(40 + hint_bytes, dst_base, 40, 20, 0, L.MODE_HINT))
+    hint_ok = (hres.err_class == 0 and hres.n_records == kept and int(hres.first_bad_record) == -1
+               and bool(torch.equal(cols["aux0"][:kept], offs_kept)))
+    del himg
+    keep.fill_(1)  # (the identity encode's mask, for any later user)
+    alg = seg_len + wal_bytes + hint_bytes
+    wr = kern.get("k_write")
+    return {"encode_ms": round(enc_ms, 3), "records_in": n_rec, "records_kept": kept, "split_records": split,
+            "wal_bytes": wal_bytes, "hint_bytes": hint_bytes, "dst_base_time": dst_base,
+            "GBs": round(alg / (enc_ms * 1e-3) / 1e9, 1),
+            "writer_TBs": round(alg / (wr * 1e-3) / 1e12, 3) if wr else None, "kernel_ms": kern,
+            "layout_events": {"wal": int(res.wal_events), "hint": int(res.hint_events)},
+            "parity": {"dst_decodes_to_kept_rows": wal_ok, "hint_decodes_to_offsets": hint_ok}}
 
 
 if __name__ == "__main__":

@@ -211,7 +211,7 @@ int main(int argc, char** argv) {
     }
   }
   const uint64_t nblocks = (n - 40 + kBlock - 1) / kBlock;
-  const EmitArgs ea{d, n, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, s.equeue, 0u, nullptr};
+  const EmitArgs ea{d, n, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, 0u, nullptr};
   EmitArgs ea_off = ea;
   ea_off.kb_flags = 1u;  // the product kernel with its emission skipped at run time
   EmitArgs ea_st = ea;   // ... with per-wave stamps of its CRC end, emission end and items
@@ -260,12 +260,10 @@ int main(int argc, char** argv) {
     EmitArgs a = a0;
     if (kb_clock && !a.kb_stamps) a.kb_stamps = seq_stamps ? seq_stamps : clk_st;
     if (run_reps == 0) {
-      hipMemsetAsync(s.equeue, 0, 1024, st);
       kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid);
       return 0.0f;
     }
-    const float ms = timeit([&] { hipMemsetAsync(s.equeue, 0, 1024, st);  // the emission queues (k_chase resets them)
-                        kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid); },
+    const float ms = timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid); },
                   reps, st);
     if (kb_clock && a.kb_stamps == clk_st) last_mhz = clock_of(clk_st, grid * kCrcWaves);
     return ms;
@@ -370,6 +368,25 @@ int main(int argc, char** argv) {
     printf("\n");
     return 0;
   }
+  if (argc > 3 && std::string(argv[3]) == "pcmp") {  // decode paths (BCW_OPT_DECODE_PATH 1 / 2) interleaved, 7 x reps
+    std::vector<float> ts[2];
+    uint64_t nrec[2] = {0, 0};
+    for (int rr = 0; rr < 7; ++rr)
+      for (int path = 1; path <= 2; ++path) {
+        CK(bcw_ctx_set_option(ctx, BCW_OPT_DECODE_PATH, path));
+        ts[path - 1].push_back(timeit([&] { bcw_decode_segment_async(ctx, d, &p, &t, dres); }, reps, st));
+        bcw_decode_result rr2;
+        CK(hipMemcpy(&rr2, dres, sizeof rr2, hipMemcpyDeviceToHost));
+        nrec[path - 1] = rr2.n_records;
+        if (rr2.err_class != 0 || rr2.n_records != res.n_records) printf("path %d: err %d n_records %lu\n", path, rr2.err_class, rr2.n_records);
+      }
+    for (int k = 0; k < 2; ++k) {
+      std::sort(ts[k].begin(), ts[k].end());
+      printf("decode path %d: min %.4f median %.4f max %.4f ms (%.0f GiB/s at the median), n_records %lu\n", k + 1,
+             ts[k][0], ts[k][3], ts[k][6], n / (ts[k][3] * 1e-3) / 1073741824.0, nrec[k]);
+    }
+    return 0;
+  }
   if (argc > 4 && std::string(argv[3]) == "cmp") {  // k_crc variants interleaved in one process (same buffers)
     const int nv = argc - 4;
     std::vector<std::vector<float>> ts(nv);
@@ -425,7 +442,6 @@ int main(int argc, char** argv) {
   printf("k_crc fast chain only (no emission) %.4f  no emission %.4f  emission only %.4f ms\n", a1, a8, a9);
   const float as = timeit([&] {
     hipMemsetAsync(&s.misc[M_DONE_CRC], 0, 8, st);  // the last workgroup finalizes
-    hipMemsetAsync(s.equeue, 0, 1024, st);
     k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
                                           s.misc, 0ull, nblocks, (uint32_t)cus);
   }, reps, st);
@@ -442,7 +458,7 @@ int main(int argc, char** argv) {
       return timeit([&] {
         kern<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
                                                               s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.epoch,
-                                                              ctx->tabs.initc, s.chase_direct, s.equeue, 0ull);
+                                                              ctx->tabs.initc, s.chase_direct, 0ull);
         ++s.epoch;
       }, reps, st);
     };
@@ -462,8 +478,7 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&stp, nwg * 32));
       for (int rep = 0; rep < 3; ++rep) {
         k_chase<32><<<(uint32_t)nwg, 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags, s.srec, s.frag_cap,
-                                                  s.lb, stp, s.misc, s.epoch, ctx->tabs.initc, s.chase_direct, s.equeue,
-                                                  0ull);
+                                                  s.lb, stp, s.misc, s.epoch, ctx->tabs.initc, s.chase_direct, 0ull);
         ++s.epoch;
         CK(hipStreamSynchronize(st));
       }
