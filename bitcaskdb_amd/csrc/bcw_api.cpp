@@ -310,11 +310,6 @@ int bcw_ctx_create(int device, bcw_ctx** out) {
       }
       put_bytes(kS2Gap + 4 * g, b);
     }
-    for (int m = 0; m < kS2XrN; ++m) {  // XR[m]: 0xff at [m - 3, m + 1), none at the last entry
-      uint8_t b[16];
-      for (int q = 0; q < 16; ++q) b[q] = (m < kS2XrN - 1 && q >= m - 3 && q < m + 1) ? 0xff : 0x00;
-      put_bytes(kS2Xr + 4 * m, b);
-    }
   }
   bool ok = hipMalloc(&c->tabs.lds_image2, image2.size() * 4) == hipSuccess &&
             hipMemcpy(c->tabs.lds_image2, image2.data(), image2.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
@@ -422,7 +417,6 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   s.nlb = nwg;
   s.epoch = 1;
   s.chase_direct = c->chase_direct;
-  s.decode_path = c->decode_path;
   // on the codec's stream: a null-stream hipMemset is not ordered before kernels on a non-blocking
   // stream, and a look-back word zeroed after k_chase published it would never be seen again
   // misc[15] (the first unknown-type fragment, an atomicMin in k_chase) starts at UINT64_MAX; every decode's
@@ -514,12 +508,8 @@ int bcw_ctx_set_option(bcw_ctx* c, int option, uint64_t value) {
       c->s.chase_direct = (uint32_t)value;
       c->chase_direct = (uint32_t)value;
       return BCW_OK;
-    case BCW_OPT_DECODE_PATH:  // 2: one launch (k_decode, the default), 1: two launches (k_chase + k_crc)
-      if (value != 1 && value != 2) return BCW_E_INVAL;
-      c->s.decode_path = (uint32_t)value;
-      c->decode_path = (uint32_t)value;
-      return BCW_OK;
-    case BCW_OPT_DECODE_CHUNKS:  // retired (bcw.h): only its one remaining value is accepted
+    case BCW_OPT_DECODE_PATH:    // retired options (bcw.h): only their one remaining value is accepted
+    case BCW_OPT_DECODE_CHUNKS:
       return value == 1 ? BCW_OK : BCW_E_INVAL;
     case BCW_OPT_TEST_ABORT_WAIT: {  // fault injection: refused unless the process opted in (BCW_TEST_HOOKS=1)
       const char* hooks = getenv("BCW_TEST_HOOKS");

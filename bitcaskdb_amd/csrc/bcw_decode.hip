@@ -21,8 +21,6 @@ namespace bcw {
 // misc counters (Scratch::misc)
 enum { M_FIRST_BAD = 0,  // first record whose parse fails (atomicMin in k_crc's emission)
        M_NE = 1,         // Full/Last fragments of the whole segment (k_chase)
-       M_TICKET = 2,     // k_decode: the next chase job (64-block group) to take (reset by the finalize)
-       M_CHASE_DONE = 3, // k_decode: chase jobs done (their tables written and released; reset by the finalize)
        M_NFRAGS = 4, M_DONE_CRC = 5,
        M_T_CRC0 = 10, M_T_FIN = 11,  // wall_clock64 stamps (diagnostics)
        M_ABORT = 12,     // k_chase: the wait site that timed out (0: none); reported as BCW_ERR_INTERNAL
@@ -182,7 +180,6 @@ __device__ __forceinline__ void put_frag_J(Frag* __restrict__ frags, uint4* __re
                                            uint32_t J, uint32_t type, bool adj) {
   if (g >= frag_cap) return;
   *reinterpret_cast<uint4*>(frags + g) = make_uint4(b, start_len, J, type & 0xffu);
-  if (!srec) return;  // (the one-launch decode's chase writes no stream records: its stream chases the headers itself)
   const uint64_t gs = boff + (start_len & 0xffffu), ge = gs + (start_len >> 16);
   const uint32_t cb = (uint32_t)(gs / kSChunk), ce = (uint32_t)(ge / kSChunk);
   const uint32_t pa = (uint32_t)(gs % kSChunk), pb = (uint32_t)(ge % kSChunk);
@@ -208,21 +205,31 @@ constexpr uint32_t kSumHasE = 1u << 16;
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no predecessor sum, 2 no table writes,
 // 16 phase cycles (chase, sum, writes; s_memtime) summed into misc[7..9], 32 per-workgroup wall-clock stamps (entry,
 // chase end, sum end, end) into lbe[4 wg ..] (kbench passes a buffer of its own; direct-sum sizes only)
-// The chase of one 64-block group `wg` by one wave (lane = block): k_chase's body (one group per one-wave workgroup),
-// and the chase jobs of the one-launch decode (k_decode: groups taken by ticket, srec = null). kHold headers per lane
-// are kept in LDS (s_hold / s_type, the caller's).
-template <int ABL, int kHold>
-__device__ __forceinline__ void chase_group(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
-                                            uint64_t nblocks, uint32_t* __restrict__ fbase,
-                                            uint32_t* __restrict__ rbase, uint2* __restrict__ bsum,
-                                            Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t frag_cap,
-                                            uint64_t* __restrict__ lb, uint64_t* __restrict__ lbe,
-                                            uint64_t* __restrict__ misc, uint64_t epoch,
-                                            const uint32_t* __restrict__ initc, uint32_t direct_max,
-                                            uint64_t test_abort_wg, uint64_t wg, uint32_t lane,
-                                            uint32_t (*__restrict__ s_hold)[2][64], uint8_t (*__restrict__ s_type)[64]) {
+template <int ABL = 0>
+__global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
+                                              uint64_t nblocks, uint32_t* __restrict__ fbase,
+                                              uint32_t* __restrict__ rbase, uint2* __restrict__ bsum,
+                                              Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t frag_cap,
+                                              uint64_t* __restrict__ lb,
+                                              uint64_t* __restrict__ lbe, uint64_t* __restrict__ misc,
+                                              uint64_t epoch, const uint32_t* __restrict__ initc,
+                                              uint32_t direct_max, uint64_t test_abort_wg) {
+  // {crc, start | len << 16} and type of each lane's first 64 headers: 36 KiB, so a k_chase workgroup still fits beside
+  // a k_crc workgroup (which leaves 44 KiB of the CU's LDS since round 4) when another segment's decode is in flight.
+  // A block with more headers is chased a second time from the 65th on when its table entries are written (16 held
+  // headers, round 3: config C k_chase 69.5 vs 58.9 us with 64, kbench)
+  // (ABL & 256, kbench: 16 held headers per lane, the round-3 size)
+  constexpr int kHold = (ABL & 256) ? 16 : kChaseHold;
+  __shared__ uint32_t s_hold[kHold][2][64];
+  __shared__ uint8_t s_type[kHold][64];
+  const uint32_t lane = threadIdx.x;
   const uint64_t tc0 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
-  if ((ABL & 32) && lane == 0) lbe[4 * wg] = wall_clock64();
+  if ((ABL & 32) && threadIdx.x == 0) lbe[4 * blockIdx.x] = wall_clock64();
+  // the workgroup id orders the look-back: workgroups are dispatched in id order (within each XCD), so one only waits
+  // on ids already running; the bounded waits (Spin) turn any other schedule into BCW_ERR_INTERNAL, never a hang.
+  // (Round 4 took tickets from one atomic counter: its 512 returning atomics on one word ended 5-7 us apart, and the
+  // last ticket's chase gated every base: k_chase B 22.1 -> 16.8 us, C 31.3 -> 24.3 us without them, kbench.)
+  const uint64_t wg = blockIdx.x;
   const uint64_t b = wg * 64 + lane;
   uint32_t bufsize = 0;
   uint64_t boff = 0;
@@ -429,31 +436,6 @@ __device__ __forceinline__ void chase_group(const uint8_t* __restrict__ seg, uin
       misc[M_NE] = total_e;
     }
   }
-}
-
-template <int ABL = 0>
-__global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
-                                              uint64_t nblocks, uint32_t* __restrict__ fbase,
-                                              uint32_t* __restrict__ rbase, uint2* __restrict__ bsum,
-                                              Frag* __restrict__ frags, uint4* __restrict__ srec, uint64_t frag_cap,
-                                              uint64_t* __restrict__ lb,
-                                              uint64_t* __restrict__ lbe, uint64_t* __restrict__ misc,
-                                              uint64_t epoch, const uint32_t* __restrict__ initc,
-                                              uint32_t direct_max, uint64_t test_abort_wg) {
-  // {crc, start | len << 16} and type of each lane's first 64 headers: 36 KiB, so a k_chase workgroup still fits beside
-  // a k_crc workgroup (which leaves 44 KiB of the CU's LDS since round 4) when another segment's decode is in flight.
-  // A block with more headers is chased a second time from the 65th on when its table entries are written (16 held
-  // headers, round 3: config C k_chase 69.5 vs 58.9 us with 64, kbench)
-  // (ABL & 256, kbench: 16 held headers per lane, the round-3 size)
-  constexpr int kHold = (ABL & 256) ? 16 : kChaseHold;
-  __shared__ uint32_t s_hold[kHold][2][64];
-  __shared__ uint8_t s_type[kHold][64];
-  // the workgroup id orders the look-back: workgroups are dispatched in id order (within each XCD), so one only waits
-  // on ids already running; the bounded waits (Spin) turn any other schedule into BCW_ERR_INTERNAL, never a hang.
-  // (Round 4 took tickets from one atomic counter: its 512 returning atomics on one word ended 5-7 us apart, and the
-  // last ticket's chase gated every base: k_chase B 22.1 -> 16.8 us, C 31.3 -> 24.3 us without them, kbench.)
-  chase_group<ABL, kHold>(seg, seg_len, start_off, nblocks, fbase, rbase, bsum, frags, srec, frag_cap, lb, lbe, misc,
-                          epoch, initc, direct_max, test_abort_wg, blockIdx.x, threadIdx.x, s_hold, s_type);
 }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -1370,476 +1352,6 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   finalize(A, T.nblocks, T.frag_cap, T.tail_panic, T.gen, T.res, lane);
 }
 
-// ------------------------------------------------------------------------------------------
-// The one-launch decode (k_decode, round 6): the stream chases the headers itself.
-//
-// k_crc's stream (stream_verify) read each fragment's geometry from k_chase's stream records, so k_chase's chase, its
-// predecessor sum and its table writes (16-22 us on config B) ran before the first chunk was loaded. Every 32 KiB block
-// starts at a fragment header and a wave streams whole blocks, so the headers arrive in the stream itself: at a
-// fragment's end the next header (wal_iterator.go:45-77: at the data end while 7 bytes are left in the block, else at
-// the next block's start) is read from the chunk's registers with readlanes. The check word needs no table:
-// J' = ~unmask(stored CRC), and the CRC-32C init value 0xFFFFFFFF is XORed into the first four bytes of the string
-// data || J' (by linearity that is the init value of the whole string), so the zero test R(D' || J') = 0 holds iff
-// ComputeCRC32(D) equals the stored CRC, for any length (also below 4 bytes, where the XOR reaches into J').
-//
-// The record emission still needs the fragment table, the block bases and the record-state summaries: two waves of
-// every workgroup take chase jobs (k_chase's chase of one 64-block group, chase_group) by ticket before they stream,
-// so the tables are written while the other waves stream. The waves' emission (after their streams) and the verdict
-// stores (at the global fragment index) wait for every job's release (M_CHASE_DONE).
-
-// bytes [o, o + 7) (o <= 15) of the 24-byte window s0..s5 (wave-uniform): the header's stored CRC, length and type
-__device__ __forceinline__ void hdr_window(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t s4, uint32_t s5,
-                                           uint32_t o, uint32_t& crc, uint32_t& len) {
-  const uint32_t q = o >> 2, r = (o & 3u) * 8u;
-  const uint32_t a = q == 0 ? s0 : q == 1 ? s1 : q == 2 ? s2 : s3;
-  const uint32_t b = q == 0 ? s1 : q == 1 ? s2 : q == 2 ? s3 : s4;
-  const uint32_t c = q == 0 ? s2 : q == 1 ? s3 : q == 2 ? s4 : s5;
-  crc = (uint32_t)((((uint64_t)b << 32) | a) >> r);
-  len = (uint32_t)((((uint64_t)c << 32) | b) >> r) & 0xffffu;
-}
-__device__ __forceinline__ uint32_t xr_index(int32_t pos, uint32_t lane) {
-  return min((uint32_t)(pos - (int32_t)(kSPiece * lane) + 3), (uint32_t)(kS2XrN - 1));
-}
-// the general fragment-end mask (mask_chunk) plus the init XOR at [pa, pa + 4) and [pc, pc + 4) (pa, pc unclamped)
-__device__ __forceinline__ void mask_chunk2(uint32_t (&x)[kSPW], const uint32_t (&w)[kSPW], int32_t pa, int32_t pb,
-                                            int32_t pc, uint32_t J, uint32_t lane, const uint32_t* __restrict__ lds) {
-  auto rel = [](int32_t p) -> int32_t { return min(max(p, -64), 4096); };
-  mask_chunk(x, w, rel(pa), rel(pb), rel(pc), J, lane, lds);
-  const uint4 X0 = lds_entry(lds + kS2Xr, xr_index(pa, lane));
-  const uint4 X1 = lds_entry(lds + kS2Xr, xr_index(pc, lane));
-  x[0] ^= X0.x | X1.x;
-  x[1] ^= X0.y | X1.y;
-  x[2] ^= X0.z | X1.z;
-  x[3] ^= X0.w | X1.w;
-}
-// the usual end (mask_gap: J at [pb, pb + 4), the next header's other bytes zeroed) plus the next fragment's init XOR
-__device__ __forceinline__ void mask_gap2(uint32_t (&x)[kSPW], const uint32_t (&w)[kSPW], int32_t pb, uint32_t J,
-                                          uint32_t lane, const uint32_t* __restrict__ lds) {
-  mask_gap(x, w, pb, J, lane, lds);
-  const uint4 X = lds_entry(lds + kS2Xr, xr_index(pb + (int32_t)kHdr, lane));
-  x[0] ^= X.x;
-  x[1] ^= X.y;
-  x[2] ^= X.z;
-  x[3] ^= X.w;
-}
-
-// Verify every fragment whose header lies in blocks [b0, b1) (one wave), chasing the headers from the chunks. Positions
-// are 32-bit, relative to the wave's first chunk cf (the one holding block b0's first header). States: a header pending
-// at hp (PEND), a fragment open with data [gs, ge) and check word J (OPEN), or none left (DONE). `ev` is the next chunk
-// that needs more than the fast chain: the one holding the open fragment's data end (its J and the next header), or the
-// next one while a header, a check word or a fragment's first four bytes straddle the chunk end (hs0 / hs1 keep the
-// last 8 bytes of a slow chunk for a header read across the boundary). The verdicts reach fok at the global index
-// f0 + i once the chase jobs have published fbase (every 64 fragments and at the end).
-template <bool FASTONLY = false>
-__device__ __forceinline__ void stream_verify2(const uint8_t* __restrict__ seg, uint64_t seg_len, uint32_t start_off,
-                                               uint64_t b0, uint64_t b1, uint8_t* __restrict__ fok, uint64_t frag_cap,
-                                               const uint32_t* __restrict__ fbase, uint32_t ngroups,
-                                               const uint32_t* __restrict__ lds, uint32_t lane,
-                                               uint64_t* __restrict__ misc, uint32_t* __restrict__ s_rem,
-                                               uint32_t wslot, const uint8_t* __restrict__ dummy) {
-  constexpr int D = 8;
-  if (b1 <= b0) return;
-  const uint64_t bb0 = (uint64_t)start_off + b0 * kBlock;
-  if (bb0 + kHdr > seg_len) return;  // the segment's short last block holds no header
-  const uint64_t cf = bb0 / kSChunk;
-  const uint64_t last_end = min((uint64_t)start_off + b1 * kBlock, seg_len);
-  if (last_end - cf * kSChunk > (1ull << 30)) {  // (no wave of a real segment spans 1 GiB)
-    if (lane == 0) atomicMax(reinterpret_cast<unsigned long long*>(&misc[M_ABORT]), 22ull);
-    return;
-  }
-  const int32_t rel0 = (int32_t)(bb0 - cf * kSChunk), end_rel = (int32_t)(last_end - cf * kSChunk);
-  const uint32_t nbw = (uint32_t)(b1 - b0);
-  uint64_t c_end = (last_end + 4u + kSChunk - 1u) / kSChunk;
-  if (c_end > c_safe_bound(seg_len)) c_end = c_safe_bound(seg_len);
-  const uint32_t nch = (uint32_t)(c_end - cf);
-  auto bstart = [&](uint32_t k) -> int32_t { return rel0 + (int32_t)(k * kBlock); };
-  auto bend = [&](uint32_t k) -> int32_t { return k + 1u == nbw ? end_rel : rel0 + (int32_t)((k + 1u) * kBlock); };
-
-  const uint8_t* tb = reinterpret_cast<const uint8_t*>(lds + kS2SliceOff);
-  const uint32_t* s_lop = lds + kS2LopOff;
-  const uint32_t* s_kop = lds + kS2KopOff;
-  const SliceLane2 sl = slice_lane2(lane);
-  constexpr uint32_t kPend = 0, kOpen = 1, kDone = 2;
-  uint32_t st = kPend;
-  int32_t hp = rel0;    // PEND: the header's position
-  uint32_t blk = 0;     // the block (wave-relative) of the pending header / open fragment
-  int32_t gs = 0, ge = 0;
-  uint32_t J = 0;
-  uint32_t hs0 = 0, hs1 = 0;
-  uint32_t i = 0, ev = 0, H = 0;
-  uint64_t okm = 0;
-  uint32_t bad = 0xffffffffu;
-  uint32_t f0 = 0xffffffffu;  // global index of the wave's first fragment (0xfffffffe: the chase gave up)
-  auto ensure_f0 = [&]() {
-    if (f0 != 0xffffffffu) return;
-    Spin sp;
-    while (__builtin_amdgcn_readfirstlane((uint32_t)__hip_atomic_load(&misc[M_CHASE_DONE], __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT)) < ngroups)
-      if (!sp.go(misc, 12)) break;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const bool ab = __builtin_amdgcn_readfirstlane((uint32_t)__hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED,
-                                                                               __HIP_MEMORY_SCOPE_AGENT)) != 0u;
-    f0 = ab ? 0xfffffffeu : __builtin_amdgcn_readfirstlane(fbase[b0]);
-  };
-  auto flush = [&](uint32_t from, uint32_t n) {  // verdicts of fragments [from, from + n) (n <= 64)
-    ensure_f0();
-    if (f0 < 0xfffffffeu && lane < n && (uint64_t)f0 + from + lane < frag_cap)
-      fok[(uint64_t)f0 + from + lane] = (uint8_t)((okm >> lane) & 1u);
-    const uint64_t fail = ~okm & (n == 64u ? ~0ull : (1ull << n) - 1ull);
-    if (fail != 0ull && bad == 0xffffffffu) bad = from + (uint32_t)__builtin_ctzll(fail);
-  };
-  // the zero test of the fragment closing at chunk-relative pb (its J ends at pb + 4) over the masked words x (see
-  // stream_verify's close), its verdict, and H = the next fragment's chain state
-  auto close = [&](const uint32_t (&x)[kSPW], int32_t pb) {
-    const uint32_t e = (uint32_t)(pb + 4), K = ((e % kSPiece) + 3u) >> 2;
-    const uint32_t Lfull = e / kSPiece + (K == (uint32_t)kSPW ? 1u : 0u), K3 = K & 3u;
-    uint32_t cap = 0;
-    const uint32_t s8 = chain_piece2<true>(tb, sl, H, x, K3, &cap);
-    const uint32_t Lsplit = K3 != 0u ? Lfull : 64u;
-    const bool full = lane < Lfull, split = lane == Lsplit;
-    const uint32_t A = full ? s8 : apply_op_b(s_kop + (split ? K3 : 0u) * 1024u, split ? cap : H);
-    const uint32_t T = wave_scan_z(apply_fwd(s_lop, lane, A), [](uint32_t a, uint32_t b) { return a ^ b; });
-    if (__builtin_amdgcn_readlane(T, 63) == 0u) okm |= 1ull << (i & 63u);
-    H = s8 ^ A;
-    ++i;
-    if ((i & 63u) == 0u) {
-      flush(i - 64u, 64u);
-      okm = 0;
-    }
-  };
-  // the header at chunk-relative pc (pc < 0: it began in the previous chunk, whose last 8 bytes are hs0 / hs1)
-  auto parse = [&](const uint32_t (&w)[kSPW], int32_t pc, uint32_t& crc, uint32_t& len16) {
-    uint32_t s0, s1, s2, s3, s4, s5, o;
-    if (pc >= 0) {
-      const uint32_t L = (uint32_t)pc >> 4, L1 = min(L + 1u, 63u);
-      s0 = __builtin_amdgcn_readlane(w[0], L);
-      s1 = __builtin_amdgcn_readlane(w[1], L);
-      s2 = __builtin_amdgcn_readlane(w[2], L);
-      s3 = __builtin_amdgcn_readlane(w[3], L);
-      s4 = __builtin_amdgcn_readlane(w[0], L1);
-      s5 = __builtin_amdgcn_readlane(w[1], L1);
-      o = (uint32_t)pc & 15u;
-    } else {
-      s0 = hs0;
-      s1 = hs1;
-      s2 = __builtin_amdgcn_readlane(w[0], 0);
-      s3 = __builtin_amdgcn_readlane(w[1], 0);
-      s4 = 0;
-      s5 = 0;
-      o = (uint32_t)(pc + 8);
-    }
-    hdr_window(s0, s1, s2, s3, s4, s5, o, crc, len16);
-  };
-  // the fragment of the header at h (block blk): data [h + 7, + len clamped to the block, wal_iterator.go:75)
-  auto open_frag = [&](int32_t h, uint32_t crc, uint32_t len16) {
-    gs = h + (int32_t)kHdr;
-    ge = gs + min((int32_t)len16, bend(blk) - gs);
-    J = ~rotl32(crc - 0xa282ead8u, 15);
-    st = kOpen;
-  };
-  // chunk c == ev: the header reads, fragment ends and beginnings inside it; then the next `ev`
-  auto slow = [&](uint32_t c, const uint32_t (&w)[kSPW]) {
-    const int32_t C0 = (int32_t)(c * kSChunk), C1 = C0 + kSChunk;
-    uint32_t nev = 0xffffffffu;
-    for (;;) {
-      if (st == kPend) {
-        if (hp + (int32_t)kHdr > C1) { nev = c + 1u; break; }  // the header straddles the chunk end
-        uint32_t crc, len16;
-        parse(w, hp - C0, crc, len16);
-        open_frag(hp, crc, len16);
-      }
-      if (st != kOpen) break;
-      if (gs >= C1) { nev = (uint32_t)gs / (uint32_t)kSChunk; break; }  // its data begins in the next chunk
-      if (ge + 4 > C1) {  // the data or J runs on into the next chunk
-        uint32_t x[kSPW];
-        mask_chunk2(x, w, gs - C0, ge - C0, 4096, J, lane, lds);
-        H = chain_piece2<false>(tb, sl, H, x);
-        nev = gs + 4 > C1 ? c + 1u : max((uint32_t)ge / (uint32_t)kSChunk, c + 1u);
-        break;
-      }
-      // the fragment closes here. The next header: at the data end while 7 bytes are left in the block, else at the
-      // next block's start (wal_iterator.go:45-49); read now when it lies in this chunk
-      int32_t hn = 0;
-      bool more = true;
-      if (ge + (int32_t)kHdr <= bend(blk)) hn = ge;
-      else if (blk + 1u < nbw && bstart(blk + 1u) + (int32_t)kHdr <= bend(blk + 1u)) { ++blk; hn = bstart(blk); }
-      else more = false;
-      const bool known = more && hn + (int32_t)kHdr <= C1;
-      uint32_t ncrc = 0, nlen = 0;
-      if (known) parse(w, hn - C0, ncrc, nlen);
-      const int32_t ngs = hn + (int32_t)kHdr, nge = ngs + min((int32_t)nlen, bend(blk) - ngs);
-      const bool next_in = known && ngs < C1 && nge >= C1;  // the next fragment's bytes [ngs, C1) are all data
-      uint32_t x[kSPW];
-      if (next_in && gs + 4 <= C0 && hn == ge && ngs + 4 <= C1) mask_gap2(x, w, ge - C0, J, lane, lds);
-      else mask_chunk2(x, w, gs - C0, ge - C0, next_in ? ngs - C0 : 4096, J, lane, lds);
-      close(x, ge - C0);
-      if (!more) { st = kDone; break; }
-      if (!known) { st = kPend; hp = hn; continue; }
-      open_frag(hn, ncrc, nlen);
-      if (next_in) { nev = ngs + 4 > C1 ? c + 1u : (uint32_t)nge / (uint32_t)kSChunk; break; }
-    }
-    if (nev == c + 1u) {  // (a header read across the boundary needs this chunk's last 8 bytes)
-      hs0 = __builtin_amdgcn_readlane(w[2], 63);
-      hs1 = __builtin_amdgcn_readlane(w[3], 63);
-    }
-    ev = nev;
-  };
-  auto step = [&](uint32_t c, const uint32_t (&w)[kSPW]) {
-    if (FASTONLY || c != ev) H = chain_piece2<false>(tb, sl, H, w);
-    else slow(c, w);
-  };
-  const uint64_t c_safe = seg_len / kSChunk;  // chunks [0, c_safe) lie inside the segment
-  const uint32_t nl = c_safe > cf ? (uint32_t)min(c_safe - cf, (uint64_t)nch) : 0u;  // pipelined chunks
-  if (nl > 0u) {
-    const uint8_t* wseg = seg + cf * kSChunk;
-    const uint32_t lane16 = lane * kSPiece;
-    // the chunk ring by hand (stream_verify)
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    v4u buf[D];
-    auto issue = [&](uint32_t c, v4u& w) {
-      const uint8_t* p = c < nl ? wseg + (size_t)c * kSChunk : dummy;
-      asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=v"(w) : "v"(lane16), "s"(p) : "memory");
-    };
-#pragma unroll
-    for (int k = 0; k < D; ++k) issue((uint32_t)k, buf[k]);
-    for (uint32_t c = 0; c < nl; c += D) {
-      const uint32_t left = nl - c;  // issue-priority balancing (stream_verify)
-      if (lane == 0) s_rem[wslot] = left;
-      const uint4 r = *reinterpret_cast<const uint4*>(s_rem + (wslot & ~3u));
-      const uint32_t mx = max(max(r.x, r.y), max(r.z, r.w));
-      if (left + (uint32_t)D >= mx) __builtin_amdgcn_s_setprio(2);
-      else __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-      for (int k = 0; k < D; ++k) {
-        if (c + k < nl) {
-          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(buf[k]) : "n"(D - 1));
-          const uint32_t w[kSPW] = {buf[k].x, buf[k].y, buf[k].z, buf[k].w};
-          step(c + k, w);
-        }
-        issue(c + k + D, buf[k]);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::"v"(buf[0]), "v"(buf[1]), "v"(buf[2]), "v"(buf[3]), "v"(buf[4]), "v"(buf[5]),
-                 "v"(buf[6]), "v"(buf[7]));
-    static_assert(D == 8, "the final wait names every ring register");
-  }
-  for (uint32_t c = nl; c < nch; ++c) {  // chunks touching the segment's end
-    uint32_t w[kSPW];
-    const uint4 A = load16_safe(seg, seg_len, (int64_t)((cf + c) * kSChunk) + lane * kSPiece);
-    w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
-    step(c, w);
-  }
-  flush(i & ~63u, i & 63u);
-  if (FASTONLY && H == 0x9e3779b9u) misc[7] = H;  // (kbench: keep the chains alive)
-  if (lane == 0 && f0 < 0xfffffffeu) {
-    if (bad != 0xffffffffu)
-      atomicMin(reinterpret_cast<unsigned long long*>(&misc[M_BAD_CRC]), (unsigned long long)(f0 + bad));
-    // the stream's chase and the chase jobs' must agree on this wave's fragments (a bug otherwise: reported as
-    // BCW_ERR_INTERNAL, never a silent pass)
-    if (!FASTONLY && (st != kDone || fbase[b1] - f0 != i))
-      atomicMax(reinterpret_cast<unsigned long long*>(&misc[M_ABORT]), 20ull);
-  }
-}
-
-// The chase jobs' arguments (k_decode)
-struct ChaseArgs {
-  uint32_t* fbase;
-  uint32_t* rbase;
-  uint2* bsum;
-  Frag* frags;
-  uint64_t* lb;
-  uint64_t* lbe;
-  const uint32_t* initc;
-  uint64_t epoch;
-  uint64_t test_abort_wg;
-  uint32_t direct_max;
-  uint32_t ngroups;
-};
-constexpr int kJobWaves = 2;   // waves of a k_decode workgroup that take chase jobs before they stream
-constexpr int kJobHold = 16;   // headers a chase job keeps in LDS per block (9 KiB per job wave)
-
-// k_decode: one 1024-thread workgroup per CU. Waves 0 and 1 take chase jobs (64-block groups, by ticket: a job only
-// waits on lower tickets, which running waves hold, so the launch needs no co-residency), then every wave streams its
-// 1 / (16 x CUs) share of the blocks (stream_verify2), then takes emission items of its workgroup once every job is
-// released (as k_crc); the last wave of the last workgroup writes the segment result (finalize).
-// ABL: tools/kbench ablations (0 in the product): 8 no emission, 8388608 every chunk on the fast chain
-template <int ABL = 0>
-__global__ __launch_bounds__(kCrcThreads) void k_decode(const uint8_t* __restrict__ seg, uint64_t seg_len,
-                                                        uint32_t start_off, uint64_t nblocks, uint8_t* __restrict__ fok,
-                                                        uint64_t frag_cap, Tables tabs, EmitArgs ea, ChaseArgs ch,
-                                                        uint32_t tail_panic, uint64_t gen,
-                                                        bcw_decode_result* __restrict__ res,
-                                                        uint64_t* __restrict__ misc) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kS2Image];
-  __shared__ CrcTail s_tail;
-  __shared__ uint32_t s_wdone;  // waves of this workgroup done
-  __shared__ uint32_t s_eq;     // the workgroup's emission items taken
-  __shared__ uint32_t s_ready;  // the chase jobs' tables acquired by one wave of the workgroup
-  __shared__ __attribute__((aligned(16))) uint32_t s_rem[kCrcWaves];
-  __shared__ uint32_t s_hold[kJobWaves][kJobHold][2][64];
-  __shared__ uint8_t s_type[kJobWaves][kJobHold][64];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (tid < (uint32_t)kCrcWaves) s_rem[tid] = 0;
-  if (ea.kb_stamps && lane == 0) {
-    uint64_t* q = ea.kb_stamps + 8 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
-    q[4] = wall_clock64();
-    q[5] = __builtin_amdgcn_s_memtime();
-  }
-  if (tid == 0) {
-    s_wdone = 0;
-    s_eq = 0;
-    s_ready = 0;
-    s_tail = CrcTail{ea, res, misc, nblocks, frag_cap, gen, 0ull, nblocks, tail_panic, gridDim.x};
-  }
-  const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
-  const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
-  // (segments hold < 2^24 blocks: the 64-bit divisions' VGPR results made wave-uniform SGPRs again)
-  const uint64_t b0 = __builtin_amdgcn_readfirstlane((uint32_t)(nblocks * gw / nw)),
-                 b1 = __builtin_amdgcn_readfirstlane((uint32_t)(nblocks * (gw + 1) / nw));
-  {  // table image -> LDS
-    constexpr uint32_t kVec = kS2Image / 4;
-    constexpr int kFull = (int)(kVec / kCrcThreads);
-    const uint4* src = reinterpret_cast<const uint4*>(tabs.lds_image2);
-    uint4* dst = reinterpret_cast<uint4*>(lds);
-    uint4 v[kFull];
-#pragma unroll
-    for (int k2 = 0; k2 < kFull; ++k2) v[k2] = src[tid + k2 * kCrcThreads];
-    const uint32_t tail = tid + kFull * kCrcThreads;
-    uint4 vt = make_uint4(0, 0, 0, 0);
-    if (tail < kVec) vt = src[tail];
-    if (tail < kVec) dst[tail] = vt;
-#pragma unroll
-    for (int k2 = 0; k2 < kFull; ++k2) dst[tid + k2 * kCrcThreads] = v[k2];
-  }
-  __syncthreads();
-  if (blockIdx.x == 0 && tid == 0) misc[M_T_CRC0] = wall_clock64();
-  if (wave < (uint32_t)kJobWaves) {
-    // chase jobs by ticket; each job's tables are released (agent scope) before it counts as done
-    for (;;) {
-      uint32_t t = 0;
-      if (lane == 0)
-        t = (uint32_t)__hip_atomic_fetch_add(&misc[M_TICKET], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      t = __builtin_amdgcn_readfirstlane(t);
-      if (t >= ch.ngroups) break;
-      chase_group<0, kJobHold>(seg, seg_len, start_off, nblocks, ch.fbase, ch.rbase, ch.bsum, ch.frags, nullptr,
-                               frag_cap, ch.lb, ch.lbe, misc, ch.epoch, ch.initc, ch.direct_max, ch.test_abort_wg, t,
-                               lane, s_hold[wave], s_type[wave]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(&misc[M_CHASE_DONE], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  stream_verify2<(ABL & 8388608) != 0>(seg, seg_len, start_off, b0, b1, fok, frag_cap, ch.fbase, ch.ngroups, lds, lane,
-                                       misc, s_rem, (wave & 3u) * 4u + (wave >> 2),
-                                       reinterpret_cast<const uint8_t*>(tabs.lds_image2));
-  __builtin_amdgcn_s_setprio(0);
-  if (ea.kb_stamps && lane == 0) {
-    uint64_t* q = ea.kb_stamps + 8 * gw;
-    q[0] = wall_clock64();
-  }
-  // ---- every chase job released: one wave of the workgroup acquires, the others see its LDS word ----
-  asm volatile("" ::: "memory");
-  if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0u) {
-    Spin sp;
-    const uint32_t ng = ch.ngroups;
-    while (__builtin_amdgcn_readfirstlane((uint32_t)__hip_atomic_load(&misc[M_CHASE_DONE], __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT)) < ng)
-      if (!sp.go(misc, 13)) break;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  // ---- record emission (k_crc's): the workgroup's items, taken from an LDS counter ----
-  uint64_t n_items = 0;
-  {
-    asm volatile("" ::: "memory");
-    CrcTail T;
-    {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(&s_tail);
-      uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
-#pragma unroll
-      for (int k = 0; k < (int)(sizeof(CrcTail) / 4); ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
-    }
-    const EmitArgs& A = T.ea;
-    if (!(ABL & 8) && !(A.kb_flags & 1u) &&
-        __builtin_amdgcn_readfirstlane(
-            (uint32_t)__hip_atomic_load(&T.misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
-      const uint64_t cb0t = T.cb0, cb1t = T.cb1, fcap = T.frag_cap;
-      const uint32_t cnt = (uint32_t)(cb1t - cb0t), G = gridDim.x, wg = blockIdx.x;
-      const uint64_t fc0 = A.fbase[cb0t], fc1 = A.fbase[cb1t];
-      const uint32_t nf_all = (uint32_t)(fc1 > fc0 ? (fc1 - fc0 < fcap ? fc1 - fc0 : fcap) : 0);
-      uint32_t bpw = nf_all ? (64u * cnt) / nf_all : cnt;
-      if (bpw < 1u) bpw = 1u;
-      bpw = __builtin_amdgcn_readfirstlane(bpw);
-      const uint32_t cq = cnt / G, cr = cnt % G;
-      const uint32_t B0 = cq * wg + (cr * wg) / G, B1 = cq * (wg + 1u) + (cr * (wg + 1u)) / G;
-      const uint64_t i0 = __builtin_amdgcn_readfirstlane((B0 + bpw - 1u) / bpw),
-                     nitems = __builtin_amdgcn_readfirstlane((B1 + bpw - 1u) / bpw);
-      auto deq = [&]() -> uint64_t {
-        uint32_t j = 0;
-        if (lane == 0) j = atomicAdd(&s_eq, 1u);
-        j = __builtin_amdgcn_readfirstlane(j);
-        return i0 + j;
-      };
-      uint64_t it = deq();
-      ItemMeta m = item_meta(A, it, bpw, cb0t, cb1t, lane);
-      while (it < nitems) {
-        ++n_items;
-        const EmitState es = emit_state(A, m.bb, lane, m.s, m.rec);
-        const uint64_t mf1 = m.f1 < fcap ? m.f1 : fcap;
-        uint64_t nx = ~0ull;
-        ItemMeta mn = m;
-        emit_chunks(A, es, m.f0, mf1, lane, [&]() {
-          nx = deq();
-          mn = item_meta(A, nx, bpw, cb0t, cb1t, lane);
-        });
-        it = nx;
-        m = mn;
-      }
-    }
-  }
-  asm volatile("" ::: "memory");
-  CrcTail T;
-  {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&s_tail);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(CrcTail) / 4); ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
-  }
-  const EmitArgs& A = T.ea;
-  if (A.kb_stamps && lane == 0) {
-    uint64_t* q = A.kb_stamps + 8 * ((uint64_t)__builtin_amdgcn_workgroup_id_x() * kCrcWaves + wave);
-    q[1] = wall_clock64(); q[2] = n_items;
-    q[6] = __builtin_amdgcn_s_memtime();
-  }
-  // ---- completion (k_crc's) ----
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  uint32_t order = 0;
-  if (lane == 0) order = atomicAdd(&s_wdone, 1u);
-  order = __builtin_amdgcn_readlane(order, 0);
-  if (order != kCrcWaves - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  uint64_t gorder = 0;
-  if (lane == 0)
-    gorder = __hip_atomic_fetch_add(&T.misc[M_DONE_CRC], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  gorder = (uint64_t)__shfl((long long)gorder, 0, 64);
-  if (gorder != T.nwg_total - 1u) return;
-  // (the finalizer reads the chase jobs' tables and counts: released by each job, acquired here)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) T.misc[M_T_FIN] = wall_clock64();
-  finalize(A, T.nblocks, T.frag_cap, T.tail_panic, T.gen, T.res, lane);
-  if (lane == 0) {
-    T.misc[M_TICKET] = 0;
-    T.misc[M_CHASE_DONE] = 0;
-  }
-}
-
 __global__ void k_export_frags(const Frag* __restrict__ frags, const uint8_t* __restrict__ fok,
                                const uint64_t* __restrict__ misc, uint64_t cap,
                                uint32_t start_off, bcw_frag_table out, const uint32_t* __restrict__ initc) {
@@ -1868,22 +1380,6 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;
   const uint32_t nb_grid = (uint32_t)((nblocks + 63) / 64);
   const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, 0u, nullptr};
-  if (s.decode_path == 2) {  // one launch (k_decode)
-    const ChaseArgs ch{s.fbase, s.rbase, s.bsum, s.frags, s.lb, s.lbe, tabs.initc, s.epoch, s.test_abort_wg,
-                       s.chase_direct, nb_grid};
-    s.test_abort_wg = 0;
-    pr.begin(K_CRC, stream, ev);
-    k_decode<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fok,
-                                                               s.frag_cap, tabs, ea, ch, tail_panic, gen, d_result,
-                                                               s.misc);
-    pr.end(K_CRC, stream, ev);
-    if ((++s.epoch & 0xffffffull) == 0) {
-      (void)hipMemsetAsync(s.lb, 0, s.nlb * sizeof(uint64_t), stream);
-      (void)hipMemsetAsync(s.lbe, 0, s.nlb * sizeof(uint64_t), stream);
-      s.epoch = 1;
-    }
-    return hipGetLastError();
-  }
   pr.begin(K_CHASE, stream, ev);
   k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
                                         s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.epoch, tabs.initc, s.chase_direct,

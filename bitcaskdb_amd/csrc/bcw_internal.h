@@ -53,12 +53,9 @@ constexpr int kSChunk = 64 * kSPiece;
 constexpr int kSPW = kSPiece / 4;  // words per lane
 constexpr int kS2Slice = 256 * 64, kS2Lop = 8 * 16 * 64, kS2Kop = kSPW * 4 * 256;
 constexpr int kS2LopOff = 0, kS2SliceOff = kS2Lop, kS2KopOff = kS2Lop + kS2Slice;
-// XR (the one-launch decode's stream, stream_verify2): 0xff at piece bytes [m - 3, m + 1) (m < 19), none at m = 19 --
-// the init value of CRC-32C XORed into a fragment's first four bytes
-constexpr int kS2GeN = 17, kS2JselN = 20, kS2GapN = 23, kS2XrN = 20;  // entries (4 dwords each)
+constexpr int kS2GeN = 17, kS2JselN = 20, kS2GapN = 23;  // entries (4 dwords each)
 constexpr int kS2Ge = kS2Slice + kS2Lop + kS2Kop, kS2Jsel = kS2Ge + 4 * kS2GeN, kS2Gap = kS2Jsel + 4 * kS2JselN;
-constexpr int kS2Xr = kS2Gap + 4 * kS2GapN;
-constexpr int kS2Image = kS2Xr + 4 * kS2XrN + 4;  // (+ pad to 16 B)
+constexpr int kS2Image = kS2Gap + 4 * kS2GapN + 4;  // (+ pad to 16 B)
 #ifndef BCW_CRC_WAVES
 #define BCW_CRC_WAVES 16
 #endif
@@ -81,7 +78,6 @@ struct Scratch {
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
   uint64_t test_abort_wg = 0;  // BCW_OPT_TEST_ABORT_WAIT for the next launch only (k_chase workgroup + 1; 0: none)
-  uint32_t decode_path = 1;    // BCW_OPT_DECODE_PATH: 2 one launch (k_decode), 1 two launches (k_chase + k_crc)
 };
 
 // Optional per-kernel HIP-event timing (bcw_ctx_set_profiling): events recorded on the launch
@@ -257,7 +253,6 @@ struct bcw_ctx {
   bcw_index_result* d_ires = nullptr;  // sync index calls
   uint32_t last_start_off = 0;
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // BCW_OPT_CHASE_DIRECT
-  uint32_t decode_path = 1;                      // BCW_OPT_DECODE_PATH
   uint64_t test_abort_wg = 0;                    // BCW_OPT_TEST_ABORT_WAIT (one-shot)
   uint64_t last_nfrag_cap = 0;
   bcw::Prof prof;

@@ -243,6 +243,7 @@ int main(int argc, char** argv) {
   const size_t clk_per = 8 * (size_t)ctx->num_cus * kCrcWaves;
   if (kb_clock) CK(hipMalloc(&clk_st, clk_per * 8));
   double last_mhz = 0;
+  static char last_tl[256] = "";
   auto clock_of = [&](const uint64_t* dq, int nw) {
     std::vector<uint64_t> q(8 * (size_t)nw);
     CK(hipMemcpy(q.data(), dq, q.size() * 8, hipMemcpyDeviceToHost));
@@ -252,6 +253,24 @@ int main(int argc, char** argv) {
       if (e[1] > e[4]) f.push_back((double)(e[6] - e[5]) / (double)(e[1] - e[4]) * 100.0);
     }
     std::sort(f.begin(), f.end());
+    // the last launch's timeline (real time, us from the first wave's entry): entry spread, stream end p50 / max,
+    // wave end max, and the median stream duration per wave
+    uint64_t t0 = ~0ull;
+    for (int w = 0; w < nw; ++w) if (q[8 * w + 4]) t0 = std::min(t0, q[8 * w + 4]);
+    std::vector<double> ent, se, we, dur;
+    for (int w = 0; w < nw; ++w) {
+      const uint64_t* e = q.data() + 8 * w;
+      if (!e[4]) continue;
+      ent.push_back((e[4] - t0) / 100.0);
+      if (e[0]) { se.push_back((e[0] - t0) / 100.0); dur.push_back((e[0] - e[4]) / 100.0); }
+      if (e[1]) we.push_back((e[1] - t0) / 100.0);
+    }
+    std::sort(ent.begin(), ent.end()); std::sort(se.begin(), se.end()); std::sort(we.begin(), we.end());
+    std::sort(dur.begin(), dur.end());
+    if (!ent.empty() && !se.empty() && !we.empty())
+      snprintf(last_tl, sizeof last_tl, "entry max %.1f | stream end p10 %.1f p50 %.1f max %.1f | end max %.1f | "
+               "stream dur p50 %.1f", ent.back(), se[se.size() / 10], se[se.size() / 2], se.back(), we.back(),
+               dur[dur.size() / 2]);
     return f.empty() ? 0.0 : f[f.size() / 2];
   };
   int run_reps = reps;            // 0: run() launches once, untimed (seqk)
@@ -368,25 +387,6 @@ int main(int argc, char** argv) {
     printf("\n");
     return 0;
   }
-  if (argc > 3 && std::string(argv[3]) == "pcmp") {  // decode paths (BCW_OPT_DECODE_PATH 1 / 2) interleaved, 7 x reps
-    std::vector<float> ts[2];
-    uint64_t nrec[2] = {0, 0};
-    for (int rr = 0; rr < 7; ++rr)
-      for (int path = 1; path <= 2; ++path) {
-        CK(bcw_ctx_set_option(ctx, BCW_OPT_DECODE_PATH, path));
-        ts[path - 1].push_back(timeit([&] { bcw_decode_segment_async(ctx, d, &p, &t, dres); }, reps, st));
-        bcw_decode_result rr2;
-        CK(hipMemcpy(&rr2, dres, sizeof rr2, hipMemcpyDeviceToHost));
-        nrec[path - 1] = rr2.n_records;
-        if (rr2.err_class != 0 || rr2.n_records != res.n_records) printf("path %d: err %d n_records %lu\n", path, rr2.err_class, rr2.n_records);
-      }
-    for (int k = 0; k < 2; ++k) {
-      std::sort(ts[k].begin(), ts[k].end());
-      printf("decode path %d: min %.4f median %.4f max %.4f ms (%.0f GiB/s at the median), n_records %lu\n", k + 1,
-             ts[k][0], ts[k][3], ts[k][6], n / (ts[k][3] * 1e-3) / 1073741824.0, nrec[k]);
-    }
-    return 0;
-  }
   if (argc > 4 && std::string(argv[3]) == "cmp") {  // k_crc variants interleaved in one process (same buffers)
     const int nv = argc - 4;
     std::vector<std::vector<float>> ts(nv);
@@ -405,6 +405,7 @@ int main(int argc, char** argv) {
       printf("k_crc<%s>: min %.4f  median %.4f  max %.4f ms", argv[4 + i], ts[i][0], ts[i][3], ts[i][6]);
       if (kb_clock) printf("  | clock median %.0f MHz, Mcycles min %.4f median %.4f", mh[i][3], mc[i][0], mc[i][3]);
       printf("\n");
+      if (kb_clock) { last_tl[0] = 0; runv(atoi(argv[4 + i])); printf("    timeline: %s\n", last_tl); }
     }
     return 0;
   }
