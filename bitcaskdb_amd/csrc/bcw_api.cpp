@@ -336,6 +336,7 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.frags);
   (void)hipFree(s.srec);
   (void)hipFree(s.fok);
+  (void)hipFree(s.wstart);
   (void)hipFree(s.misc);
   s = Scratch{};
 }
@@ -410,6 +411,7 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
             hipMalloc(&s.lbe, nwg * 8) == hipSuccess && hipMalloc(&s.frags, fc * sizeof(Frag)) == hipSuccess &&
             hipMalloc(&s.srec, (fc + 4) * sizeof(uint4)) == hipSuccess &&
             hipMalloc(&s.fok, fc) == hipSuccess &&
+            hipMalloc(&s.wstart, ((size_t)c->num_cus * kCrcWaves + 1) * 4) == hipSuccess &&
             hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;

@@ -213,7 +213,8 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                               uint64_t* __restrict__ lb,
                                               uint64_t* __restrict__ lbe, uint64_t* __restrict__ misc,
                                               uint64_t epoch, const uint32_t* __restrict__ initc,
-                                              uint32_t direct_max, uint64_t test_abort_wg) {
+                                              uint32_t direct_max, uint64_t test_abort_wg,
+                                              uint32_t* __restrict__ wstart, uint32_t nwaves) {
   // {crc, start | len << 16} and type of each lane's first 64 headers: 36 KiB, so a k_chase workgroup still fits beside
   // a k_crc workgroup (which leaves 44 KiB of the CU's LDS since round 4) when another segment's decode is in flight.
   // A block with more headers is chased a second time from the 65th on when its table entries are written (16 held
@@ -398,16 +399,37 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     // header.
     const bool next_hdr = b + 1 < nblocks && seg_len - (boff + kBlock) >= kHdr;
     auto adj = [&](uint32_t k, uint32_t sl_k) { return k + 1u < n || (next_hdr && (sl_k & 0xffffu) + (sl_k >> 16) == kBlock); };
+    // k_crc's wave ranges, balanced by bytes: wave w streams the fragments whose header lies in [P_w, P_w+1),
+    // P_w = start_off + floor(L w / nwaves) (L = seg_len - start_off), so wstart[w] = the first fragment whose header
+    // is at or after P_w. This lane writes the boundaries that fall in its block, walking its headers in order.
+    // (Whole blocks per wave left 7 of config B's 4096 waves with 9 blocks instead of 8: they ended ~20 us after the
+    // median wave, kbench timelines.)
+    const uint64_t L = seg_len - start_off, rel = boff - start_off;
+    uint64_t w = (rel * nwaves + L - 1) / L;  // the first boundary at or after the block's start
+    // (the last block also takes P_nwaves = seg_len, which lies at its span's end when L is a multiple of 32 KiB)
+    const uint64_t w_end = b + 1 == nblocks ? (uint64_t)nwaves + 1
+                                            : min((uint64_t)nwaves + 1, ((rel + kBlock) * nwaves + L - 1) / L);
+    uint64_t bw = w < w_end ? (L * w) / nwaves - rel : 0;  // boundary w, block-relative
+    auto bounds_upto = [&](uint64_t hp, uint64_t idx) {  // boundaries at or before the header at hp: idx
+      while (w < w_end && bw <= hp) {
+        wstart[w] = (uint32_t)(idx < 0xffffffffull ? idx : 0xffffffffull);
+        ++w;
+        bw = (L * w) / nwaves - rel;
+      }
+    };
     for (uint32_t k = 0; k < nh; ++k) {
       const uint32_t sl = s_hold[k][1][lane];
       put_frag_J(frags, srec, g0 + k, frag_cap, (uint32_t)b, boff, sl, s_hold[k][0][lane], s_type[k][lane],
                  adj(k, sl));
+      bounds_upto((sl & 0xffffu) - kHdr, g0 + k);
     }
     if (n > (uint32_t)kHold)  // the tail of a block with more headers than held, chased again from the first of them
       chase_block(seg, seg_len, boff, bufsize, [&](uint32_t k, uint32_t start, uint32_t len, uint32_t crc, uint32_t type) {
         put_frag(frags, srec, g0 + k, frag_cap, (uint32_t)b, boff, start, len, crc, type, initc,
                  adj(k, start | (len << 16)));
+        bounds_upto(start - kHdr, g0 + k);
       }, hres, (uint32_t)kHold);
+    bounds_upto(~0ull, g0 + n);  // boundaries after the block's last header: the next block's first fragment
   }
   if (ABL & 32) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -577,7 +599,8 @@ struct EmitArgs {
   uint64_t* misc;
   uint32_t kb_flags; // tools/kbench only (0 in the product): 1 = skip the emission at run time
   uint64_t* kb_stamps;  // tools/kbench only (null in the product): 8 words per wave {CRC done, emission done, items,
-                        // fragments, entry (real time), entry (shader cycles), emission done (shader cycles), 0}
+                        // fragments, entry (real time), entry (shader cycles), emission done (shader cycles),
+                        // XCC id << 32 | HW_ID}
 };
 
 
@@ -1191,9 +1214,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
                                                      uint32_t tail_panic, uint64_t gen,
                                                      bcw_decode_result* __restrict__ res,
                                                      uint64_t* __restrict__ misc, uint64_t cb0, uint64_t cb1,
-                                                     uint32_t nwg_total) {
-  // [cb0, cb1): the blocks this launch verifies and emits (the whole segment); nwg_total: the workgroups that count
-  // towards completion
+                                                     uint32_t nwg_total, const uint32_t* __restrict__ wstart) {
+  // [cb0, cb1): the blocks this launch emits (the whole segment); nwg_total: the workgroups that count towards
+  // completion; wstart: each wave's first fragment (k_chase, gridDim.x x kCrcWaves + 1 entries)
   __shared__ __attribute__((aligned(16))) uint32_t lds[kS2Image];
   __shared__ CrcTail s_tail;
   __shared__ uint32_t s_wdone;  // waves of this workgroup done
@@ -1207,6 +1230,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     uint64_t* q = ea.kb_stamps + 8 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
     q[4] = wall_clock64();
     q[5] = __builtin_amdgcn_s_memtime();
+    // the XCC (HW_REG_XCC_ID, 20) and HW_ID (4: wave / SIMD / CU / SH / SE) this wave runs on
+    q[7] = ((uint64_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) | __builtin_amdgcn_s_getreg(4 | (31 << 11));
   }
   if (tid == 0) {
     s_wdone = 0;
@@ -1217,11 +1242,11 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
   // every wave streams the fragments of its 1 / (16 x CUs) share of the blocks (dedicated emission waves measured
   // slower)
-  const uint64_t cn = cb1 - cb0;
-  const uint64_t b0 = cb0 + cn * gw / nw, b1 = cb0 + cn * (gw + 1) / nw;
-  const uint64_t f0 = fbase[b0];
-  uint64_t f1 = fbase[b1];
+  // the wave's fragments, balanced by bytes (k_chase's wstart)
+  const uint64_t f0 = wstart[gw];
+  uint64_t f1 = wstart[gw + 1];
   if (f1 > frag_cap) f1 = frag_cap;
+  if (f0 > f1) f1 = f0;
   // a k_chase wait gave up (Spin): the bases are unreliable, so no fragment is read and no row written
   const bool aborted = __builtin_amdgcn_readfirstlane(
                            (uint32_t)__hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
@@ -1383,7 +1408,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   pr.begin(K_CHASE, stream, ev);
   k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
                                         s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.epoch, tabs.initc, s.chase_direct,
-                                        s.test_abort_wg);
+                                        s.test_abort_wg, s.wstart, (uint32_t)num_cus * kCrcWaves);
   s.test_abort_wg = 0;
   pr.end(K_CHASE, stream, ev);
   if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse
@@ -1395,7 +1420,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.fok,
                                                          s.srec, s.frag_cap, tabs, ea,
                                                          tail_panic, gen, d_result, s.misc, 0ull, nblocks,
-                                                         (uint32_t)num_cus);
+                                                         (uint32_t)num_cus, s.wstart);
   pr.end(K_CRC, stream, ev);
   return hipGetLastError();
 }

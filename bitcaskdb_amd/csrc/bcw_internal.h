@@ -75,6 +75,7 @@ struct Scratch {
   Frag* frags = nullptr;       // [frag_cap]
   uint4* srec = nullptr;       // [frag_cap + 4] stream record per fragment (k_chase -> k_crc, bcw_decode.hip kRecUsual)
   uint8_t* fok = nullptr;      // [frag_cap] CRC verdict per fragment (k_crc; dense: 64 verdicts are one 64 B store)
+  uint32_t* wstart = nullptr;  // [CUs x kCrcWaves + 1] each k_crc wave's first fragment (byte-balanced, k_chase)
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
   uint64_t test_abort_wg = 0;  // BCW_OPT_TEST_ABORT_WAIT for the next launch only (k_chase workgroup + 1; 0: none)

@@ -331,10 +331,11 @@ int bcw_encode_segment(bcw_ctx* ctx, const uint8_t* h_src, const bcw_encode_para
 /* ---- device index: the bitcaskDB index (index.go) resident in HBM -------------------------------
  * Observable semantics of Index.Get/Put/Delete/SoftDelete (index.go:81-165): a map from MergedKey(ns, key)
  * = ns || key (utils.go:133-139) to (fid, off, size), hashed with murmur3 Sum64 (index.go:15-19). Get
- * reports ErrKeyNotFound, or ErrKeySoftDeleted when off == 0. The reference's sampled approximate-LRU
- * eviction (random, map.go:349-371) is not restated: the device index keeps every key and grows. With a bounded
- * Go index (IndexLimited below the key count) the Go index stays authoritative and the device filter runs
- * against a snapshot of it (bcw_index_clear + bcw_index_apply of its live entries).
+ * reports ErrKeyNotFound, or ErrKeySoftDeleted when off == 0. Unbounded by default (the index grows); the
+ * reference's sampled approximate-LRU eviction (map.go:349-420) has a deterministic counterpart,
+ * bcw_index_set_limit below. For exact parity with a bounded Go index (IndexLimited below the key count) keep the
+ * Go index authoritative and run the device filter against a snapshot of it (bcw_index_clear + bcw_index_apply
+ * of its live entries).
  * Batches keep the reference's sequential order: the last operation on a key wins. An index is bound to
  * the context it was created on (its stream and device; the table-driven calls read that context's
  * fragment table of its latest decode). */
@@ -390,9 +391,10 @@ int bcw_index_apply(bcw_index* ix, uint64_t n, const uint8_t* h_keys, const uint
  * (db_impl.go:433-452, manifest.Apply db_impl.go:402): h_found[i] = 1 when op i replaced or removed a value
  * (the key was present before it: a previous op of the same batch counts), h_free_fid[i] / h_free_bytes[i] =
  * that value's fid / valueSize (0, 0 when h_found[i] = 0). The Go shim sums writeStats[free_fid] += free_bytes
- * exactly as writeIndex does. The device index never evicts, so a Put of a new key reports nothing -- with a
- * bounded Go index (IndexLimited below the key count) the reference reports the evicted entry instead: keep the
- * Go index authoritative then ("bounded index"). Synchronous. */
+ * exactly as writeIndex does. A Put of a new key reports nothing; evictions by bcw_index_set_limit's bound are
+ * counted in bcw_index_info instead -- with a bounded Go index (IndexLimited below the key count) the reference
+ * reports the evicted entry on the Put: keep the Go index authoritative then ("bounded index").
+ * Synchronous. */
 int bcw_index_apply_stat(bcw_index* ix, uint64_t n, const uint8_t* h_keys, const uint64_t* h_key_off,
                          const uint8_t* h_ops, const uint64_t* h_fid, const uint64_t* h_off, const uint64_t* h_size,
                          uint8_t* h_found, uint64_t* h_free_fid, uint64_t* h_free_bytes);

@@ -243,7 +243,7 @@ int main(int argc, char** argv) {
   const size_t clk_per = 8 * (size_t)ctx->num_cus * kCrcWaves;
   if (kb_clock) CK(hipMalloc(&clk_st, clk_per * 8));
   double last_mhz = 0;
-  static char last_tl[256] = "";
+  static char last_tl[1024] = "";
   auto clock_of = [&](const uint64_t* dq, int nw) {
     std::vector<uint64_t> q(8 * (size_t)nw);
     CK(hipMemcpy(q.data(), dq, q.size() * 8, hipMemcpyDeviceToHost));
@@ -267,10 +267,41 @@ int main(int argc, char** argv) {
     }
     std::sort(ent.begin(), ent.end()); std::sort(se.begin(), se.end()); std::sort(we.begin(), we.end());
     std::sort(dur.begin(), dur.end());
-    if (!ent.empty() && !se.empty() && !we.empty())
-      snprintf(last_tl, sizeof last_tl, "entry max %.1f | stream end p10 %.1f p50 %.1f max %.1f | end max %.1f | "
-               "stream dur p50 %.1f", ent.back(), se[se.size() / 10], se[se.size() / 2], se.back(), we.back(),
-               dur[dur.size() / 2]);
+    if (!ent.empty() && !se.empty() && !we.empty()) {
+      int o = snprintf(last_tl, sizeof last_tl, "entry max %.1f | stream end p10 %.1f p50 %.1f max %.1f | end max %.1f | "
+                       "stream dur p50 %.1f", ent.back(), se[se.size() / 10], se[se.size() / 2], se.back(), we.back(),
+                       dur[dur.size() / 2]);
+      // per XCC (HW_REG_XCC_ID): stream end p50 / max and wave end max; then the last wave's stream end, end, items
+      std::vector<double> xs[16], xe[16];
+      int last = -1;
+      for (int w = 0; w < nw; ++w) {
+        const uint64_t* e = q.data() + 8 * w;
+        if (!e[4] || !e[0] || !e[1]) continue;
+        const int x = (int)((e[7] >> 32) & 15);
+        xs[x].push_back((e[0] - t0) / 100.0); xe[x].push_back((e[1] - t0) / 100.0);
+        if (last < 0 || e[1] > q[8 * last + 1]) last = w;
+      }
+      o += snprintf(last_tl + o, sizeof last_tl - o, "\n      per XCC stream end p50/max, end max:");
+      for (int x = 0; x < 16; ++x) {
+        if (xs[x].empty()) continue;
+        std::sort(xs[x].begin(), xs[x].end()); std::sort(xe[x].begin(), xe[x].end());
+        o += snprintf(last_tl + o, sizeof last_tl - o, " x%d %.1f/%.1f,%.1f", x, xs[x][xs[x].size() / 2], xs[x].back(),
+                      xe[x].back());
+      }
+      if (last >= 0) {
+        const uint64_t* e = q.data() + 8 * last;
+        double wsm = 0; uint64_t wit = 0;  // its workgroup's last stream end and items
+        for (int v = 0; v < kCrcWaves; ++v) {
+          const uint64_t* f = q.data() + 8 * ((last / kCrcWaves) * kCrcWaves + v);
+          if (f[0]) wsm = std::max(wsm, (f[0] - t0) / 100.0);
+          wit += f[2];
+        }
+        o += snprintf(last_tl + o, sizeof last_tl - o, "\n      last wave w%d (XCC %d, HW_ID %08lx): stream end %.1f, end "
+                      "%.1f, items %lu; its workgroup: last stream end %.1f, items %lu", last, (int)((e[7] >> 32) & 15),
+                      (unsigned long)(e[7] & 0xffffffffu), (e[0] - t0) / 100.0, (e[1] - t0) / 100.0,
+                      (unsigned long)e[2], wsm, (unsigned long)wit);
+      }
+    }
     return f.empty() ? 0.0 : f[f.size() / 2];
   };
   int run_reps = reps;            // 0: run() launches once, untimed (seqk)
@@ -279,10 +310,10 @@ int main(int argc, char** argv) {
     EmitArgs a = a0;
     if (kb_clock && !a.kb_stamps) a.kb_stamps = seq_stamps ? seq_stamps : clk_st;
     if (run_reps == 0) {
-      kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid);
+      kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid, s.wstart);
       return 0.0f;
     }
-    const float ms = timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid); },
+    const float ms = timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid, s.wstart); },
                   reps, st);
     if (kb_clock && a.kb_stamps == clk_st) last_mhz = clock_of(clk_st, grid * kCrcWaves);
     return ms;
@@ -444,7 +475,7 @@ int main(int argc, char** argv) {
   const float as = timeit([&] {
     hipMemsetAsync(&s.misc[M_DONE_CRC], 0, 8, st);  // the last workgroup finalizes
     k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
-                                          s.misc, 0ull, nblocks, (uint32_t)cus);
+                                          s.misc, 0ull, nblocks, (uint32_t)cus, s.wstart);
   }, reps, st);
   printf("k_crc + finalize %.4f ms\n", as);
   {
@@ -459,7 +490,8 @@ int main(int argc, char** argv) {
       return timeit([&] {
         kern<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
                                                               s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.epoch,
-                                                              ctx->tabs.initc, s.chase_direct, 0ull);
+                                                              ctx->tabs.initc, s.chase_direct, 0ull, s.wstart,
+                                                              (uint32_t)cus * kCrcWaves);
         ++s.epoch;
       }, reps, st);
     };
@@ -479,7 +511,8 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&stp, nwg * 32));
       for (int rep = 0; rep < 3; ++rep) {
         k_chase<32><<<(uint32_t)nwg, 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags, s.srec, s.frag_cap,
-                                                  s.lb, stp, s.misc, s.epoch, ctx->tabs.initc, s.chase_direct, 0ull);
+                                                  s.lb, stp, s.misc, s.epoch, ctx->tabs.initc, s.chase_direct, 0ull,
+                                                  s.wstart, (uint32_t)cus * kCrcWaves);
         ++s.epoch;
         CK(hipStreamSynchronize(st));
       }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 GPU runs (one gpurun call): STEPS picks from
-#   tests   the -m gpu suite (TESTS selects files, default the whole suite)
+#   tests   the -m gpu suite (TESTS selects files, default the whole suite; PYK a -k expression)
 #   smoke   __graft_entry__.smoke()
 #   bench   bench.py exactly as the driver runs it (config B, --warmup 5 --steps 20)
 #   kb      tools/kbench default mode on config B and C (pipeline and per-kernel times, k_chase phase stamps)
@@ -22,7 +22,7 @@ KERNEL=${KERNEL:-k_crc}
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
 if has tests; then
   echo "== tests $(date +%T)"
-  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v --timeout 150 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1 || { tail -40 "$OUT/gpu_tests.log"; exit 1; }
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu ${PYK:+-k "$PYK"} -x -v --timeout 150 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1 || { tail -40 "$OUT/gpu_tests.log"; exit 1; }
   tail -1 "$OUT/gpu_tests.log"
 fi
 if has smoke; then
