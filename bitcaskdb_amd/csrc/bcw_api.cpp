@@ -513,6 +513,10 @@ int bcw_ctx_set_option(bcw_ctx* c, int option, uint64_t value) {
     case BCW_OPT_DECODE_PATH:    // retired options (bcw.h): only their one remaining value is accepted
     case BCW_OPT_DECODE_CHUNKS:
       return value == 1 ? BCW_OK : BCW_E_INVAL;
+    case BCW_OPT_FILTER_SNAPSHOT:
+      if (value > 1) return BCW_E_INVAL;
+      c->filter_snapshot = value != 0;
+      return BCW_OK;
     case BCW_OPT_TEST_ABORT_WAIT: {  // fault injection: refused unless the process opted in (BCW_TEST_HOOKS=1)
       const char* hooks = getenv("BCW_TEST_HOOKS");
       if (!hooks || strcmp(hooks, "1") != 0 || value > 0xffffffffull) return BCW_E_INVAL;

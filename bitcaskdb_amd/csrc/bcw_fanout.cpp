@@ -204,13 +204,25 @@ int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const 
   *n_done = 0;
   if (!n_src) return BCW_OK;
 
-  // the filter snapshot: the index's entries that point into the sources, split by fid
+  // A context on the index's device filters against the index itself (read-only: nothing modifies it during the
+  // call; its own stream's work is drained first). The others filter against a snapshot: the index's entries that
+  // point into the sources, split by fid, each source's slice loaded into a staging index on that context.
+  bcw_ctx* const ixc = index_ctx(ix);
+  if (!ixc) return BCW_E_INVAL;
+  bool any_remote = false;
+  for (uint32_t w = 0; w < n_ctx; ++w) any_remote |= ctxs[w]->device != ixc->device || ctxs[w]->filter_snapshot;
+  {
+    DeviceGuard dg(ixc->device);
+    if (!dg.ok || hipStreamSynchronize(ixc->cur) != hipSuccess) return BCW_E_HIP;
+  }
   std::vector<uint64_t> fids(n_src);
   for (uint64_t k = 0; k < n_src; ++k) fids[k] = srcs[k].fid;
   Entries snap;
   uint64_t sn = 0, skb = 0;
-  int rc = ix_export(ix, fids.data(), n_src, snap, &sn, &skb);
-  if (rc != BCW_OK) return rc;
+  if (any_remote) {
+    const int rc = ix_export(ix, fids.data(), n_src, snap, &sn, &skb);
+    if (rc != BCW_OK) return rc;
+  }
   std::vector<uint64_t> by(sn);  // entry indices grouped by fid
   std::iota(by.begin(), by.end(), 0ull);
   std::stable_sort(by.begin(), by.end(), [&](uint64_t a, uint64_t b) { return snap.f[a] < snap.f[b]; });
@@ -225,8 +237,20 @@ int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const 
 
   auto worker = [&](uint32_t w) {
     bcw_ctx* c = ctxs[w];
+    const bool direct = c->device == ixc->device && !c->filter_snapshot;
     Staging stg;
     Entries mine;
+    uint64_t* d_cnt = nullptr;  // (direct) the filter's counters
+    struct FreeCnt {
+      bcw_ctx* c;
+      uint64_t*& p;
+      ~FreeCnt() {
+        if (p) {
+          DeviceGuard dg(c->device);
+          (void)hipFree(p);
+        }
+      }
+    } free_cnt{c, d_cnt};
     for (uint64_t k = w; k < n_src; k += n_ctx) {
       const bcw_compact_src& S = srcs[k];
       bcw_encode_params p = *dst;
@@ -236,8 +260,13 @@ int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const 
       // this source's slice of the snapshot, loaded into the staging index
       auto lo = std::lower_bound(by.begin(), by.end(), S.fid, [&](uint64_t e, uint64_t f) { return snap.f[e] < f; });
       auto hi = std::upper_bound(lo, by.end(), S.fid, [&](uint64_t f, uint64_t e) { return f < snap.f[e]; });
-      const uint64_t m = (uint64_t)(hi - lo);
-      int r = stg.ready(c, m + 16, 64 * m + 4096);
+      const uint64_t m = direct ? 0 : (uint64_t)(hi - lo);
+      int r = BCW_OK;
+      if (direct && !d_cnt) {
+        DeviceGuard dg(c->device);
+        r = dg.ok && hipMalloc(&d_cnt, kIxCounters * sizeof(uint64_t)) == hipSuccess ? BCW_OK : BCW_E_HIP;
+      }
+      if (!direct) r = stg.ready(c, m + 16, 64 * m + 4096);
       if (r == BCW_OK && m) {
         mine.room(m, 0);
         mine.k.clear();
@@ -262,7 +291,9 @@ int bcw_compact_wals(bcw_index* ix, bcw_ctx* const* ctxs, uint32_t n_ctx, const 
         r = dg.ok ? sync_decode(c, S.data, dp, dres) : BCW_E_HIP;
         if (r == BCW_OK) r = ensure_keep(c, c->d_tab.capacity);
         if (r == BCW_OK)
-          r = bcw_compact_filter_async(stg.ix, c->d_seg, &dp, &c->d_tab, c->d_result, S.fid, c->d_keep, c->d_ires);
+          r = direct ? ix_filter_on(ix, c, c->d_seg, &dp, &c->d_tab, c->d_result, S.fid, c->d_keep, d_cnt, c->d_ires)
+                     : bcw_compact_filter_async(stg.ix, c->d_seg, &dp, &c->d_tab, c->d_result, S.fid, c->d_keep,
+                                                c->d_ires);
         if (r == BCW_OK && (hipMemcpyAsync(&filt[k], c->d_ires, sizeof filt[k], hipMemcpyDeviceToHost, c->cur) !=
                                 hipSuccess ||
                             hipStreamSynchronize(c->cur) != hipSuccess))

@@ -951,6 +951,33 @@ int ix_export(bcw_index* x, const uint64_t* h_fids, uint64_t n_fids, IxSink& sin
 }
 }  // namespace bcw
 
+namespace bcw {
+int ix_filter_on(bcw_index* x, bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_params* p,
+                 const bcw_record_table* d_table, const bcw_decode_result* d_result, uint64_t src_fid, uint8_t* d_keep,
+                 uint64_t* d_cnt, bcw_index_result* d_out) {
+  static_assert(C_NUM <= kIxCounters, "the per-call counters hold every index counter");
+  if (!x || !c || !p || !d_table || !d_result || !d_keep || !d_cnt || p->mode != BCW_MODE_RECORD ||
+      c->device != x->ctx->device)
+    return BCW_E_INVAL;
+  if (!c->s.frags || !d_table->foff || !d_table->key_len || !d_table->first_frag || !d_table->emit_frag ||
+      !d_table->hdr_size)
+    return BCW_E_INVAL;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
+  const uint64_t rows = d_table->capacity;
+  hipStream_t st = c->cur;
+  // the index's counters (its overflow flag included), then this call's own zeroed
+  (void)hipMemcpyAsync(d_cnt, x->cnt, C_NUM * sizeof(uint64_t), hipMemcpyDeviceToDevice, st);
+  (void)hipMemsetAsync(d_cnt + C_NIN, 0, 3 * sizeof(uint64_t), st);
+  const Src s = table_src(c, d_seg, p, d_table, SRC_RECORD);
+  if (rows)
+    k_ix_filter<<<(uint32_t)((rows + 255) / 256), 256, 0, st>>>(s, rows, d_result, c->frag_gen, x->slots, x->cap - 1,
+                                                                 x->arena, src_fid, d_keep, d_cnt);
+  if (d_out) k_ix_result<<<1, 1, 0, st>>>(d_cnt, d_out);
+  return hipGetLastError() == hipSuccess ? BCW_OK : BCW_E_HIP;
+}
+}  // namespace bcw
+
 extern "C" {
 
 int bcw_index_create(bcw_ctx* c, uint64_t keys, uint64_t arena_bytes, bcw_index** out) {

@@ -187,6 +187,13 @@ struct DeviceGuard {
 
 // The context an index was created on (bcw_index.hip): the sync entry points refuse an index of another context.
 bcw_ctx* index_ctx(const bcw_index* ix);
+// doFilter (bcw_compact_filter_async) of context c's latest decode against index x, on c's stream, with the call's
+// counters in d_cnt (kIxCounters words of c's device): another context on the index's device filters against the
+// index itself, read-only, while no call modifies it (bcw_compact_wals).
+constexpr int kIxCounters = 16;
+int ix_filter_on(bcw_index* x, bcw_ctx* c, const uint8_t* d_seg, const bcw_decode_params* p,
+                 const bcw_record_table* d_table, const bcw_decode_result* d_result, uint64_t src_fid, uint8_t* d_keep,
+                 uint64_t* d_cnt, bcw_index_result* d_out);
 
 // Host-side table builders (bcw_api.cpp).
 void build_initc(uint32_t* initc);
@@ -255,6 +262,7 @@ struct bcw_ctx {
   uint32_t last_start_off = 0;
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // BCW_OPT_CHASE_DIRECT
   uint64_t test_abort_wg = 0;                    // BCW_OPT_TEST_ABORT_WAIT (one-shot)
+  bool filter_snapshot = false;                  // BCW_OPT_FILTER_SNAPSHOT (bcw_compact_wals)
   uint64_t last_nfrag_cap = 0;
   bcw::Prof prof;
 };

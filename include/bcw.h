@@ -198,11 +198,16 @@ const char* bcw_kernel_name(int kernel_id);
  *                         process runs with the environment variable BCW_TEST_HOOKS=1 (else BCW_E_INVAL). In the
  *                         NEXT decode on the context, the k_chase workgroup value - 1 gives up its predecessor wait
  *                         at once (0: none, the default), as a wait that ran past its 200 ms bound would; that decode
- *                         reports BCW_ERR_INTERNAL with no rows. One-shot. */
+ *                         reports BCW_ERR_INTERNAL with no rows. One-shot.
+ *   BCW_OPT_FILTER_SNAPSHOT  bcw_compact_wals: 1 = this context filters its sources against a staging copy of the
+ *                         index entries that point into them (the path of a context on another device), even when it
+ *                         shares the index's device; 0 (default) = a context on the index's device filters against the
+ *                         index itself. Both give the same keep masks. */
 #define BCW_OPT_CHASE_DIRECT 1
 #define BCW_OPT_DECODE_PATH 2
 #define BCW_OPT_DECODE_CHUNKS 3
 #define BCW_OPT_TEST_ABORT_WAIT 4
+#define BCW_OPT_FILTER_SNAPSHOT 5
 #define BCW_CHASE_DIRECT_MAX 1024
 /* the largest segment a decode accepts (2^24 blocks of 32 KiB: 512 GiB, beyond one MI355X's 288 GB of HBM);
  * bcw_decode_segment(_async) returns BCW_E_INVAL above it */

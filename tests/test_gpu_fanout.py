@@ -207,10 +207,23 @@ def _oracle_compact(srcs, oc, dst_base):
     return rd, rh, outs
 
 
-@pytest.mark.parametrize("nctx", [2, 3])
-def test_compact_fanout_vs_oracle(ctx, ctx2, ctx3, nctx):
+@pytest.fixture
+def snapshot_ctx(ctx2, ctx3):
+    """sets BCW_OPT_FILTER_SNAPSHOT on ctx2 / ctx3 for one test: they then filter against a staging snapshot of the
+    index, the path of a context on another device (the box has one GPU), and back to the direct filter after"""
+    def use(on: bool):
+        for c in (ctx2, ctx3):
+            c.set_option(L.OPT_FILTER_SNAPSHOT, int(on))
+    yield use
+    use(False)
+
+
+@pytest.mark.parametrize("nctx,snapshot", [(2, False), (3, False), (2, True), (3, True)])
+def test_compact_fanout_vs_oracle(ctx, ctx2, ctx3, nctx, snapshot, snapshot_ctx):
     """5 sources appended to one dst / hint pair: the same bytes, offsets and kept counts as the oracle's serial
-    doCompactionWork, and as the device's serial compact_one_wal_filtered loop"""
+    doCompactionWork, and as the device's serial compact_one_wal_filtered loop; the contexts filter against the index
+    itself (on its device) or against a staging snapshot of it (the path of another device)"""
+    snapshot_ctx(snapshot)
     srcs, ents, oc, later = _compaction_setup(21, 5)
     rd, rh, outs = _oracle_compact(srcs, oc, BASE + 10)
     assert all(o[0] == 0 for o in outs)
@@ -229,9 +242,12 @@ def test_compact_fanout_vs_oracle(ctx, ctx2, ctx3, nctx):
     assert [k for _, k in ser] == [k for _, k in res]
 
 
-def test_compact_fanout_source_error(ctx, ctx2):
+@pytest.mark.parametrize("snapshot", [False, True])
+def test_compact_fanout_source_error(ctx, ctx2, snapshot, snapshot_ctx):
     """a CRC failure in the third source: the sources before it and its rows before the bad fragment are
-    appended, the error is the serial path's, the later sources are not appended"""
+    appended, the error is the serial path's, the later sources are not appended (ctx2 filtering directly or
+    against a snapshot)"""
+    snapshot_ctx(snapshot)
     srcs, ents, oc, later = _compaction_setup(22, 5)
     fid, data = srcs[2]
     srcs[2] = (fid, _corrupt(data, 0.5))

@@ -169,25 +169,24 @@ def test_config_e_compaction_2m_rebase(ctx):
     np.testing.assert_array_equal(goffs[:n], offs[:n])
 
 
+@pytest.mark.timeout(600)
 def test_config_e_full_size_realistic_chunks(ctx):
     """config E at its full size, the realistic compaction: 10,000,000 config-E records (NsSize
     20, 100 B keys, 4 KiB values) in ten source WALs of 1,000,000, each re-encoded with a seeded 70 % keep mask
     against a dst baseTime 500,000 s below the source's and appended at the running wal_pos / hint_pos (one dst WAL
     of ~29.6 GB, one hint WAL of ~0.9 GB, as doCompactionWork's loop appends source after source,
     compaction.go:201-211). Every chunk's appended dst bytes, hint bytes and returned offsets equal
-    oc_compact_append's on writers opened at the same positions (compaction.go:294-327, hint.go:32-48)."""
+    oc_compact_append's on writers opened at the same positions (compaction.go:294-327, hint.go:32-48). The device
+    encodes run in order; the oracle's checks run on 4 host threads beside them (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     dst_base = BASE - 500_000
-    wal_pos = hint_pos = 40
-    total_in = total_kept = 0
-    rng = np.random.default_rng(2026)
-    for k in range(10):
-        src = np.frombuffer(O.synth(1 << 40, 1_000_000, 900 + k, 20, 100, 4096, 0, BASE), dtype=np.uint8)
-        keep = (rng.random(1_000_000) < 0.7).astype(np.uint8)
+
+    def check(k, src, keep, wal_pos, hint_pos, res, wal, hb, goffs):
         dst, hint = O.Writer(dst_base, dst_base, at=wal_pos), O.Writer(dst_base, dst_base, at=hint_pos)
         ec, er, nin, offs = O.compact_append(dst, hint, 31, src, 40, BASE, dst_base, 20, 20, keep)
         assert ec == 0 and nin == 1_000_000, (k, ec, er, nin)
-        res, wal, hb, goffs = ctx.encode(src, L.ENC_COMPACT, 40, dst_base, 31, wal_pos, hint_pos, 20, 20, keep)
-        assert res.err_class == 0 and res.n_in == nin and res.n_written == int(keep.sum()), k
+        assert res.n_in == nin and res.n_written == int(keep.sum()), k
         assert (res.wal_end, res.hint_end) == (dst.size(), hint.size()), k
         ref = dst.data()
         assert len(wal) == len(ref), (k, len(wal), len(ref))
@@ -195,11 +194,24 @@ def test_config_e_full_size_realistic_chunks(ctx):
         assert bad.size == 0, f"chunk {k}: dst WAL differs at file offset {wal_pos + int(bad[0])}"
         assert hb == hint.data(), f"chunk {k}: hint WAL differs"
         np.testing.assert_array_equal(goffs[:nin], offs[:nin])
-        wal_pos, hint_pos = res.wal_end, res.hint_end
-        total_in += nin
-        total_kept += int(keep.sum())
-        del src, dst, hint, ref, wal, hb
-    assert total_in == 10_000_000 and wal_pos > 29_000_000_000
+        return nin, int(keep.sum())
+
+    wal_pos = hint_pos = 40
+    rng = np.random.default_rng(2026)
+    futs = []
+    with ThreadPoolExecutor(4) as pool:
+        for k in range(10):
+            src = np.frombuffer(O.synth(1 << 40, 1_000_000, 900 + k, 20, 100, 4096, 0, BASE), dtype=np.uint8)
+            keep = (rng.random(1_000_000) < 0.7).astype(np.uint8)
+            res, wal, hb, goffs = ctx.encode(src, L.ENC_COMPACT, 40, dst_base, 31, wal_pos, hint_pos, 20, 20, keep)
+            assert res.err_class == 0, (k, res.err_class)
+            futs.append(pool.submit(check, k, src, keep, wal_pos, hint_pos, res, wal, hb, goffs))
+            wal_pos, hint_pos = res.wal_end, res.hint_end
+            del src, wal, hb
+            if len(futs) >= 4:  # (at most 4 chunks' buffers alive at once)
+                futs[-4].result()
+        done = [f.result() for f in futs]
+    assert sum(d[0] for d in done) == 10_000_000 and wal_pos > 29_000_000_000
 
 
 def test_config_b_second_context(ctx_path, config_b):

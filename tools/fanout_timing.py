@@ -84,11 +84,21 @@ def main():
     fan([ctx])  # warm: scratch and pinned staging of both contexts
     fan([ctx, ctx2])
     serial()
-    t = {"serial_compact_segment": [], "fanout_1ctx": [], "fanout_2ctx": []}
+    def snap(on):
+        for c in (ctx, ctx2):
+            c.set_option(L.OPT_FILTER_SNAPSHOT, int(on))
+
+    snap(True)
+    fan([ctx, ctx2])  # (warm the staging indexes)
+    snap(False)
+    t = {"serial_compact_segment": [], "fanout_1ctx": [], "fanout_2ctx": [], "fanout_2ctx_snapshot": []}
     for _ in range(3):
         t["serial_compact_segment"].append(serial())
         t["fanout_1ctx"].append(fan([ctx]))
         t["fanout_2ctx"].append(fan([ctx, ctx2]))
+        snap(True)
+        t["fanout_2ctx_snapshot"].append(fan([ctx, ctx2]))
+        snap(False)
     src_bytes = sum(int(d.size) for d, _ in srcs)
     line = {"what": "bcw_compact_wals: %d x 1 GiB config-B sources, all rows kept, outputs to host" % nsrc,
             "src_bytes": src_bytes,
