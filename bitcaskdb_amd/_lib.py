@@ -125,6 +125,7 @@ OPT_DECODE_CHUNKS = 3  # bcw_ctx_set_option: retired (only 1 accepted)
 OPT_DECODE_PATH = 2  # bcw_ctx_set_option: retired (only 1 accepted: k_chase + k_crc)
 OPT_TEST_ABORT_WAIT = 4  # bcw_ctx_set_option: fault injection (needs BCW_TEST_HOOKS=1): the next decode's k_chase workgroup value-1 gives up its wait
 OPT_FILTER_SNAPSHOT = 5  # bcw_ctx_set_option: bcw_compact_wals filters this context's sources against a staging snapshot
+OPT_XCD_BALANCE = 6  # bcw_ctx_set_option: k_crc's stream split over the XCDs by their measured rates (default 1)
 E_IO = -6
 ENC_COMPACT, ENC_HINT = 0, 1
 ENC_ERR_NONE, ENC_ERR_SRC, ENC_ERR_EXPIRE, ENC_ERR_PANIC, ENC_ERR_TABLE, ENC_ERR_STALE = 0, 1, 2, 3, 4, 5

@@ -337,6 +337,7 @@ static void free_scratch(Scratch& s) {
   (void)hipFree(s.srec);
   (void)hipFree(s.fok);
   (void)hipFree(s.wstart);
+  (void)hipFree(s.xbal);
   (void)hipFree(s.misc);
   s = Scratch{};
 }
@@ -412,6 +413,7 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
             hipMalloc(&s.srec, (fc + 4) * sizeof(uint4)) == hipSuccess &&
             hipMalloc(&s.fok, fc) == hipSuccess &&
             hipMalloc(&s.wstart, ((size_t)c->num_cus * kCrcWaves + 1) * 4) == hipSuccess &&
+            hipMalloc(&s.xbal, sizeof(XBal)) == hipSuccess &&
             hipMalloc(&s.misc, 16 * sizeof(uint64_t)) == hipSuccess;
   if (!ok) { free_scratch(s); return BCW_E_NOMEM; }
   s.nblocks_cap = nb;
@@ -424,7 +426,10 @@ static int ensure_scratch(bcw_ctx* c, uint64_t nblocks, uint64_t frag_cap) {
   // misc[15] (the first unknown-type fragment, an atomicMin in k_chase) starts at UINT64_MAX; every decode's
   // finalizer resets it for the next one
   // misc[0] (first bad record) and misc[14] (first CRC failure) start at UINT64_MAX too
-  if (hipMemsetAsync(s.lb, 0, nwg * 8, c->cur) != hipSuccess || hipMemsetAsync(s.lbe, 0, nwg * 8, c->cur) != hipSuccess ||
+  XBal xb{};  // equal weights to begin with; k_crc's finalize adapts them decode by decode
+  for (uint32_t y = 0; y < 8; ++y) xb.w[y] = 65536u;
+  if (hipMemcpyHtoDAsync(s.xbal, &xb, sizeof xb, c->cur) != hipSuccess || hipStreamSynchronize(c->cur) != hipSuccess ||
+      hipMemsetAsync(s.lb, 0, nwg * 8, c->cur) != hipSuccess || hipMemsetAsync(s.lbe, 0, nwg * 8, c->cur) != hipSuccess ||
       hipMemsetAsync(s.misc, 0, 16 * sizeof(uint64_t), c->cur) != hipSuccess ||
       hipMemsetAsync(s.misc + 14, 0xff, 2 * sizeof(uint64_t), c->cur) != hipSuccess ||
       hipMemsetAsync(s.misc, 0xff, sizeof(uint64_t), c->cur) != hipSuccess) {
@@ -513,6 +518,10 @@ int bcw_ctx_set_option(bcw_ctx* c, int option, uint64_t value) {
     case BCW_OPT_DECODE_PATH:    // retired options (bcw.h): only their one remaining value is accepted
     case BCW_OPT_DECODE_CHUNKS:
       return value == 1 ? BCW_OK : BCW_E_INVAL;
+    case BCW_OPT_XCD_BALANCE:
+      if (value > 1) return BCW_E_INVAL;
+      c->s.xbal_on = (uint32_t)value;
+      return BCW_OK;
     case BCW_OPT_FILTER_SNAPSHOT:
       if (value > 1) return BCW_E_INVAL;
       c->filter_snapshot = value != 0;

@@ -202,6 +202,90 @@ __device__ __forceinline__ void put_frag(Frag* __restrict__ frags, uint4* __rest
 // after the block's last Full/Last fragment (the whole block when it has none).
 constexpr uint32_t kSumHasE = 1u << 16;
 
+// The 8 class weights of XBal (lane k of xw holds class k's: 65536 + 256 d_k, |d_k| < 128) as uniform scalars: the
+// d_k packed in bytes, their prefix sums in 16-bit fields. A class is picked by shifts (selects or an indexed array
+// became a lookup table in scratch memory, which cost k_chase ~20 us).
+struct ClassW {
+  uint64_t pw;        // byte k: d_k
+  uint64_t pp0, pp1;  // 16-bit field k (of pp0 for k < 4, of pp1 for k >= 4): d_0 + ... + d_{k-1}
+  uint64_t p8;        // all weights
+  __device__ __forceinline__ uint64_t weight(uint32_t y) const {
+    return (uint64_t)(65536 + 256 * (int64_t)(int8_t)(uint8_t)(pw >> (8u * y)));
+  }
+  __device__ __forceinline__ uint64_t prefix(uint32_t y) const {
+    const uint64_t f = (y < 4u ? pp0 : pp1) >> (16u * (y & 3u));
+    return (uint64_t)(65536 * (int64_t)y + 256 * (int64_t)(int16_t)(uint16_t)f);
+  }
+  // the classes k >= 1 whose prefix lies at or below x
+  __device__ __forceinline__ uint32_t classes_below(double x) const {
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < 8; ++k) n += (double)prefix(k) <= x ? 1u : 0u;
+    return n;
+  }
+};
+// k_crc's wave boundaries: range r (workgroup r, class r % 8) has its class's weight; wave v = 16 r + j starts at
+// the fraction num16(v) / den16 of the segment after start_off, num16(v) = 16 x (weights of ranges < r) +
+// weight(r % 8) j, rounded down to 1 KiB: P(v) = 1024 floor(num16(v) C / den16), C = floor(L / 1024) (exact in 64 bits
+// up to 512 GiB). Its inverse is exact too: the first v with P(v) >= x is the first with num16(v) >= N =
+// ceil(ceil(x / 1024) den16 / C).
+// floor(a / b) for a < 2^62, 0 < b < 2^32, from a floating-point estimate (rb = 1 / b) and exact steps: a 64-bit
+// integer division is a ~100-instruction sequence, and k_chase's table pass ran 8 k cycles longer with four of them
+__device__ __forceinline__ uint64_t div_floor(uint64_t a, uint64_t b, double rb) {
+  uint64_t q = (uint64_t)((double)a * rb);
+  while (q * b > a) --q;
+  while ((q + 1) * b <= a) ++q;
+  return q;
+}
+struct WavePart {
+  ClassW cw;
+  uint64_t L, nwaves, round16, den16, C;
+  double rden, rC;
+  __device__ __forceinline__ WavePart(const ClassW& c, uint64_t L_, uint64_t nwaves_) : cw(c), L(L_), nwaves(nwaves_) {
+    const uint32_t G = (uint32_t)(nwaves / kCrcWaves);
+    round16 = 16ull * cw.p8;
+    den16 = round16 * (G / 8u) + 16ull * cw.prefix(G % 8u);
+    C = L / 1024u;
+    rden = 1.0 / (double)den16;
+    rC = C ? 1.0 / (double)C : 0.0;
+  }
+  __device__ __forceinline__ uint64_t P(uint64_t v) const {
+    if (v >= nwaves) return L;
+    const uint64_t r = v / kCrcWaves;
+    const uint32_t y = (uint32_t)(r % 8u);
+    const uint64_t num16 = round16 * (r / 8u) + 16ull * cw.prefix(y) + cw.weight(y) * (v % kCrcWaves);
+    return 1024u * div_floor(num16 * C, den16, rden);
+  }
+  __device__ __forceinline__ uint64_t first_at(uint64_t x) const {
+    if (C == 0) return x == 0 ? 0 : nwaves;  // (a segment under 1 KiB: every boundary but the last at 0)
+    const uint64_t X = (x + 1023u) / 1024u, N = div_floor(X * den16 + C - 1, C, rC);
+    const uint32_t q = (uint32_t)N / (uint32_t)round16;  // (N <= den16 + 1 < 2^32)
+    const uint64_t rem = N - (uint64_t)q * round16;
+    uint32_t y = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < 8; ++k) y += 16ull * cw.prefix(k) <= rem ? 1u : 0u;
+    const uint64_t wy = cw.weight(y), base = 16ull * cw.prefix(y);
+    const uint32_t jj = (uint32_t)(rem - base + wy - 1) / (uint32_t)wy;  // 0..16 (16: the next range's first wave)
+    const uint64_t v = ((uint64_t)q * 8u + y) * kCrcWaves + jj;
+    return v < nwaves ? v : nwaves;
+  }
+};
+
+__device__ __forceinline__ ClassW class_weights(uint32_t xw) {
+  ClassW c{0, 0, 0, 0};
+  int64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t d = ((int64_t)__builtin_amdgcn_readlane(xw, k) - 65536) / 256;
+    c.pw |= (uint64_t)(uint8_t)(int8_t)d << (8 * k);
+    if (k < 4) c.pp0 |= (uint64_t)(uint16_t)(int16_t)acc << (16 * k);
+    else c.pp1 |= (uint64_t)(uint16_t)(int16_t)acc << (16 * (k - 4));
+    acc += d;
+  }
+  c.p8 = (uint64_t)(65536 * 8 + 256 * acc);
+  return c;
+}
+
 // ABL: ablation bits for tools/kbench only (0 in the product): 1 no predecessor sum, 2 no table writes,
 // 16 phase cycles (chase, sum, writes; s_memtime) summed into misc[7..9], 32 per-workgroup wall-clock stamps (entry,
 // chase end, sum end, end) into lbe[4 wg ..] (kbench passes a buffer of its own; direct-sum sizes only)
@@ -214,7 +298,8 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                               uint64_t* __restrict__ lbe, uint64_t* __restrict__ misc,
                                               uint64_t epoch, const uint32_t* __restrict__ initc,
                                               uint32_t direct_max, uint64_t test_abort_wg,
-                                              uint32_t* __restrict__ wstart, uint32_t nwaves) {
+                                              uint32_t* __restrict__ wstart, uint32_t nwaves,
+                                              XBal* __restrict__ xb, uint32_t xb_on) {
   // {crc, start | len << 16} and type of each lane's first 64 headers: 36 KiB, so a k_chase workgroup still fits beside
   // a k_crc workgroup (which leaves 44 KiB of the CU's LDS since round 4) when another segment's decode is in flight.
   // A block with more headers is chased a second time from the 65th on when its table entries are written (16 held
@@ -224,6 +309,8 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   __shared__ uint32_t s_hold[kHold][2][64];
   __shared__ uint8_t s_type[kHold][64];
   const uint32_t lane = threadIdx.x;
+  // k_crc's per-XCD split (XBal): the range weight of each class, requested now, used after the chase
+  const uint32_t xw = lane < 8u ? (xb_on ? xb->w[lane] : 65536u) : 0u;
   const uint64_t tc0 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
   if ((ABL & 32) && threadIdx.x == 0) lbe[4 * blockIdx.x] = wall_clock64();
   // the workgroup id orders the look-back: workgroups are dispatched in id order (within each XCD), so one only waits
@@ -231,6 +318,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
   // (Round 4 took tickets from one atomic counter: its 512 returning atomics on one word ended 5-7 us apart, and the
   // last ticket's chase gated every base: k_chase B 22.1 -> 16.8 us, C 31.3 -> 24.3 us without them, kbench.)
   const uint64_t wg = blockIdx.x;
+  if (wg >= (nblocks + 63) / 64) return;  // (the grid is padded to a multiple of 8 workgroups, see launch_decode)
   const uint64_t b = wg * 64 + lane;
   uint32_t bufsize = 0;
   uint64_t boff = 0;
@@ -261,6 +349,7 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
                                  });
   const uint64_t tc1 = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
   if ((ABL & 32) && lane == 0) lbe[4 * wg + 1] = wall_clock64();
+  if (wg == 0 && lane == 0) xb->on = xb_on;
   const uint32_t incl = wave_add_scan(n, lane);
   const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
   const uint32_t incl_e = wave_add_scan(ne, lane);
@@ -399,22 +488,23 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     // header.
     const bool next_hdr = b + 1 < nblocks && seg_len - (boff + kBlock) >= kHdr;
     auto adj = [&](uint32_t k, uint32_t sl_k) { return k + 1u < n || (next_hdr && (sl_k & 0xffffu) + (sl_k >> 16) == kBlock); };
-    // k_crc's wave ranges, balanced by bytes: wave w streams the fragments whose header lies in [P_w, P_w+1),
-    // P_w = start_off + floor(L w / nwaves) (L = seg_len - start_off), so wstart[w] = the first fragment whose header
-    // is at or after P_w. This lane writes the boundaries that fall in its block, walking its headers in order.
+    // k_crc's wave ranges, balanced by bytes: wave w streams the fragments whose header lies in [P_w, P_w+1)
+    // (positions after start_off), so wstart[w] = the first fragment whose header is at or after P_w. This lane writes the boundaries that fall in its block, walking its headers in order.
     // (Whole blocks per wave left 7 of config B's 4096 waves with 9 blocks instead of 8: they ended ~20 us after the
     // median wave, kbench timelines.)
+    // Range r (k_crc's workgroup with ticket r / 8 of XCD r % 8) has weight s_w[r % 8]; wave v = 16 r + j starts at
+    // the fraction (16 x (weights of ranges < r) + s_w[r % 8] j) / (16 x all weights) of the bytes after start_off.
     const uint64_t L = seg_len - start_off, rel = boff - start_off;
-    uint64_t w = (rel * nwaves + L - 1) / L;  // the first boundary at or after the block's start
-    // (the last block also takes P_nwaves = seg_len, which lies at its span's end when L is a multiple of 32 KiB)
-    const uint64_t w_end = b + 1 == nblocks ? (uint64_t)nwaves + 1
-                                            : min((uint64_t)nwaves + 1, ((rel + kBlock) * nwaves + L - 1) / L);
-    uint64_t bw = w < w_end ? (L * w) / nwaves - rel : 0;  // boundary w, block-relative
-    auto bounds_upto = [&](uint64_t hp, uint64_t idx) {  // boundaries at or before the header at hp: idx
+    const WavePart wp(class_weights(xw), L, nwaves);
+    uint64_t w = wp.first_at(rel);
+    // (the last block also takes P_nwaves = L, which lies at its span's end when L is a multiple of 32 KiB)
+    const uint64_t w_end = b + 1 == nblocks ? (uint64_t)nwaves + 1 : wp.first_at(rel + kBlock);
+    uint64_t bw = w < w_end ? wp.P(w) - rel : 0;  // boundary w, block-relative
+    auto bounds_upto = [&](uint64_t hp, uint64_t idx) __attribute__((always_inline)) {  // boundaries at or before hp: idx
       while (w < w_end && bw <= hp) {
         wstart[w] = (uint32_t)(idx < 0xffffffffull ? idx : 0xffffffffull);
         ++w;
-        bw = (L * w) / nwaves - rel;
+        bw = wp.P(w) - rel;
       }
     };
     for (uint32_t k = 0; k < nh; ++k) {
@@ -653,7 +743,8 @@ __device__ __forceinline__ EmitState emit_state(const EmitArgs& A, uint64_t b0, 
 // one lane each.
 // hook(): called once, right after the first chunk's fragment descriptors are requested (the caller issues the
 // next work item's loads there, so they fly beside this item's).
-template <typename Hook>
+// NOSTORE (tools/kbench only): the rows are computed but not stored
+template <bool NOSTORE = false, typename Hook>
 __device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& es, uint64_t f0, uint64_t f1,
                                             uint32_t lane, Hook&& hook) {
   if (f0 >= f1) {
@@ -760,7 +851,9 @@ __device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& 
       uint64_t key_len, val_len, meta_len, expire, aux0, aux1;
       parse_record(A.p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
       const bcw_record_table& tab = A.tab;
-      if (r < tab.capacity) {
+      if (NOSTORE) {
+        if (status == 0xeeu) tab.foff[r] = foff ^ size ^ expire ^ aux0 ^ aux1 ^ key_len ^ val_len ^ meta_len ^ hdr ^ flags ^ etag_off;
+      } else if (r < tab.capacity) {
         tab.foff[r] = foff;
         tab.size[r] = size;
         tab.expire[r] = expire;
@@ -1200,11 +1293,35 @@ struct CrcTail {
   uint32_t tail_panic, nwg_total;
 };
 
+// The next decode's split (XBal), by the last wave of k_crc: every workgroup's stream times are in (the completion
+// counter orders them). Class y's mean stream time T_y against the mean over the classes T: its range weight moves a
+// quarter of the way to w_y T / T_y (kept within 0.8-1.25 of equal), when k_chase used the weights. The times are
+// reset for the next launch.
+__device__ __forceinline__ void xbal_update(XBal* __restrict__ xb, uint32_t lane) {
+  const uint32_t y = lane & 7u;
+  const uint64_t t = __hip_atomic_load(&xb->t[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t n = __hip_atomic_load(&xb->n[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float Ty = n && t ? (float)t / (float)n : 0.0f;
+  const bool all = __ballot(lane < 8u && Ty > 0.0f) == 0xffull && xb->on != 0u;  // every XCD measured
+  float sT = lane < 8u ? Ty : 0.0f;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) sT += __shfl_xor(sT, d, 64);
+  if (lane < 8u) {
+    if (all) {
+      const float wy = (float)xb->w[y] * (1.0f + 0.25f * ((sT / 8.0f) / Ty - 1.0f));
+      const float d = fminf(fmaxf(rintf((wy - 65536.0f) / 256.0f), -51.0f), 64.0f);  // (k_chase's ClassW: 256 steps)
+      xb->w[y] = (uint32_t)(65536 + 256 * (int32_t)d);
+    }
+    xb->t[y] = 0;
+    xb->n[y] = 0;
+  }
+}
+
 // k_crc: one 1024-thread workgroup per CU. Each wave verifies the fragments of its share of the blocks (stream_verify),
 // then takes record-emission items of its workgroup's blocks (emit_chunks); the last wave of the last workgroup
 // writes the segment result (finalize).
 // ABL: tools/kbench ablations (0 in the product): 8 no emission, 32768 no CRC pass (the emission alone), 8388608 every
-// chunk on the fast chain (stream_verify<true>)
+// chunk on the fast chain (stream_verify<true>), 4096 emission without the row stores
 template <int ABL = 0>
 __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__ seg, uint64_t seg_len,
                                                      uint32_t start_off, uint64_t nblocks,
@@ -1214,7 +1331,8 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
                                                      uint32_t tail_panic, uint64_t gen,
                                                      bcw_decode_result* __restrict__ res,
                                                      uint64_t* __restrict__ misc, uint64_t cb0, uint64_t cb1,
-                                                     uint32_t nwg_total, const uint32_t* __restrict__ wstart) {
+                                                     uint32_t nwg_total, const uint32_t* __restrict__ wstart,
+                                                     XBal* __restrict__ xb) {
   // [cb0, cb1): the blocks this launch emits (the whole segment); nwg_total: the workgroups that count towards
   // completion; wstart: each wave's first fragment (k_chase, gridDim.x x kCrcWaves + 1 entries)
   __shared__ __attribute__((aligned(16))) uint32_t lds[kS2Image];
@@ -1222,6 +1340,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   __shared__ uint32_t s_wdone;  // waves of this workgroup done
   __shared__ uint32_t s_eq;     // the workgroup's emission items taken
   __shared__ __attribute__((aligned(16))) uint32_t s_rem[kCrcWaves];  // chunks left per wave [simd][age] (stream_verify)
+  __shared__ uint32_t s_sdone;              // waves of this workgroup whose stream is done
+  __shared__ unsigned long long s_tsum;     // their summed stream times
+  __shared__ uint64_t s_t0;                 // the workgroup's start (wall_clock64)
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1236,21 +1357,11 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   if (tid == 0) {
     s_wdone = 0;
     s_eq = 0;
+    s_sdone = 0;
+    s_tsum = 0;
+    s_t0 = wall_clock64();
     s_tail = CrcTail{ea, res, misc, nblocks, frag_cap, gen, cb0, cb1, tail_panic, nwg_total};
   }
-  const uint64_t nw = (uint64_t)gridDim.x * kCrcWaves;
-  const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
-  // every wave streams the fragments of its 1 / (16 x CUs) share of the blocks (dedicated emission waves measured
-  // slower)
-  // the wave's fragments, balanced by bytes (k_chase's wstart)
-  const uint64_t f0 = wstart[gw];
-  uint64_t f1 = wstart[gw + 1];
-  if (f1 > frag_cap) f1 = frag_cap;
-  if (f0 > f1) f1 = f0;
-  // a k_chase wait gave up (Spin): the bases are unreliable, so no fragment is read and no row written
-  const bool aborted = __builtin_amdgcn_readfirstlane(
-                           (uint32_t)__hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
-  if (aborted) f1 = f0;
   {  // table image -> LDS: all 16 B loads in flight before the first store
     constexpr uint32_t kVec = kS2Image / 4;
     constexpr int kFull = (int)(kVec / kCrcThreads);
@@ -1267,6 +1378,17 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     for (int k2 = 0; k2 < kFull; ++k2) dst[tid + k2 * kCrcThreads] = v[k2];
   }
   __syncthreads();
+  // every wave streams the fragments of its share of the segment's bytes: 1 / (16 x CUs), weighted by its
+  // workgroup's class (XBal; k_chase's wstart; dedicated emission waves measured slower)
+  const uint64_t gw = (uint64_t)blockIdx.x * kCrcWaves + wave;
+  const uint64_t f0 = wstart[gw];
+  uint64_t f1 = wstart[gw + 1];
+  if (f1 > frag_cap) f1 = frag_cap;
+  if (f0 > f1) f1 = f0;
+  // a k_chase wait gave up (Spin): the bases are unreliable, so no fragment is read and no row written
+  const bool aborted = __builtin_amdgcn_readfirstlane(
+                           (uint32_t)__hip_atomic_load(&misc[M_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+  if (aborted) f1 = f0;
   if (blockIdx.x == 0 && tid == 0) misc[M_T_CRC0] = wall_clock64();
   const uint32_t nfr = f1 > f0 ? (uint32_t)(f1 - f0) : 0u;
   // ---- record emission: the workgroup's work items (those starting in its blocks), taken from an LDS counter by
@@ -1319,7 +1441,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       const uint64_t mf1 = m.f1 < fcap ? m.f1 : fcap;
       uint64_t nx = ~0ull;
       ItemMeta mn = m;
-      emit_chunks(A, es, m.f0, mf1, lane, [&]() {
+      emit_chunks<(ABL & 4096) != 0>(A, es, m.f0, mf1, lane, [&]() {
         if (taken < max_items) {
           nx = deq();
           mn = item_meta(A, nx, bpw, cb0t, cb1t, lane);
@@ -1331,14 +1453,29 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     n_items += taken;
   };
   if (ABL & 64) emit_items(~0ull);  // (kbench: emission before the stream)
-  if (!(ABL & 32768))
+  if (ABL & 16384) {  // (kbench: the wave's range as 4 consecutive stream_verify calls: the cost of a ring restart)
+    for (uint32_t q = 0; q < 4u; ++q) {
+      const uint32_t a = nfr * q / 4u, b = nfr * (q + 1u) / 4u;
+      stream_verify<(ABL & 8388608) != 0>(seg, seg_len, fok, srec, f0 + a, b - a, lds, lane, misc, s_rem,
+                                          (wave & 3u) * 4u + (wave >> 2),
+                                          reinterpret_cast<const uint8_t*>(tabs.lds_image2));
+    }
+  } else if (!(ABL & 32768))
     stream_verify<(ABL & 8388608) != 0>(seg, seg_len, fok, srec, f0, nfr, lds, lane, misc, s_rem,
                                         (wave & 3u) * 4u + (wave >> 2),
                                         reinterpret_cast<const uint8_t*>(tabs.lds_image2));
   __builtin_amdgcn_s_setprio(0);
+  if (lane == 0) {  // this wave's stream time; the workgroup's last stream adds its workgroup's to its class's (XBal)
+    atomicAdd(&s_tsum, (unsigned long long)(wall_clock64() - s_t0));
+    if (atomicAdd(&s_sdone, 1u) == kCrcWaves - 1u) {
+      const uint32_t c = blockIdx.x & 7u;
+      __hip_atomic_fetch_add(&xb->t[c], (uint64_t)s_tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&xb->n[c], (uint64_t)kCrcWaves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   if (ea.kb_stamps && lane == 0) {  // (kbench: this wave's CRC end and fragments, written now so that nothing of it
                                    // stays live across the emission)
-    uint64_t* q = ea.kb_stamps + 8 * gw;
+    uint64_t* q = ea.kb_stamps + 8 * ((uint64_t)blockIdx.x * kCrcWaves + wave);
     q[0] = wall_clock64();
     q[3] = nfr;
   }
@@ -1375,6 +1512,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   if (gorder != T.nwg_total - 1u) return;
   if (lane == 0) T.misc[M_T_FIN] = wall_clock64();
   finalize(A, T.nblocks, T.frag_cap, T.tail_panic, T.gen, T.res, lane);
+  xbal_update(xb, lane);
 }
 
 __global__ void k_export_frags(const Frag* __restrict__ frags, const uint8_t* __restrict__ fok,
@@ -1403,12 +1541,15 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   hipEvent_t ev = nullptr;
   const uint64_t tail = (p.seg_len - p.start_off) % kBlock;
   const uint32_t tail_panic = (tail > 0 && tail < kHdr) ? 1u : 0u;
-  const uint32_t nb_grid = (uint32_t)((nblocks + 63) / 64);
+  // k_chase's grid padded to a multiple of 8 workgroups (the extra ones return at once) and k_crc's one per CU: the
+  // dispatcher then starts every k_crc on the same XCD, so each workgroup class (blockIdx % 8, XBal) keeps its XCD
+  // from decode to decode
+  const uint32_t nb_grid = (uint32_t)(((nblocks + 63) / 64 + 7) / 8 * 8);
   const EmitArgs ea{d_seg, p.seg_len, p, s.frags, s.fbase, s.rbase, s.bsum, t, s.misc, 0u, nullptr};
   pr.begin(K_CHASE, stream, ev);
   k_chase<0><<<nb_grid, 64, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
                                         s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.epoch, tabs.initc, s.chase_direct,
-                                        s.test_abort_wg, s.wstart, (uint32_t)num_cus * kCrcWaves);
+                                        s.test_abort_wg, s.wstart, (uint32_t)num_cus * kCrcWaves, s.xbal, s.xbal_on);
   s.test_abort_wg = 0;
   pr.end(K_CHASE, stream, ev);
   if ((++s.epoch & 0xffffffull) == 0) {  // 24-bit look-back epochs: clear the words before reuse
@@ -1420,7 +1561,7 @@ hipError_t launch_decode(const uint8_t* d_seg, const bcw_decode_params& p, const
   k_crc<0><<<(uint32_t)num_cus, kCrcThreads, 0, stream>>>(d_seg, p.seg_len, p.start_off, nblocks, s.fbase, s.fok,
                                                          s.srec, s.frag_cap, tabs, ea,
                                                          tail_panic, gen, d_result, s.misc, 0ull, nblocks,
-                                                         (uint32_t)num_cus, s.wstart);
+                                                         (uint32_t)num_cus, s.wstart, s.xbal);
   pr.end(K_CRC, stream, ev);
   return hipGetLastError();
 }

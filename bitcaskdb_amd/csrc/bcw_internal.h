@@ -13,6 +13,19 @@ constexpr uint32_t kHdr = BCW_HEADER_SIZE;   // wal.go:53
 constexpr uint32_t kWin = 128;               // CRC window per lane (bytes)
 constexpr int kWaveLanes = 64;
 
+// k_crc's stream balanced per XCD (bcw_decode.hip): workgroup r streams range r of the segment, and the dispatcher
+// places workgroup r on XCD (r + s) % 8 with the same s every decode (both kernels' grids are multiples of 8), so each
+// class r % 8 is one XCD. The ranges of class y are sized in proportion to its weight, the rate measured by the
+// previous decode on the context (the XCDs of an MI355X stream up to ~6 % apart, kbench per-XCD timelines). Only the
+// work split depends on it, never a result.
+struct XBal {
+  uint32_t w[8];    // byte weight of a range of class y (65536: equal)
+  uint32_t pad0[8];
+  uint64_t t[8];    // k_crc: summed stream times (wall_clock64 ticks) of class y's waves (the finalize resets them)
+  uint64_t n[8];    // their count
+  uint32_t on;      // k_chase used the weights (BCW_OPT_XCD_BALANCE): the finalize updates them only then
+  uint32_t pad[7];
+};
 // One parsed fragment header (wal_iterator.go:62-77), 16 bytes.
 struct Frag {
   uint32_t blk;    // block index within the segment
@@ -76,6 +89,8 @@ struct Scratch {
   uint4* srec = nullptr;       // [frag_cap + 4] stream record per fragment (k_chase -> k_crc, bcw_decode.hip kRecUsual)
   uint8_t* fok = nullptr;      // [frag_cap] CRC verdict per fragment (k_crc; dense: 64 verdicts are one 64 B store)
   uint32_t* wstart = nullptr;  // [CUs x kCrcWaves + 1] each k_crc wave's first fragment (byte-balanced, k_chase)
+  XBal* xbal = nullptr;        // the per-XCD split of k_crc's stream (persists across decodes)
+  uint32_t xbal_on = 1;        // BCW_OPT_XCD_BALANCE
   uint64_t* misc = nullptr;    // [16] device counters (see bcw_decode.hip)
   uint32_t chase_direct = BCW_CHASE_DIRECT_MAX;  // k_chase: direct predecessor sum up to this many workgroups
   uint64_t test_abort_wg = 0;  // BCW_OPT_TEST_ABORT_WAIT for the next launch only (k_chase workgroup + 1; 0: none)

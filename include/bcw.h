@@ -202,12 +202,16 @@ const char* bcw_kernel_name(int kernel_id);
  *   BCW_OPT_FILTER_SNAPSHOT  bcw_compact_wals: 1 = this context filters its sources against a staging copy of the
  *                         index entries that point into them (the path of a context on another device), even when it
  *                         shares the index's device; 0 (default) = a context on the index's device filters against the
- *                         index itself. Both give the same keep masks. */
+ *                         index itself. Both give the same keep masks.
+ *   BCW_OPT_XCD_BALANCE   1 (default): the CRC pass splits the segment over the XCDs in proportion to their stream
+ *                         rates measured by the previous decode on the context; 0: equal bytes per workgroup. Only
+ *                         the work split changes, never a result. */
 #define BCW_OPT_CHASE_DIRECT 1
 #define BCW_OPT_DECODE_PATH 2
 #define BCW_OPT_DECODE_CHUNKS 3
 #define BCW_OPT_TEST_ABORT_WAIT 4
 #define BCW_OPT_FILTER_SNAPSHOT 5
+#define BCW_OPT_XCD_BALANCE 6
 #define BCW_CHASE_DIRECT_MAX 1024
 /* the largest segment a decode accepts (2^24 blocks of 32 KiB: 512 GiB, beyond one MI355X's 288 GB of HBM);
  * bcw_decode_segment(_async) returns BCW_E_INVAL above it */

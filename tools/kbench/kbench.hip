@@ -288,6 +288,22 @@ int main(int argc, char** argv) {
         o += snprintf(last_tl + o, sizeof last_tl - o, " x%d %.1f/%.1f,%.1f", x, xs[x][xs[x].size() / 2], xs[x].back(),
                       xe[x].back());
       }
+      {  // the slowest 5 % of the streams against the rest: their fragments per wave
+        std::vector<std::pair<double, uint64_t>> dv;
+        for (int w = 0; w < nw; ++w) {
+          const uint64_t* e = q.data() + 8 * w;
+          if (e[4] && e[0]) dv.push_back({(double)(e[0] - e[4]) / 100.0, e[3]});
+        }
+        std::sort(dv.begin(), dv.end());
+        if (dv.size() >= 40) {
+          const size_t n5 = dv.size() / 20;
+          double fs = 0, fa = 0;
+          for (size_t i = dv.size() - n5; i < dv.size(); ++i) fs += dv[i].second;
+          for (auto& x : dv) fa += x.second;
+          o += snprintf(last_tl + o, sizeof last_tl - o, "\n      fragments per wave: slowest 5 %% %.0f, all %.0f",
+                        fs / n5, fa / dv.size());
+        }
+      }
       if (last >= 0) {
         const uint64_t* e = q.data() + 8 * last;
         double wsm = 0; uint64_t wit = 0;  // its workgroup's last stream end and items
@@ -310,10 +326,10 @@ int main(int argc, char** argv) {
     EmitArgs a = a0;
     if (kb_clock && !a.kb_stamps) a.kb_stamps = seq_stamps ? seq_stamps : clk_st;
     if (run_reps == 0) {
-      kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid, s.wstart);
+      kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid, s.wstart, s.xbal);
       return 0.0f;
     }
-    const float ms = timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid, s.wstart); },
+    const float ms = timeit([&] { kern<<<grid, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, a, 0u, 0ull, dres, s.misc, 0ull, nblocks, grid, s.wstart, s.xbal); },
                   reps, st);
     if (kb_clock && a.kb_stamps == clk_st) last_mhz = clock_of(clk_st, grid * kCrcWaves);
     return ms;
@@ -326,6 +342,10 @@ int main(int argc, char** argv) {
       case 8388608: return run(k_crc<8388608>, cus, ea);  // every chunk on the fast chain
       case 8388616: return run(k_crc<8388616>, cus, ea);  // the same without emission
       case 32768: return run(k_crc<32768>, cus, ea);      // emission only (no CRC pass)
+      case 4096: return run(k_crc<4096>, cus, ea);        // emission without row stores
+      case 16384: return run(k_crc<16384>, cus, ea);      // each wave's range as 4 stream_verify calls
+      case 16392: return run(k_crc<16392>, cus, ea);      // the same without emission
+      case 36864: return run(k_crc<36864>, cus, ea);      // emission only, without row stores
       case 99: return run(k_crc<0>, cus, ea_off);
       case 98: { const float r = run(k_crc<0>, cus, ea_st); stamp_report(); return r; }
       default: return run(k_crc<0>, cus, ea);
@@ -390,6 +410,26 @@ int main(int argc, char** argv) {
       printf(" %.0f", ms * 1e3);
     }
     printf("\n");
+    return 0;
+  }
+  if (argc > 3 && std::string(argv[3]) == "xbal") {  // pipelines with the per-XCD split on / off, interleaved
+    const uint64_t nb = (n - 40 + kBlock - 1) / kBlock;
+    std::vector<float> ton, toff;
+    for (int r = 0; r < 7; ++r)
+      for (int on = 0; on <= 1; ++on) {
+        s.xbal_on = (uint32_t)on;
+        const float ms = timeit([&] { CK(launch_decode(d, p, t, dres, ctx->tabs, s, nb, 1, st, cus, nullptr)); }, reps, st);
+        (on ? ton : toff).push_back(ms);
+      }
+    std::sort(ton.begin(), ton.end()); std::sort(toff.begin(), toff.end());
+    XBal xb;
+    CK(hipMemcpy(&xb, s.xbal, sizeof xb, hipMemcpyDeviceToHost));
+    printf("xbal pipeline on: min %.4f median %.4f max %.4f ms | off: min %.4f median %.4f max %.4f ms\n", ton[0], ton[3],
+           ton[6], toff[0], toff[3], toff[6]);
+    printf("xbal weights:");
+    for (int y = 0; y < 8; ++y) printf(" %.3f", xb.w[y] / 65536.0);
+    printf("\n");
+    s.xbal_on = 1;
     return 0;
   }
   if (argc > 4 && std::string(argv[3]) == "seq") {  // N back-to-back pipelines (k_chase + k_crc), per-launch times
@@ -475,7 +515,7 @@ int main(int argc, char** argv) {
   const float as = timeit([&] {
     hipMemsetAsync(&s.misc[M_DONE_CRC], 0, 8, st);  // the last workgroup finalizes
     k_crc<0><<<cus, kCrcThreads, 0, st>>>(d, n, 40, nblocks, s.fbase, s.fok, s.srec, s.frag_cap, ctx->tabs, ea, 0u, 0ull, dres,
-                                          s.misc, 0ull, nblocks, (uint32_t)cus, s.wstart);
+                                          s.misc, 0ull, nblocks, (uint32_t)cus, s.wstart, s.xbal);
   }, reps, st);
   printf("k_crc + finalize %.4f ms\n", as);
   {
@@ -491,7 +531,7 @@ int main(int argc, char** argv) {
         kern<<<(uint32_t)((nblocks + 63) / 64), 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags,
                                                               s.srec, s.frag_cap, s.lb, s.lbe, s.misc, s.epoch,
                                                               ctx->tabs.initc, s.chase_direct, 0ull, s.wstart,
-                                                              (uint32_t)cus * kCrcWaves);
+                                                              (uint32_t)cus * kCrcWaves, s.xbal, s.xbal_on);
         ++s.epoch;
       }, reps, st);
     };
@@ -512,7 +552,7 @@ int main(int argc, char** argv) {
       for (int rep = 0; rep < 3; ++rep) {
         k_chase<32><<<(uint32_t)nwg, 64, 0, st>>>(d, n, 40, nblocks, s.fbase, s.rbase, s.bsum, s.frags, s.srec, s.frag_cap,
                                                   s.lb, stp, s.misc, s.epoch, ctx->tabs.initc, s.chase_direct, 0ull,
-                                                  s.wstart, (uint32_t)cus * kCrcWaves);
+                                                  s.wstart, (uint32_t)cus * kCrcWaves, s.xbal, s.xbal_on);
         ++s.epoch;
         CK(hipStreamSynchronize(st));
       }

@@ -5,6 +5,7 @@
 #   bench   bench.py exactly as the driver runs it (config B, --warmup 5 --steps 20)
 #   kb      tools/kbench default mode on config B and C (pipeline and per-kernel times, k_chase phase stamps)
 #   cmp     tools/kbench k_crc variants (VARIANTS) interleaved, config B and C, in-kernel clock
+#   xbal    tools/kbench pipelines with the per-XCD split on / off (config B and C)
 #   prof    rocprofv3 kernel trace of the driver's bench command + the timed-window summary
 #   pmc     HBM read (TCC_EA0_RDREQ_*) and WRITE_SIZE passes of k_crc (KERNEL) on config B
 # Output under gpurun_out/$TAG/.
@@ -47,6 +48,13 @@ if has cmp; then
     echo "== kbench cmp config $m $(date +%T)"
     KB_CLOCK=1 timeout -k 10 300 tools/kbench/kbench $((1 << 30)) $m cmp $VARIANTS > "$OUT/cmp_$m.log" 2>&1 || { tail -5 "$OUT/cmp_$m.log"; exit 1; }
     grep -E -A1 "k_crc<" "$OUT/cmp_$m.log"
+  done
+fi
+if has xbal; then
+  for m in 0 1; do
+    echo "== kbench xbal config $m $(date +%T)"
+    timeout -k 10 300 tools/kbench/kbench $((1 << 30)) $m xbal > "$OUT/xbal_$m.log" 2>&1 || { tail -5 "$OUT/xbal_$m.log"; exit 1; }
+    grep -E "xbal" "$OUT/xbal_$m.log"
   done
 fi
 if has prof; then
