@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events bracket every N-th k_crc launch of the timed region")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05_k_crc_pmc.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r06", "k_crc_pmc.json"),
                     help="PMC traffic summary (tools/pmc_summary.py over rocprofv3 --pmc passes of this command) to "
                          "report as roofline.traffic; used only when its decode_src_sha16 matches this build's "
                          "decode sources (bitcaskdb_amd/build.py decode_src_sha16)")
