@@ -206,6 +206,8 @@ def _load():
         "bcw_stage_destroy": (C.c_int, [vp]),
         "bcw_stage_read": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint64, vp, vp, C.c_uint32]),
         "bcw_stage_write": (C.c_int, [vp, C.c_int, C.c_uint64, vp, C.c_uint64, vp, C.c_uint32]),
+        "bcw_peer_enable": (C.c_int, [C.c_int, C.c_int]),
+        "bcw_stage_peer": (C.c_int, [vp, vp, vp, C.c_int, C.c_uint64, vp]),
         "bcw_synth_segment": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_int, C.c_uint64, vp, C.c_uint64, u64p, u64p]),
     }

@@ -163,4 +163,33 @@ int bcw_stage_write(bcw_stage* s, int fd, uint64_t file_off, const uint8_t* d_sr
   return err.load();
 }
 
+int bcw_peer_enable(int a, int b) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || a < 0 || b < 0 || a >= n || b >= n) return BCW_E_INVAL;
+  if (a == b) return BCW_OK;
+  for (int k = 0; k < 2; ++k) {
+    const int from = k ? b : a, to = k ? a : b;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, from, to) != hipSuccess || !can) return BCW_E_HIP;
+    DeviceGuard dg(from);
+    if (!dg.ok) return BCW_E_HIP;
+    const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();  // (clears the sticky status)
+    else if (e != hipSuccess) return BCW_E_HIP;
+  }
+  return BCW_OK;
+}
+
+int bcw_stage_peer(bcw_ctx* c, uint8_t* d_dst, const uint8_t* d_src, int src_device, uint64_t len, void* hip_stream) {
+  if (!c || (len && (!d_dst || !d_src)) || src_device < 0) return BCW_E_INVAL;
+  if (!len) return BCW_OK;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return BCW_E_HIP;
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->cur;
+  const hipError_t e = src_device == c->device
+                           ? hipMemcpyAsync(d_dst, d_src, len, hipMemcpyDeviceToDevice, st)
+                           : hipMemcpyPeerAsync(d_dst, c->device, d_src, src_device, len, st);
+  return e == hipSuccess ? BCW_OK : BCW_E_HIP;
+}
+
 }  // extern "C"

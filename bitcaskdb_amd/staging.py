@@ -66,3 +66,20 @@ class Stage:
             self.write(fd, os.fstat(fd).st_size, d_src, length, stream, threads)
         finally:
             os.close(fd)
+
+
+def peer_enable(device_a: int, device_b: int):
+    """bcw_peer_enable: each of the two devices may map the other's memory (xGMI peer access)"""
+    rc = L.lib.bcw_peer_enable(device_a, device_b)
+    if rc != 0:
+        raise OSError(f"bcw_peer_enable({device_a}, {device_b}): {L.lib.bcw_strerror(rc).decode()}")
+
+
+def peer_copy(ctx: Context, d_dst: int, d_src: int, src_device: int, length: int, stream: int | None = None):
+    """bcw_stage_peer: length bytes of a segment resident on src_device -> d_dst on the context's device, device to
+    device (over xGMI between linked GPUs), queued on the context's stream (or `stream`)"""
+    rc = L.lib.bcw_stage_peer(ctx.handle, C.c_void_p(d_dst), C.c_void_p(d_src), src_device, length,
+                              C.c_void_p(stream) if stream else None)
+    if rc != 0:
+        raise OSError(f"bcw_stage_peer: {L.lib.bcw_strerror(rc).decode()}")
+

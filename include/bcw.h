@@ -575,6 +575,15 @@ int bcw_stage_read(bcw_stage* st, int fd, uint64_t file_off, uint64_t len, uint8
 int bcw_stage_write(bcw_stage* st, int fd, uint64_t file_off, const uint8_t* d_src, uint64_t len,
                     void* hip_stream, uint32_t threads);
 
+/* Segments already resident in another GPU's HBM (several GPUs in one process; SURVEY.md north_star: segment buffers
+ * scattered and gathered over xGMI). bcw_peer_enable lets each of the two devices map the other's memory (both
+ * directions; BCW_OK when already enabled or a == b, BCW_E_HIP when the pair cannot). bcw_stage_peer copies len bytes
+ * of d_src, in the HBM of device src_device, to d_dst on the context's device, device to device (over xGMI between
+ * linked MI355Xs once peer access is enabled; never through host memory), queued on hip_stream (NULL: the context's
+ * stream) so that a decode queued after it on that stream sees the bytes. Asynchronous. */
+int bcw_peer_enable(int device_a, int device_b);
+int bcw_stage_peer(bcw_ctx* ctx, uint8_t* d_dst, const uint8_t* d_src, int src_device, uint64_t len, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -105,3 +105,34 @@ def test_file_to_file_compaction(ctx, tmp_path):
     assert ec == 0
     assert (tmp_path / "2.merge").read_bytes() == rd.data()
     assert (tmp_path / "2.tmp").read_bytes() == rh.data()
+
+
+def test_peer_copy_then_decode(ctx):
+    """bcw_stage_peer: a segment resident in another buffer of the GPU (the box has one device: the same-device
+    branch; between two devices it is hipMemcpyPeerAsync over xGMI) copied device to device on the context's
+    stream, then decoded: every column equals the oracle's. bcw_peer_enable of a device with itself is a no-op;
+    out-of-range devices are refused."""
+    import ctypes as C
+    from bitcaskdb_amd.staging import peer_copy, peer_enable
+    data = O.synth(8 << 20, 0, 77, value_mode=1)
+    src = D.DevBuf(len(data))
+    src.upload(np.frombuffer(data, np.uint8))
+    dst = D.DevBuf(len(data) + 64)
+    peer_enable(0, 0)
+    with pytest.raises(OSError):
+        peer_enable(0, 1 << 20)
+    peer_copy(ctx, dst.ptr + 16, src.ptr, 0, len(data))
+    ctx.sync()
+    assert bytes(dst.download(len(data), 16)) == data
+    n_rows = len(data) // 64 + 64
+    tab = D.DevTable(n_rows)
+    d_res = D.DevBuf(C.sizeof(L.DecodeResult))
+    dp = L.DecodeParams(len(data), BASE, 40, 20, 20, L.MODE_RECORD)
+    assert L.lib.bcw_decode_segment_async(ctx.handle, C.c_void_p(dst.ptr + 16), C.byref(dp), C.byref(tab.t),
+                                          d_res.vp()) == 0
+    ctx.sync()
+    r = L.DecodeResult.from_buffer_copy(bytes(d_res.download()))
+    ref = O.decode(data, 40, BASE, 20, 20, want_bytes=False)
+    assert r.err_class == ref.err_class == 0 and r.n_records == len(ref.recs)
+    np.testing.assert_array_equal(tab.column("foff", r.n_records), ref.recs["foff"])
+    np.testing.assert_array_equal(tab.column("size", r.n_records), ref.recs["size"])
