@@ -492,16 +492,18 @@ __global__ __launch_bounds__(64) void k_chase(const uint8_t* __restrict__ seg, u
     // (positions after start_off), so wstart[w] = the first fragment whose header is at or after P_w. This lane writes the boundaries that fall in its block, walking its headers in order.
     // (Whole blocks per wave left 7 of config B's 4096 waves with 9 blocks instead of 8: they ended ~20 us after the
     // median wave, kbench timelines.)
-    // Range r (k_crc's workgroup with ticket r / 8 of XCD r % 8) has weight s_w[r % 8]; wave v = 16 r + j starts at
-    // the fraction (16 x (weights of ranges < r) + s_w[r % 8] j) / (16 x all weights) of the bytes after start_off.
+    // Range r (k_crc's workgroup r, class r % 8) has its class's weight (WavePart). This lane writes the boundaries
+    // that lie in its block: from the first at or after its start while they lie before its end (the segment's last
+    // block: every one left, up to P_nwaves = L, which lies at its span's end when L is a multiple of 32 KiB). (A
+    // second first_at for the block's end cost ~1 us of k_chase's table pass.)
     const uint64_t L = seg_len - start_off, rel = boff - start_off;
     const WavePart wp(class_weights(xw), L, nwaves);
+    const uint64_t span = b + 1 == nblocks ? ~0ull : (uint64_t)kBlock - 1;  // the last position it owns
     uint64_t w = wp.first_at(rel);
-    // (the last block also takes P_nwaves = L, which lies at its span's end when L is a multiple of 32 KiB)
-    const uint64_t w_end = b + 1 == nblocks ? (uint64_t)nwaves + 1 : wp.first_at(rel + kBlock);
-    uint64_t bw = w < w_end ? wp.P(w) - rel : 0;  // boundary w, block-relative
+    uint64_t bw = wp.P(w) - rel;  // boundary w, block-relative
     auto bounds_upto = [&](uint64_t hp, uint64_t idx) __attribute__((always_inline)) {  // boundaries at or before hp: idx
-      while (w < w_end && bw <= hp) {
+      const uint64_t h = hp < span ? hp : span;
+      while (w <= nwaves && bw <= h) {
         wstart[w] = (uint32_t)(idx < 0xffffffffull ? idx : 0xffffffffull);
         ++w;
         bw = wp.P(w) - rel;
