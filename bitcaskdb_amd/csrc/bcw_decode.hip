@@ -1296,9 +1296,9 @@ struct CrcTail {
 };
 
 // The next decode's split (XBal), by the last wave of k_crc: every workgroup's stream times are in (the completion
-// counter orders them). Class y's mean stream time T_y against the mean over the classes T: its range weight moves a
-// quarter of the way to w_y T / T_y (kept within 0.8-1.25 of equal), when k_chase used the weights. The times are
-// reset for the next launch.
+// counter orders them). Class y's mean stream time T_y against the mean over the classes T: its range weight moves
+// half way to w_y T / T_y (kept within 0.8-1.25 of equal), when k_chase used the weights: a fresh context converges
+// within the driver's warmup decodes. The times are reset for the next launch.
 __device__ __forceinline__ void xbal_update(XBal* __restrict__ xb, uint32_t lane) {
   const uint32_t y = lane & 7u;
   const uint64_t t = __hip_atomic_load(&xb->t[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1310,7 +1310,7 @@ __device__ __forceinline__ void xbal_update(XBal* __restrict__ xb, uint32_t lane
   for (int d = 32; d >= 1; d >>= 1) sT += __shfl_xor(sT, d, 64);
   if (lane < 8u) {
     if (all) {
-      const float wy = (float)xb->w[y] * (1.0f + 0.25f * ((sT / 8.0f) / Ty - 1.0f));
+      const float wy = (float)xb->w[y] * (1.0f + 0.5f * ((sT / 8.0f) / Ty - 1.0f));
       const float d = fminf(fmaxf(rintf((wy - 65536.0f) / 256.0f), -51.0f), 64.0f);  // (k_chase's ClassW: 256 steps)
       xb->w[y] = (uint32_t)(65536 + 256 * (int32_t)d);
     }
