@@ -154,3 +154,23 @@ def test_stream_verify_geometry_corrupt(ctx_path, where):
         bad = bytearray(data)
         bad[pos] ^= 0x41
         assert_parity(ctx_path, bytes(bad), cases.params(), f"corrupt {where} frag {f}")
+
+
+@pytest.mark.parametrize("size,mode", [(48 << 20, 0), (24 << 20, 1), (300 << 10, 0), (5000, 0)])
+def test_xcd_balance_split_changes_no_result(size, mode):
+    """the per-XCD split of k_crc's stream (XBal, BCW_OPT_XCD_BALANCE): six decodes in a row with the weights adapting
+    after each, then with equal bytes per workgroup, then again with the weights -- every decode bit-exact against the
+    oracle (sizes from a few hundred boundaries per block to several blocks per wave); other values are refused"""
+    from bitcaskdb_amd import Context
+    from bitcaskdb_amd import _lib as L
+    seg = O.synth(size, 0, 5 + size % 97, value_mode=mode) if size > 10000 else cases.wal_of(
+        [cases.rec(i, vlen=100 + i) for i in range(30)])[0]
+    c = Context(0)
+    try:
+        for on in (1, 1, 1, 1, 1, 1, 0, 1):
+            c.set_option(L.OPT_XCD_BALANCE, on)
+            assert_parity(c, seg, cases.params(), f"xbal={on} size={size}")
+        with pytest.raises(ValueError):
+            c.set_option(L.OPT_XCD_BALANCE, 3)
+    finally:
+        c.close()
