@@ -1299,18 +1299,31 @@ struct CrcTail {
 // counter orders them). Class y's mean stream time T_y against the mean over the classes T: its range weight moves
 // half way to w_y T / T_y (kept within 0.8-1.25 of equal), when k_chase used the weights: a fresh context converges
 // within the driver's warmup decodes. The times are reset for the next launch.
-__device__ __forceinline__ void xbal_update(XBal* __restrict__ xb, uint32_t lane) {
+struct XBalIn {  // class y = lane % 8: its summed stream times, their count, its weight; whether k_chase used them
+  uint64_t t, n;
+  uint32_t w, on;
+};
+// (requested before the finalize's loads, so that the two round trips overlap)
+__device__ __forceinline__ XBalIn xbal_load(const XBal* __restrict__ xb, uint32_t lane) {
   const uint32_t y = lane & 7u;
-  const uint64_t t = __hip_atomic_load(&xb->t[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t n = __hip_atomic_load(&xb->n[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  XBalIn v;
+  v.t = __hip_atomic_load(&xb->t[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v.n = __hip_atomic_load(&xb->n[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v.w = xb->w[y];
+  v.on = xb->on;
+  return v;
+}
+__device__ __forceinline__ void xbal_update(XBal* __restrict__ xb, uint32_t lane, const XBalIn& in) {
+  const uint32_t y = lane & 7u;
+  const uint64_t t = in.t, n = in.n;
   const float Ty = n && t ? (float)t / (float)n : 0.0f;
-  const bool all = __ballot(lane < 8u && Ty > 0.0f) == 0xffull && xb->on != 0u;  // every XCD measured
+  const bool all = __ballot(lane < 8u && Ty > 0.0f) == 0xffull && in.on != 0u;  // every XCD measured
   float sT = lane < 8u ? Ty : 0.0f;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) sT += __shfl_xor(sT, d, 64);
   if (lane < 8u) {
     if (all) {
-      const float wy = (float)xb->w[y] * (1.0f + 0.5f * ((sT / 8.0f) / Ty - 1.0f));
+      const float wy = (float)in.w * (1.0f + 0.5f * ((sT / 8.0f) / Ty - 1.0f));
       const float d = fminf(fmaxf(rintf((wy - 65536.0f) / 256.0f), -51.0f), 64.0f);  // (k_chase's ClassW: 256 steps)
       xb->w[y] = (uint32_t)(65536 + 256 * (int32_t)d);
     }
@@ -1364,20 +1377,41 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
     s_t0 = wall_clock64();
     s_tail = CrcTail{ea, res, misc, nblocks, frag_cap, gen, cb0, cb1, tail_panic, nwg_total};
   }
-  {  // table image -> LDS: all 16 B loads in flight before the first store
-    constexpr uint32_t kVec = kS2Image / 4;
-    constexpr int kFull = (int)(kVec / kCrcThreads);
-    const uint4* src = reinterpret_cast<const uint4*>(tabs.lds_image2);
-    uint4* dst = reinterpret_cast<uint4*>(lds);
-    uint4 v[kFull];
+  {  // table image -> LDS, all loads in flight before the first store. The slice rows hold every table dword 8 times
+     // (the bank-conflict-free copies, kS2Image): their 8 KiB of distinct dwords are read and replicated here, the
+     // rest copied as it is -- 57 of the image's 113 KiB read per workgroup
+    const uint4* src4 = reinterpret_cast<const uint4*>(tabs.lds_image2);
+    uint4* dst4 = reinterpret_cast<uint4*>(lds);
+    constexpr uint32_t kLop4 = kS2SliceOff / 4, kKop4 = kS2KopOff / 4, kEnd4 = kS2Image / 4;
+    constexpr uint32_t kN4 = kLop4 + (kEnd4 - kKop4);  // uint4s copied as they are
+    constexpr int kPer = (int)((kN4 + kCrcThreads - 1) / kCrcThreads);
+    static_assert(kS2Slice == 256 * 64 && kCrcThreads * 2 == 256 * 8, "slice rows: 256 x 8 distinct dwords");
+    auto at = [](uint32_t i) { return i < kLop4 ? i : i - kLop4 + kKop4; };
+    uint4 v[kPer];
 #pragma unroll
-    for (int k2 = 0; k2 < kFull; ++k2) v[k2] = src[tid + k2 * kCrcThreads];
-    const uint32_t tail = tid + kFull * kCrcThreads;
-    uint4 vt = make_uint4(0, 0, 0, 0);
-    if (tail < kVec) vt = src[tail];
-    if (tail < kVec) dst[tail] = vt;
+    for (int k2 = 0; k2 < kPer; ++k2) {
+      const uint32_t i = tid + k2 * kCrcThreads;
+      v[k2] = i < kN4 ? src4[at(i)] : make_uint4(0, 0, 0, 0);
+    }
+    const uint32_t* src1 = tabs.lds_image2 + kS2SliceOff;
+    uint32_t sv[2];
 #pragma unroll
-    for (int k2 = 0; k2 < kFull; ++k2) dst[tid + k2 * kCrcThreads] = v[k2];
+    for (int k2 = 0; k2 < 2; ++k2) {  // row e = t / 8, distinct dword t % 8 (its 8 copies are consecutive)
+      const uint32_t t = tid + k2 * kCrcThreads;
+      sv[k2] = src1[(t >> 3) * 64u + (t & 7u) * 8u];
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < kPer; ++k2) {
+      const uint32_t i = tid + k2 * kCrcThreads;
+      if (i < kN4) dst4[at(i)] = v[k2];
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const uint32_t t = tid + k2 * kCrcThreads;
+      uint4* d = reinterpret_cast<uint4*>(lds + kS2SliceOff + (t >> 3) * 64u + (t & 7u) * 8u);
+      d[0] = make_uint4(sv[k2], sv[k2], sv[k2], sv[k2]);
+      d[1] = make_uint4(sv[k2], sv[k2], sv[k2], sv[k2]);
+    }
   }
   __syncthreads();
   // every wave streams the fragments of its share of the segment's bytes: 1 / (16 x CUs), weighted by its
@@ -1513,8 +1547,9 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
   gorder = (uint64_t)__shfl((long long)gorder, 0, 64);
   if (gorder != T.nwg_total - 1u) return;
   if (lane == 0) T.misc[M_T_FIN] = wall_clock64();
+  const XBalIn xin = xbal_load(xb, lane);
   finalize(A, T.nblocks, T.frag_cap, T.tail_panic, T.gen, T.res, lane);
-  xbal_update(xb, lane);
+  xbal_update(xb, lane, xin);
 }
 
 __global__ void k_export_frags(const Frag* __restrict__ frags, const uint8_t* __restrict__ fok,
