@@ -648,13 +648,14 @@ struct RegReader {
   uint32_t t[kTailWords];
   uint32_t nhead;        // head: record bytes held
   uint64_t tstart;       // first record byte held by the tail (>= size when none)
+  uint64_t tend;         // and the byte after its last
   const uint8_t* seg;
   const Frag* frags;
   uint32_t start_off;
   uint32_t f_first, f_last;
   __device__ __forceinline__ uint32_t operator()(uint64_t pos) {
     if (pos < nhead) return reg_byte(h, (uint32_t)pos);
-    if (pos >= tstart) return reg_byte(t, (uint32_t)(pos - tstart));
+    if (pos >= tstart && pos < tend) return reg_byte(t, (uint32_t)(pos - tstart));
     return walk_byte(seg, frags, start_off, f_first, f_last, pos);
   }
 };
@@ -746,7 +747,7 @@ __device__ __forceinline__ EmitState emit_state(const EmitArgs& A, uint64_t b0, 
 // hook(): called once, right after the first chunk's fragment descriptors are requested (the caller issues the
 // next work item's loads there, so they fly beside this item's).
 // NOSTORE (tools/kbench only): the rows are computed but not stored
-template <bool NOSTORE = false, typename Hook>
+template <bool NOSTORE = false, bool NOPARSE = false, typename Hook>
 __device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& es, uint64_t f0, uint64_t f1,
                                             uint32_t lane, Hook&& hook) {
   if (f0 >= f1) {
@@ -823,6 +824,11 @@ __device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& 
     const uint32_t sw0 = (uint32_t)__shfl((int)f.blk, src_here ? (int)(src - c0) : (int)lane, 64);
     const uint32_t sw1 = (uint32_t)__shfl((int)((uint32_t)f.start | ((uint32_t)f.len << 16)),
                                           src_here ? (int)(src - c0) : (int)lane, 64);
+    // the fragment after src (a record head that runs past its first fragment continues there)
+    const bool nx_here = src + 1u >= c0 && src + 1u < c0 + 64;
+    const uint32_t sx0 = (uint32_t)__shfl((int)f.blk, nx_here ? (int)(src + 1u - c0) : (int)lane, 64);
+    const uint32_t sx1 = (uint32_t)__shfl((int)((uint32_t)f.start | ((uint32_t)f.len << 16)),
+                                          nx_here ? (int)(src + 1u - c0) : (int)lane, 64);
     if (isE) {
       const uint64_t size = full ? (uint64_t)len : acc_before + len;
       const uint64_t r = rec + __builtin_popcountll(E & below);
@@ -837,12 +843,24 @@ __device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& 
       if (want > fs.len) want = fs.len;
       rd.nhead = (uint32_t)want;
       load_words(A.seg, A.seg_len, a0, rd.h);
-      rd.tstart = ~0ull;
+      rd.tstart = rd.tend = ~0ull;
       if (hint) {  // the last bytes: HintRecord.Decode reads fid, offset and size after the key
         uint64_t nt = size < 32u ? size : 32u;
         if (nt > len) nt = len;
         rd.tstart = size - nt;
         load_words(A.seg, A.seg_len, D + len - nt, rd.t);  // this lane's (Full/Last) fragment ends the record
+      } else if (want < (size < 64u ? size : 64u)) {
+        // RecordFromBytes reads past the first fragment (a record that starts in the last bytes of a block): the next
+        // fragment's first 32 B, loaded beside the head, instead of a fragment walk per byte (two dependent loads
+        // each: one such record held its whole work item ~20 us)
+        Frag f2;
+        if (nx_here) { f2.blk = sx0; f2.start = (uint16_t)sx1; f2.len = (uint16_t)(sx1 >> 16); }
+        else f2 = frags[src + 1u];
+        load_words(A.seg, A.seg_len, (uint64_t)start_off + (uint64_t)f2.blk * kBlock + f2.start, rd.t);
+        uint64_t n2 = f2.len < 32u ? f2.len : 32u;
+        if (n2 > size - want) n2 = size - want;
+        rd.tstart = want;
+        rd.tend = want + n2;
       } else {
 #pragma unroll
         for (int k = 0; k < kTailWords; ++k) rd.t[k] = 0;
@@ -851,7 +869,13 @@ __device__ __forceinline__ void emit_chunks(const EmitArgs& A, const EmitState& 
       rd.f_first = src; rd.f_last = (uint32_t)g;
       uint8_t status, hdr, flags, etag_off;
       uint64_t key_len, val_len, meta_len, expire, aux0, aux1;
-      parse_record(A.p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
+      if (NOPARSE) {  // (kbench: the head's words folded instead of parsed)
+        status = 0; hdr = (uint8_t)rd.h[0]; flags = (uint8_t)rd.h[5]; etag_off = 0;
+        key_len = rd.h[6] ^ rd.h[9]; val_len = rd.h[7] ^ rd.h[12]; meta_len = rd.h[8] ^ rd.h[15]; expire = rd.h[10];
+        aux0 = rd.t[0]; aux1 = rd.t[1];
+      } else {
+        parse_record(A.p, rd, size, status, hdr, flags, etag_off, key_len, val_len, meta_len, expire, aux0, aux1);
+      }
       const bcw_record_table& tab = A.tab;
       if (NOSTORE) {
         if (status == 0xeeu) tab.foff[r] = foff ^ size ^ expire ^ aux0 ^ aux1 ^ key_len ^ val_len ^ meta_len ^ hdr ^ flags ^ etag_off;
@@ -1477,7 +1501,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc(const uint8_t* __restrict__
       const uint64_t mf1 = m.f1 < fcap ? m.f1 : fcap;
       uint64_t nx = ~0ull;
       ItemMeta mn = m;
-      emit_chunks<(ABL & 4096) != 0>(A, es, m.f0, mf1, lane, [&]() {
+      emit_chunks<(ABL & 4096) != 0, (ABL & 131072) != 0>(A, es, m.f0, mf1, lane, [&]() {
         if (taken < max_items) {
           nx = deq();
           mn = item_meta(A, nx, bpw, cb0t, cb1t, lane);

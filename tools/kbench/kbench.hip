@@ -343,6 +343,8 @@ int main(int argc, char** argv) {
       case 8388616: return run(k_crc<8388616>, cus, ea);  // the same without emission
       case 32768: return run(k_crc<32768>, cus, ea);      // emission only (no CRC pass)
       case 4096: return run(k_crc<4096>, cus, ea);        // emission without row stores
+      case 131072: return run(k_crc<131072>, cus, ea);    // emission without the RecordFromBytes parse
+      case 163840: return run(k_crc<163840>, cus, ea);    // emission only, without the parse
       case 16384: return run(k_crc<16384>, cus, ea);      // each wave's range as 4 stream_verify calls
       case 16392: return run(k_crc<16392>, cus, ea);      // the same without emission
       case 36864: return run(k_crc<36864>, cus, ea);      // emission only, without row stores
