@@ -364,11 +364,14 @@ def main():
     ptr_t = {"u8": L.u64p, "u4": L.u32p, "u1": L.u8p}
 
     def make_table(cap):
+        # a record-mode table: aux0 / aux1 are hint-mode columns and stay NULL (bcw.h), as a record-mode caller passes them
         cols = {}
         for name, dt in L.TABLE_COLUMNS:
+            if name in ("aux0", "aux1"):
+                continue
             tdt = {"u8": torch.int64, "u4": torch.int32, "u1": torch.uint8}[dt]
             cols[name] = torch.empty(cap, dtype=tdt, device=dev)
-        return L.RecordTable(cap, *[C.cast(C.c_void_p(cols[name].data_ptr()), ptr_t[dt])
+        return L.RecordTable(cap, *[C.cast(C.c_void_p(cols[name].data_ptr()), ptr_t[dt]) if name in cols else None
                                     for name, dt in L.TABLE_COLUMNS]), cols
     slots = []
     for j in range(nslot):
